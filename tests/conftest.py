@@ -1,0 +1,14 @@
+"""Shared pytest setup: import paths and the ``gpu`` marker."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "transformer-stm_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
