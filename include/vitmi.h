@@ -1,0 +1,152 @@
+/*
+ * vitmi.h — C ABI of libvitmi.so, the MI355X (gfx950 / CDNA4) ViT training path.
+ *
+ * Drop-in boundary.  The reference's hot path is the forward + autodiff backward
+ * of its transformer stage, dispatched by Keras to TensorFlow GPU library ops
+ * (SURVEY.md §2 op table).  Each entry point below replaces one such library op
+ * at its call site in the reference; the Python layer (vitmi/ops.py, vitmi/modules.py)
+ * mirrors the reference's layer API and calls these through ctypes.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers owned by the caller (the PyTorch caching
+ *     allocator).  No entry point allocates, frees or synchronises the host.
+ *   - Every call is stream-ordered on `stream` (a hipStream_t) and re-entrant.
+ *   - Matrices are row-major with an explicit leading dimension in ELEMENTS.
+ *   - Accumulating outputs (parameter gradients) are fp32 and updated with +=,
+ *     the semantics of torch's .grad accumulation.
+ *   - Return 0 on success, otherwise a VITMI_ERR_* code; vitmi_last_error()
+ *     returns a thread-local message.  Shapes are validated on the host before
+ *     any launch; there is no silent fallback path.
+ */
+#ifndef VITMI_H
+#define VITMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vitmi_stream_t; /* hipStream_t */
+
+enum { VITMI_OK = 0, VITMI_ERR_INVALID = 1, VITMI_ERR_HIP = 2, VITMI_ERR_UNSUPPORTED = 3 };
+enum { VITMI_F32 = 0, VITMI_BF16 = 1 };
+
+/* GEMM epilogues (all apply `bias` (fp32, may be NULL) first where it applies) */
+enum {
+  VITMI_EPI_STORE = 0,     /* C = acc + bias                                        */
+  VITMI_EPI_BIAS_GELU = 1, /* aux = acc + bias (pre-activation), C = gelu(aux)       */
+  VITMI_EPI_RESIDUAL = 2,  /* C(f32) = residual(f32) + acc + bias                    */
+  VITMI_EPI_DGELU = 3,     /* C = acc * gelu'(aux)                                  */
+  VITMI_EPI_ACCUM = 4      /* C(f32) += acc                                          */
+};
+
+enum { VITMI_LOSS_CE = 0, VITMI_LOSS_MSE = 1 };
+
+int vitmi_version(void);
+const char* vitmi_last_error(void);
+/* number of hipDevice compute units seen by the library (0 on error) */
+int vitmi_device_cus(void);
+
+/* ---------------------------------------------------------------------------
+ * Generic MFMA GEMM:  C[M,N] (op)= sum_k A(m,k) * B(k,n)
+ *   a_kmajor=1: A stored [M][lda] (k contiguous);  0: A stored [K][lda] (m contiguous)
+ *   b_kmajor=1: B stored [N][ldb] (k contiguous);  0: B stored [K][ldb] (n contiguous)
+ *   dtype: operand type (VITMI_BF16 -> v_mfma_f32_16x16x32_bf16, VITMI_F32 -> v_mfma_f32_16x16x4_f32)
+ *   c_dtype: output type; aux (epilogue GELU pre-activation) has the operand dtype.
+ *   k-major operands need K % 64 == 0 (bf16) / K % 32 == 0 (f32); ragged M/N and a
+ *   ragged reduction over m-major operands are zero-filled by the buffer range check.
+ * Replaces the reference's Dense/EinsumDense MatMul and their autodiff transposes
+ * (models/CvT(Par).py:132-134,137,142,188,254,256).
+ */
+int vitmi_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+               const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+               int c_dtype, int epilogue, const float* bias, void* aux, int64_t ldaux,
+               const float* residual, int64_t ldr, void* workspace, size_t ws_bytes,
+               vitmi_stream_t stream);
+size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N,
+                                 int64_t K, int epilogue);
+
+/* Linear layer y = x W^T + b  (keras layers.Dense, models/CvT(Par).py:132-134,142,254,256;
+ * torch nn.Linear in old_codes/MS_CvT.py:63-65,116-121).  x [M,K], W [N,K] -> y [M,N]. */
+int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, const void* x, const void* w,
+                     const float* bias, void* y, int y_dtype, int epilogue, void* aux,
+                     const float* residual, vitmi_stream_t stream);
+/* dx[M,K] = dy[M,N] W[N,K]   (epilogue STORE or DGELU with aux = pre-activation [M,K]) */
+int vitmi_linear_dgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* w,
+                       void* dx, int dx_dtype, int epilogue, const void* aux,
+                       vitmi_stream_t stream);
+/* dW[N,K] (f32) += dy[M,N]^T x[M,K]; uses split-K over M with fp32 partial slabs */
+int vitmi_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* x,
+                       float* dw, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
+/* db[N] (f32) += sum_m dy[m, n]  (dy [M][ldy] of `dtype`) */
+int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, int64_t ldy, float* db,
+                    void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+size_t vitmi_bias_grad_workspace_size(int64_t M, int64_t N);
+
+/* ---------------------------------------------------------------------------
+ * LayerNorm over the last dim D (layers.LayerNormalization, models/CvT(Par).py:248,328;
+ * old_codes/MS_CvT.py:39-45).  x is fp32 [M][ldx]; y [M][ldy] of y_dtype; mean/rstd fp32 [M].
+ */
+int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const float* gamma,
+                        const float* beta, float eps, void* y, int y_dtype, int64_t ldy,
+                        float* mean, float* rstd, vitmi_stream_t stream);
+/* dx = dres + LN'(dy); optional low-precision copy dx_lp (bf16); dgamma/dbeta += (fp32). */
+int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtype, int64_t lddy,
+                        const float* x, int64_t ldx, const float* mean, const float* rstd,
+                        const float* gamma, const float* dres, int64_t ldres, float* dx,
+                        int64_t lddx, void* dx_lp, int64_t lddx_lp, float* dgamma, float* dbeta,
+                        void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D);
+
+/* ---------------------------------------------------------------------------
+ * Multi-head scaled-dot-product attention (layers.MultiHeadAttention called (q, v, k),
+ * models/CvT(Par).py:137,185; einsum-softmax-einsum old_codes/MS_CvT.py:202-207).
+ * qkv: [B*N][3*H*dh] token-major (q | k | v column blocks, head h at h*dh); o: [B*N][H*dh];
+ * lse: fp32 [B*H][N] (natural-log softmax normaliser per query, saved for backward).
+ * dh must be 64.  dtype selects bf16 MFMA (VITMI_BF16) or fp32 (VITMI_F32) kernels.
+ */
+int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float scale, const void* qkv,
+                        void* o, float* lse, vitmi_stream_t stream);
+int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, const void* qkv,
+                        const void* o, const void* dout, const float* lse, void* dqkv,
+                        void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+size_t vitmi_attention_bwd_workspace_size(int B, int N, int H);
+
+/* ---------------------------------------------------------------------------
+ * Patch embedding Conv2D(k=P, s=P) as a GEMM (models/CvT(Par).py:203-212;
+ * old_codes/MS_CvT.py:352-361): im2col of the fp32 NCHW images into
+ * patches [B*(S/P)^2][C*P*P] of `dtype` (column order c, kh, kw = the conv weight's).
+ */
+int vitmi_patch_im2col(int dtype, int B, int C, int S, int P, const float* img, void* patches,
+                       vitmi_stream_t stream);
+/* x[b][0] = cls + pos[0];  x[b][1+p] = tok[b*np+p] + pos[1+p]   (cls/pos may be NULL) */
+int vitmi_tokens_assemble(int B, int np, int D, const float* tok, const float* cls,
+                          const float* pos, float* x, vitmi_stream_t stream);
+/* backward of assemble: dtok (f32, and optional bf16 copy) = dx[:,1:];  dpos += sum_b dx,
+ * dcls += sum_b dx[:,0]   (NULL pointers skip that output) */
+int vitmi_tokens_assemble_bwd(int B, int np, int D, const float* dx, float* dtok, void* dtok_lp,
+                              float* dcls, float* dpos, vitmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Head (layers.Dense(num_classes) on LN(cls), models/CvT(Par).py:326-329,350) and loss
+ * (compile(loss='mean_squared_error') :464-466; softmax-CE for >=2 classes).
+ * y: fp32 [B][ldy]; W fp32 [C][D].
+ */
+int vitmi_head_fwd(int B, int D, int C, const float* y, int64_t ldy, const float* w,
+                   const float* b, float* logits, vitmi_stream_t stream);
+int vitmi_head_bwd(int B, int D, int C, const float* dlogits, const float* y, int64_t ldy,
+                   const float* w, float* dy, float* dw, float* db, vitmi_stream_t stream);
+/* loss = mean over batch; dlogits = d loss / d logits.  target: int64 [B] (CE) or f32 [B] (MSE) */
+int vitmi_loss_fwd_bwd(int kind, int B, int C, const float* logits, const void* target,
+                       float* loss, float* dlogits, vitmi_stream_t stream);
+
+/* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
+int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VITMI_H */

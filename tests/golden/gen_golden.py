@@ -106,7 +106,7 @@ def save(path, img, tgt, params, logits, loss, grads):
 
 def gen_mscvt():
     ms = load_mscvt()
-    D, H, depth, P, img_size = 64, 4, 2, 8, 32
+    D, H, depth, P, img_size = 128, 2, 2, 8, 32
     spec = {
         "NUM_STAGES": 1, "PATCH_SIZE": [P], "PATCH_STRIDE": [P], "PATCH_PADDING": [0],
         "DIM_EMBED": [D], "DEPTH": [depth], "NUM_HEADS": [H], "MLP_RATIO": [4.0],
@@ -145,7 +145,7 @@ def gen_mscvt():
 
 def gen_hf():
     from transformers import ViTConfig as HFConfig, ViTForImageClassification
-    D, H, depth, P, img_size = 64, 4, 2, 8, 32
+    D, H, depth, P, img_size = 128, 2, 2, 8, 32
     cfg = HFConfig(image_size=img_size, patch_size=P, num_channels=3, hidden_size=D,
                    num_hidden_layers=depth, num_attention_heads=H, intermediate_size=4 * D,
                    hidden_act="gelu", layer_norm_eps=1e-6, qkv_bias=True, num_labels=2,

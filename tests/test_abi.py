@@ -1,0 +1,57 @@
+"""CPU-side checks of the C-ABI boundary: the library loads (no GPU needed) and
+exports exactly the entry points include/vitmi.h declares; host validation
+rejects bad shapes before any launch."""
+import os
+import re
+
+import pytest
+
+from vitmi import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vitmi.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vitmi_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_loader_table():
+    assert header_functions() == sorted(_lib.exported_symbols())
+
+
+def test_library_exports_every_symbol():
+    lib = _lib.lib()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert lib.vitmi_version() >= 100
+
+
+def test_host_validation_rejects_bad_shapes():
+    lib = _lib.lib()
+    # k-major operand with K % 64 != 0 (bf16) must fail before any launch
+    rc = lib.vitmi_gemm(1, 1, 1, 128, 128, 100, 16, 128, 16, 128, 16, 128, 1, 0, None, None, 0, None, 0,
+                        None, 0, None)
+    assert rc == 1
+    assert b"K %" in lib.vitmi_last_error() or b"K " in lib.vitmi_last_error()
+    # attention head dim must be 64
+    rc = lib.vitmi_attention_fwd(1, 1, 10, 2, 32, 1.0, 16, 16, 16, None)
+    assert rc == 1 and b"64" in lib.vitmi_last_error()
+    # layernorm D must be a multiple of 4
+    rc = lib.vitmi_layernorm_fwd(4, 30, 16, 30, 16, 16, 1e-6, 16, 0, 30, 16, 16, None)
+    assert rc == 1
+
+
+def test_workspace_queries_are_pure_host():
+    lib = _lib.lib()
+    assert lib.vitmi_attention_bwd_workspace_size(2, 197, 12) == 2 * 197 * 12 * 4
+    assert lib.vitmi_linear_wgrad_workspace_size(1, 50432, 768, 768) > 0
+    assert lib.vitmi_bias_grad_workspace_size(50432, 768) > 0
+
+
+@pytest.mark.parametrize("name", ["vitmi_gemm", "vitmi_attention_fwd", "vitmi_layernorm_bwd"])
+def test_argtypes_declared(name):
+    fn = getattr(_lib.lib(), name)
+    assert fn.argtypes is not None and len(fn.argtypes) > 5

@@ -1,0 +1,139 @@
+"""End-to-end parity of the MI355X ViT path against the CPU oracle (oracle/vit_ref.py)
+and against the golden vectors of the reference's own MS_CvT module / HF ViT.
+
+Tolerances:  fp32: logits max-abs <= 1e-3 (north star; we assert
+1e-4), loss rel <= 1e-5, every grad ||d||/||g|| <= 1e-3.  bf16: grads <= 2e-2; logits
+max-abs measured and asserted against a bf16-appropriate bound (stated per test)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import vit_ref  # noqa: E402
+from vitmi.config import ViTConfig, config_c1, config_c2, preset  # noqa: E402
+from vitmi.modules import VisionTransformer, cross_entropy, mse_loss  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gpu_step(cfg, params, img, tgt):
+    model = VisionTransformer(cfg).cuda()
+    model.load_param_dict(params)
+    logits = model(img.cuda())
+    loss = cross_entropy(logits, tgt.cuda()) if cfg.num_classes > 1 else mse_loss(logits, tgt.cuda())
+    loss.backward()
+    grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()}
+    return logits.detach().cpu(), loss.detach().cpu(), grads
+
+
+def compare(cfg, params, img, tgt, logit_tol, grad_tol, loss_tol=1e-5):
+    l_ref, loss_ref, g_ref = vit_ref.forward_backward(img, tgt, params, cfg)
+    l, loss, g = gpu_step(cfg, params, img, tgt)
+    err = (l - l_ref).abs().max().item()
+    assert err <= logit_tol, f"logits max-abs {err:.3e} > {logit_tol}"
+    assert abs(loss.item() - loss_ref.item()) <= loss_tol * max(1.0, abs(loss_ref.item())), (loss, loss_ref)
+    worst = max((vit_ref.rel_err(g[k], g_ref[k]), k) for k in g_ref)
+    assert worst[0] <= grad_tol, f"grad {worst[1]} rel {worst[0]:.3e}"
+    return err, worst
+
+
+def test_c1_fp32_matches_oracle():
+    cfg = config_c1()                           # ViT-Ti/16 64x64 bs8 (BASELINE config 1)
+    params = vit_ref.init_params(cfg, seed=0)
+    img, tgt = vit_ref.synthetic_batch(cfg, 8)
+    compare(cfg, params, img, tgt, logit_tol=1e-4, grad_tol=1e-4)
+
+
+def test_c1_bf16_matches_oracle():
+    cfg = config_c1(dtype="bf16")
+    params = vit_ref.init_params(cfg, seed=0)
+    img, tgt = vit_ref.synthetic_batch(cfg, 8)
+    compare(cfg, params, img, tgt, logit_tol=5e-2, grad_tol=2e-2, loss_tol=2e-2)
+
+
+@pytest.mark.parametrize("variant", [dict(tie_norms=True), dict(qkv_bias=False, attn_scale="dim"),
+                                     dict(num_classes=1), dict(embed_norm=True, pos_embed=False)])
+def test_knob_variants_fp32(variant):
+    cfg = ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2, num_classes=2,
+                    dtype="fp32").replace(**variant)
+    params = vit_ref.init_params(cfg, seed=1)
+    img, tgt = vit_ref.synthetic_batch(cfg, 5, seed=7)
+    compare(cfg, params, img, tgt, logit_tol=1e-4, grad_tol=1e-4)
+
+
+def _golden(name):
+    z = np.load(os.path.join(GOLD, name))
+    params = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p::")}
+    grads = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("g::")}
+    return z, params, grads
+
+
+@pytest.mark.parametrize("name,cfg", [
+    ("mscvt_vit_stage.npz", ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2,
+                                      num_classes=2, attn_scale="dim", ln_eps=1e-5, qkv_bias=False,
+                                      embed_norm=True, pos_embed=False, dtype="fp32")),
+    ("hf_vit.npz", ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2, num_classes=2,
+                             attn_scale="head", ln_eps=1e-6, qkv_bias=True, dtype="fp32")),
+])
+def test_gpu_matches_reference_goldens(name, cfg):
+    """Replay the golden vectors of the reference's own MS_CvT module and of the offline HF
+    ViT (tests/golden/gen_golden.py) through the HIP path: logits, loss and every gradient."""
+    z, params, grads = _golden(name)
+    img, tgt = torch.from_numpy(z["input"]), torch.from_numpy(z["target"])
+    l, loss, g = gpu_step(cfg, params, img, tgt)
+    assert np.abs(l.numpy() - z["logits"]).max() <= 1e-4
+    assert abs(loss.item() - float(z["loss"])) <= 1e-5
+    for k, ref in grads.items():
+        assert vit_ref.rel_err(g[k], ref) <= 1e-4, k
+
+
+def test_vit_b_bf16_logits_vs_oracle():
+    """BASELINE config 3 architecture (ViT-B/16 224^2) in bf16 at bs=2 vs the fp32 CPU oracle."""
+    cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype="bf16")
+    params = vit_ref.init_params(cfg, seed=0, randomize_all=False)
+    img, _ = vit_ref.synthetic_batch(cfg, 2)
+    with torch.no_grad():
+        ref = vit_ref.forward(img, params, cfg)
+        model = VisionTransformer(cfg).cuda()
+        model.load_param_dict(params)
+        out = model(img.cuda()).cpu()
+    err = (out - ref).abs().max().item()
+    print(f"ViT-B/16 bf16 logits max-abs vs fp32 oracle: {err:.3e}")
+    assert err < 2e-2
+
+
+def test_c2_fp32_logits_vs_oracle():
+    """BASELINE config 2: ViT-S/16 224^2 bs=128 fp32 on the GPU vs the CPU oracle, logits <= 1e-3."""
+    cfg = config_c2()
+    params = vit_ref.init_params(cfg, seed=0, randomize_all=False)
+    img, _ = vit_ref.synthetic_batch(cfg, 128)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    with torch.no_grad():
+        ref = vit_ref.forward(img, params, cfg)
+        model = VisionTransformer(cfg).cuda()
+        model.load_param_dict(params)
+        out = model(img.cuda()).cpu()
+    err = (out - ref).abs().max().item()
+    print(f"ViT-S/16 fp32 bs=128 logits max-abs vs CPU oracle: {err:.3e}")
+    assert err <= 1e-3
+
+
+def test_training_steps_reduce_loss():
+    cfg = ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2, num_classes=2,
+                    dtype="bf16")
+    torch.manual_seed(0)
+    model = VisionTransformer(cfg).cuda()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    img, tgt = vit_ref.synthetic_batch(cfg, 16)
+    img, tgt = img.cuda(), tgt.cuda()
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = cross_entropy(model(img), tgt)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.5 * losses[0], losses

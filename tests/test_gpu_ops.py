@@ -1,0 +1,231 @@
+"""Per-kernel numerics on the MI355X: every HIP kernel against a plain PyTorch fp32
+reference of the same op (computed on the CPU from the same rounded inputs)."""
+
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from vitmi import ops  # noqa: E402
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+# ------------------------------------------------------------------ GEMM
+FWD_SHAPES = [(197 * 3, 320, 192), (256, 384, 64), (1000, 2304, 768), (5, 64, 128)]
+
+
+@pytest.mark.parametrize("M,N,K", FWD_SHAPES)
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_linear_fwd_store(M, N, K, T):
+    x, w, b = rnd(M, K, dtype=T, seed=1), rnd(N, K, dtype=T, seed=2, scale=0.05), rnd(N, seed=3)
+    ref = x.float() @ w.float().t() + b
+    y32 = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), torch.float32)
+    assert rel(y32, ref) < 1e-5
+    y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), T)
+    assert rel(y.float(), ref) < (8e-3 if T == BF else 1e-5)
+
+
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_linear_fwd_gelu_and_residual(T):
+    M, N, K = 394, 768, 192
+    x, w, b = rnd(M, K, dtype=T, seed=4), rnd(N, K, dtype=T, seed=5, scale=0.05), rnd(N, seed=6)
+    u_ref = x.float() @ w.float().t() + b
+    a, u = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), T, ops.EPI_BIAS_GELU)
+    assert rel(u.float(), u_ref) < (8e-3 if T == BF else 1e-5)
+    assert rel(a.float(), F.gelu(u_ref)) < (8e-3 if T == BF else 1e-5)
+    r = rnd(M, N, seed=7)
+    y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), torch.float32, ops.EPI_RESIDUAL, residual=r.to(DEV))
+    assert rel(y, u_ref + r) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(394, 768, 192), (197 * 4, 2304, 768), (64, 192, 576)])
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_linear_dgrad(M, N, K, T):
+    dy, w = rnd(M, N, dtype=T, seed=8), rnd(N, K, dtype=T, seed=9, scale=0.05)
+    ref = dy.float() @ w.float()
+    dx = ops.linear_dgrad(dy.to(DEV), w.to(DEV), torch.float32)
+    assert rel(dx, ref) < 1e-5
+    u = rnd(M, K, dtype=T, seed=10)
+    dg = ops.linear_dgrad(dy.to(DEV), w.to(DEV), T, ops.EPI_DGELU, aux=u.to(DEV))
+    uu = u.float().requires_grad_(True)
+    gl = torch.autograd.grad(F.gelu(uu), uu, ref)[0]
+    assert rel(dg.float(), gl) < (8e-3 if T == BF else 1e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(197 * 2, 384, 192), (4000, 384, 768), (50, 64, 64), (20000, 192, 576)])
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_linear_wgrad_accumulates(M, N, K, T):
+    dy, x = rnd(M, N, dtype=T, seed=11), rnd(M, K, dtype=T, seed=12)
+    prev = rnd(N, K, seed=13)
+    ref = prev + dy.float().t() @ x.float()
+    dw = prev.clone().to(DEV)
+    ops.linear_wgrad(dy.to(DEV), x.to(DEV), dw)
+    assert rel(dw, ref) < 2e-5
+
+
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_bias_grad(T):
+    dy = rnd(197 * 3 + 1, 2304, dtype=T, seed=14)
+    db = torch.ones(2304, device=DEV)
+    ops.bias_grad(dy.to(DEV), db)
+    assert rel(db, 1 + dy.float().sum(0)) < 1e-5
+
+
+# ------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("D", [64, 192, 384, 768, 1024])
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_layernorm_fwd_bwd(D, T):
+    M = 197 * 2 + 3
+    x = rnd(M, D, seed=15) * 2 + 0.5
+    w, b = 1 + 0.1 * rnd(D, seed=16), 0.1 * rnd(D, seed=17)
+    y, mean, rstd = ops.layernorm_fwd(x.to(DEV), w.to(DEV), b.to(DEV), 1e-6, T)
+    ref = F.layer_norm(x, (D,), w, b, 1e-6)
+    assert rel(y.float(), ref) < (5e-3 if T == BF else 1e-6)
+    dy = rnd(M, D, seed=18).to(T)
+    dres = rnd(M, D, seed=19)
+    dg, dbb = torch.full((D,), 0.5, device=DEV), torch.full((D,), -0.5, device=DEV)
+    dx, dx_lp = ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, w.to(DEV), dg, dbb, dres=dres.to(DEV),
+                                  lp_dtype=BF)
+    xx, ww, bb = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    F.layer_norm(xx, (D,), ww, bb, 1e-6).backward(dy.float())
+    assert rel(dx, xx.grad + dres) < 1e-5
+    assert rel(dx_lp.float(), xx.grad + dres) < 5e-3
+    assert rel(dg, 0.5 + ww.grad) < 1e-5
+    assert rel(dbb, -0.5 + bb.grad) < 1e-5
+
+
+def test_layernorm_strided_rows():
+    B, N, D = 5, 17, 192
+    x = rnd(B, N, D, seed=20)
+    w, b = torch.ones(D), torch.zeros(D)
+    xd = x.to(DEV)
+    y, mean, rstd = ops.layernorm_fwd(xd[:, 0], w.to(DEV), b.to(DEV), 1e-6, torch.float32)
+    assert rel(y, F.layer_norm(x[:, 0], (D,), w, b, 1e-6)) < 1e-6
+    dx = torch.zeros(B, N, D, device=DEV)
+    dy = rnd(B, D, seed=21)
+    ops.layernorm_bwd(dy.to(DEV), xd[:, 0], mean, rstd, w.to(DEV), None, None, dx=dx[:, 0])
+    xx = x[:, 0].clone().requires_grad_()
+    F.layer_norm(xx, (D,), w, b, 1e-6).backward(dy)
+    assert rel(dx[:, 0], xx.grad) < 1e-5
+    assert dx[:, 1:].abs().max().item() == 0.0
+
+
+# ------------------------------------------------------------------ attention
+def attn_ref(qkv, B, N, H, scale):
+    D = qkv.shape[-1] // 3
+    q, k, v = qkv.float().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    p = s.softmax(-1)
+    o = (p @ v).transpose(1, 2).reshape(B * N, D)
+    lse = torch.logsumexp(s, -1).reshape(B * H, N)
+    return o, lse
+
+
+ATT = [(2, 197, 2), (1, 17, 3), (2, 64, 1), (1, 577, 2), (3, 1, 2), (1, 130, 1)]
+
+
+@pytest.mark.parametrize("B,N,H", ATT)
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_attention_fwd_bwd(B, N, H, T):
+    D = 64 * H
+    scale = 64 ** -0.5
+    qkv = rnd(B * N, 3 * D, dtype=T, seed=22)
+    o, lse = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
+    o_ref, lse_ref = attn_ref(qkv, B, N, H, scale)
+    tol = 1e-2 if T == BF else 1e-5
+    assert rel(o.float(), o_ref) < tol
+    assert rel(lse, lse_ref) < 1e-5
+    do = rnd(B * N, D, dtype=T, seed=23)
+    dqkv = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+    qq = qkv.float().clone().requires_grad_()
+    o2, _ = attn_ref(qq, B, N, H, scale)
+    o2.backward(do.float())
+    g = qq.grad.view(B * N, 3, D)
+    d = dqkv.float().cpu().view(B * N, 3, D)
+    for i, name in enumerate("qkv"):
+        assert rel(d[:, i], g[:, i]) < (2e-2 if T == BF else 1e-5), name
+
+
+def test_attention_softmax_spike():
+    """A key row that dominates one query forces the online-softmax rescale branch."""
+    B, N, H = 1, 197, 1
+    qkv = rnd(B * N, 192, seed=24) * 0.5
+    qkv[150, 64:128] = qkv[3, 0:64] * 40   # k_150 aligned with q_3 -> huge score at tile 2
+    qkv = qkv.to(BF)
+    o, lse = ops.attention_fwd(qkv.to(DEV), B, N, H, 0.125)
+    o_ref, lse_ref = attn_ref(qkv, B, N, H, 0.125)
+    assert rel(o.float(), o_ref) < 1e-2
+    assert rel(lse, lse_ref) < 1e-5
+
+
+# ------------------------------------------------------------------ embed / head / loss / cast
+@pytest.mark.parametrize("C,S,P", [(3, 64, 16), (1, 32, 8), (3, 224, 16)])
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_im2col(C, S, P, T):
+    img = torch.rand(2, C, S, S)
+    out = ops.patch_im2col(img.to(DEV), P, T)
+    G = S // P
+    ref = img.view(2, C, G, P, G, P).permute(0, 2, 4, 1, 3, 5).reshape(2 * G * G, C * P * P)
+    assert torch.equal(out.cpu(), ref.to(T))
+
+
+def test_tokens_assemble_roundtrip():
+    B, np_, D = 3, 16, 192
+    tok, cls, pos = rnd(B * np_, D, seed=25), rnd(D, seed=26), rnd(np_ + 1, D, seed=27)
+    x = ops.tokens_assemble(tok.to(DEV), B, np_, cls.to(DEV), pos.to(DEV))
+    ref = torch.cat([cls.expand(B, 1, D), tok.view(B, np_, D)], 1) + pos
+    assert torch.allclose(x.cpu(), ref)
+    dx = rnd(B, np_ + 1, D, seed=28)
+    dcls, dpos = torch.zeros(D, device=DEV), torch.ones((np_ + 1) * D, device=DEV)
+    dtok, dtok_lp = ops.tokens_assemble_bwd(dx.to(DEV), B, np_, True, BF, dcls, dpos)
+    assert torch.equal(dtok.cpu(), dx[:, 1:].reshape(B * np_, D))
+    assert torch.equal(dtok_lp.cpu(), dx[:, 1:].reshape(B * np_, D).to(BF))
+    assert rel(dpos.view(np_ + 1, D), 1 + dx.sum(0)) < 1e-6
+    assert rel(dcls, dx[:, 0].sum(0)) < 1e-6
+
+
+def test_head_and_losses():
+    B, D, C = 37, 192, 3
+    y, w, b = rnd(B, D, seed=29), rnd(C, D, seed=30), rnd(C, seed=31)
+    logits = ops.head_fwd(y.to(DEV), w.to(DEV), b.to(DEV))
+    assert rel(logits, y @ w.t() + b) < 1e-6
+    tgt = torch.randint(0, C, (B,))
+    loss, dl = ops.loss_fwd_bwd(logits, tgt.to(DEV), ops.LOSS_CE)
+    z = (y @ w.t() + b).requires_grad_()
+    ref = F.cross_entropy(z, tgt)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5
+    assert rel(dl, z.grad) < 1e-5
+    t2 = rnd(B, C, seed=32)
+    loss2, dl2 = ops.loss_fwd_bwd(logits, t2.to(DEV), ops.LOSS_MSE)
+    z2 = (y @ w.t() + b).requires_grad_()
+    r2 = F.mse_loss(z2, t2)
+    r2.backward()
+    assert abs(loss2.item() - r2.item()) < 1e-5 and rel(dl2, z2.grad) < 1e-5
+    dw, db = torch.zeros(C, D, device=DEV), torch.zeros(C, device=DEV)
+    dy = ops.head_bwd(dl, y.to(DEV), w.to(DEV), dw, db)
+    assert rel(dy, z.grad @ w) < 1e-5
+    assert rel(dw, z.grad.t() @ y) < 1e-5 and rel(db, z.grad.sum(0)) < 1e-5
+
+
+def test_cast():
+    x = rnd(1000003, seed=33)
+    y = ops.cast_bf16(x.to(DEV))
+    assert torch.equal(y.cpu(), x.to(BF))
+
+
+

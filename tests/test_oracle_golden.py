@@ -23,11 +23,11 @@ def _load(name):
 CASES = {
     # MS_CvT semantics: scale D**-0.5 (MS_CvT.py:100), no qkv bias (:82), LN in
     # ConvEmbed (:358), eps 1e-5, no pos-embed.
-    "mscvt_vit_stage.npz": ViTConfig(img_size=32, patch_size=8, embed_dim=64, depth=2, num_heads=4,
+    "mscvt_vit_stage.npz": ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2,
                                      num_classes=2, attn_scale="dim", ln_eps=1e-5, qkv_bias=False,
                                      embed_norm=True, pos_embed=False),
     # standard ViT semantics (Keras knobs: head-dim scale, bias, eps 1e-6) + pos-embed
-    "hf_vit.npz": ViTConfig(img_size=32, patch_size=8, embed_dim=64, depth=2, num_heads=4,
+    "hf_vit.npz": ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2,
                             num_classes=2, attn_scale="head", ln_eps=1e-6, qkv_bias=True,
                             embed_norm=False, pos_embed=True),
 }

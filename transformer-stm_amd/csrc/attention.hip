@@ -1,0 +1,651 @@
+// attention.hip — multi-head scaled-dot-product attention, forward and backward, gfx950.
+//
+// Replaces layers.MultiHeadAttention (models/CvT(Par).py:137,185) / the
+// einsum-softmax-einsum of old_codes/MS_CvT.py:202-207.
+//
+// Layout: qkv [B*N][3*D] token-major (q | k | v, head h at columns h*64), o [B*N][D],
+// lse fp32 [B*H][N].  dh = 64.
+//
+// bf16 path (v_mfma_f32_32x32x16_bf16), flash-style with the whole softmax in registers:
+//   * "swapped" S^T = K Q^T: the query sits on the MFMA lane, so a softmax row is
+//     lane-local (16 keys per lane + one xor-32 exchange), no LDS round trip;
+//   * the S^T accumulator feeds the P.V product directly as the B operand
+//     (O^T = V^T P^T sums over the accumulator's ROW index: no lane movement);
+//   * V^T / Q^T / K^T / dO^T operands come from row-major LDS tiles through
+//     ds_read_b64_tr_b16 (hardware transpose);
+//   * one XOR swizzle serves both the row reads (ds_read_b128) and the transposed
+//     reads of every 64x64 bf16 tile: chunk' = chunk ^ (((row>>1)&1)<<2 | ((row>>2)&3)).
+//   Tiles are staged by LDS-DMA (buffer_load ... lds) with the range check zero-filling
+//   keys/queries >= N.  Backward = delta pre-pass + dK/dV kernel (keys on lanes, query
+//   tiles streamed) + dQ kernel (queries on lanes, key tiles streamed); no atomics.
+// fp32 path: thread-per-row VALU kernels (exact fp32; the parity configuration).
+#include "common.h"
+
+namespace vitmi {
+
+static constexpr int DH = 64;
+static constexpr float LOG2E = 1.4426950408889634f;
+static constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ int att_swz(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+
+// byte offset of 16-B chunk `ch` of row `row` in a [64][64] bf16 tile (128-B rows)
+__device__ __forceinline__ int toff(int row, int ch) { return row * 128 + ((ch ^ att_swz(row)) << 4); }
+
+// Stage 64 rows x 128 B (64 bf16 of one head) of a token-major matrix into a tile.
+// rs is rebased at (batch start, column); row r of the tile = token tok0 + r.
+template <int NWAVES>
+__device__ __forceinline__ void stage_tile(char* lds, __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes,
+                                           int tok0, int wave, int lane) {
+#pragma unroll
+  for (int p = wave; p < 8; p += NWAVES) {
+    const int r = p * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ att_swz(r);
+    const uint32_t voff = (uint32_t)((int64_t)(tok0 + r) * ld_bytes + c * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, lds + p * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// A/B fragment of a 32x32x16 step from a row-major tile: lane row = row0 + (lane&31),
+// k = 16*s + 8*(lane>>5) + j   -> one ds_read_b128
+__device__ __forceinline__ bf16x8 frag_row(const char* t, int row0, int s, int lane) {
+  const int row = row0 + (lane & 31);
+  return *(const bf16x8*)(t + toff(row, 2 * s + (lane >> 5)));
+}
+
+// Transposed fragment: operand X^T[col][k] where the tile holds X[k][col] (rows = k).
+// lane (col = c0 + (lane&31), h = lane>>5), element j <-> k-row
+//   k0 + 8*(j>>2) + 4*h + (j&3)   (the accumulator-as-operand k order)
+__device__ __forceinline__ bf16x8 frag_tr(const char* t, int k0, int c0, int lane) {
+  const int g = lane >> 4, tl = lane & 15, q = tl >> 2, p = tl & 3;
+  const int h = g >> 1;
+  const int col = c0 + 16 * (g & 1) + 4 * p;  // first of 4 columns this lane addresses
+  bf16x8 f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = k0 + 8 * i + 4 * h + q;
+    const int addr = toff(row, col >> 3) + ((col & 7) << 1);
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, t + addr));
+    bf16x4 b = __builtin_bit_cast(bf16x4, v);
+    f[4 * i + 0] = b[0];
+    f[4 * i + 1] = b[1];
+    f[4 * i + 2] = b[2];
+    f[4 * i + 3] = b[3];
+  }
+  return f;
+}
+
+// key/query index held in accumulator register r of a 32x32 tile for lane-half h
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// accumulator regs 8s..8s+7 -> bf16 operand fragment
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
+  return r;
+}
+
+// 16 B of a token row from global via the range-checked buffer path (zero past the end)
+__device__ __forceinline__ bf16x8 load_row16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// store 4 consecutive d values (fp32) of row `row` as bf16 (8 bytes)
+__device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float d) {
+  bf16x4 v;
+  v[0] = (bf16)a; v[1] = (bf16)b; v[2] = (bf16)c; v[3] = (bf16)d;
+  *(bf16x4*)p = v;
+}
+
+// =============================================================== forward (bf16)
+// grid (ceil(N/128), B*H), 256 threads: wave w owns queries q0 + 32w .. +31.
+__global__ __launch_bounds__(256) void attn_fwd_bf16(const bf16* __restrict__ qkv,
+                                                     bf16* __restrict__ o, float* __restrict__ lse,
+                                                     int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][K|V] 8 KiB tiles
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int64_t ldb = ld * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+
+  const int qw = blockIdx.x * 128 + wave * 32;  // first query of this wave
+  const int q = qw + (lane & 31);
+  // Q^T operand fragments: lane col q, k = d = 16s + 8h + j
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
+
+  const float c2 = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x16 oacc[2] = {zero16(), zero16()};
+
+  const int nt = (N + 63) / 64;
+  stage_tile<4>(smem, rk, ldb, 0, wave, lane);
+  stage_tile<4>(smem + 8192, rv, ldb, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nt) {
+      char* nb = smem + (buf ^ 1) * 16384;
+      stage_tile<4>(nb, rk, ldb, (t + 1) * 64, wave, lane);
+      stage_tile<4>(nb + 8192, rv, ldb, (t + 1) * 64, wave, lane);
+    }
+    const char* kt = smem + buf * 16384;
+    const char* vt = kt + 8192;
+    if (qw < N) {
+      f32x16 st[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        st[u] = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) st[u] = mfma32(frag_row(kt, 32 * u, s, lane), qf[s], st[u]);
+      }
+      // scale, mask, tile max
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = t * 64 + 32 * u + acc_row(r, h);
+          const float v = key < N ? st[u][r] * c2 : -INFINITY;
+          st[u][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mn);  // m=-inf on the first tile -> 0
+      m = mn;
+      float rs = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(st[u][r] - mn);
+          st[u][r] = p;
+          rs += p;
+        }
+      l = l * alpha + rs;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
+      // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pb = pack8(st[u], s);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            oacc[dt] = mfma32(frag_tr(vt, 32 * u + 16 * s, 32 * dt, lane), pb, oacc[dt]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (qw >= N) return;
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (q < N) {
+    const float inv = 1.f / lt;
+    bf16* orow = o + ((int64_t)b * N + q) * D + hd * DH;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * h;
+        store4(orow + d, oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv, oacc[dt][4 * g4 + 2] * inv,
+               oacc[dt][4 * g4 + 3] * inv);
+      }
+    if (h == 0) lse[(int64_t)bh * N + q] = (m + log2f(lt)) * LN2;
+  }
+}
+
+// =============================================================== backward (bf16)
+// delta[bh][q] = sum_d dO[q][d] * O[q][d]
+template <typename T>
+__global__ void attn_bwd_delta(const T* __restrict__ o, const T* __restrict__ dout,
+                               float* __restrict__ delta, int BN, int N, int H) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (token, head)
+  if (i >= (int64_t)BN * H) return;
+  const int64_t tok = i / H;
+  const int hd = (int)(i % H);
+  const int D = H * DH;
+  const T* po = o + tok * D + hd * DH;
+  const T* pd = dout + tok * D + hd * DH;
+  float s = 0.f;
+#pragma unroll 8
+  for (int d = 0; d < DH; ++d) s += to_f32(po[d]) * to_f32(pd[d]);
+  const int b = (int)(tok / N), q = (int)(tok % N);
+  delta[((int64_t)b * H + hd) * N + q] = s;
+}
+
+// dK/dV: grid (ceil(N/128), B*H), wave w owns keys k0 = 128*bx + 32w .. +31.
+__global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][Q|dO]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  const float* lse_bh = lse + (int64_t)bh * N;
+  const float* del_bh = delta + (int64_t)bh * N;
+
+  const int kw = blockIdx.x * 128 + wave * 32;
+  const int key = kw + (lane & 31);
+  // K^T / V^T operand fragments (B operands): lane col = key, k = d = 16s + 8h + j
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = load_row16(rk, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
+    vf[s] = load_row16(rv, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
+  }
+  const float c2 = scale * LOG2E;
+  f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+
+  const int nt = (N + 63) / 64;
+  stage_tile<4>(smem, rq, ldb, 0, wave, lane);
+  stage_tile<4>(smem + 8192, rdo, ldo, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nt) {
+      char* nb = smem + (buf ^ 1) * 16384;
+      stage_tile<4>(nb, rq, ldb, (t + 1) * 64, wave, lane);
+      stage_tile<4>(nb + 8192, rdo, ldo, (t + 1) * 64, wave, lane);
+    }
+    const char* qt = smem + buf * 16384;
+    const char* dt_ = qt + 8192;
+    if (kw < N) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // 32-query sub-tile
+        f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sa = mfma32(frag_row(qt, 32 * u, s, lane), kf[s], sa);   // S[q][key]
+          dp = mfma32(frag_row(dt_, 32 * u, s, lane), vf[s], dp);  // dP[q][key]
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = t * 64 + 32 * u + acc_row(r, h);
+          const bool ok = qi < N;
+          const float L2 = ok ? lse_bh[qi] * LOG2E : 0.f;
+          const float dl = ok ? del_bh[qi] : 0.f;
+          const float p = ok ? exp2f(sa[r] * c2 - L2) : 0.f;
+          sa[r] = p;
+          dp[r] = p * (dp[r] - dl);
+        }
+        // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
+#pragma unroll
+          for (int d2 = 0; d2 < 2; ++d2) {
+            dvt[d2] = mfma32(frag_tr(dt_, 32 * u + 16 * s, 32 * d2, lane), pb, dvt[d2]);
+            dkt[d2] = mfma32(frag_tr(qt, 32 * u + 16 * s, 32 * d2, lane), sb, dkt[d2]);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (kw >= N || key >= N) return;
+  bf16* row = dqkv + ((int64_t)b * N + key) * ld;
+#pragma unroll
+  for (int d2 = 0; d2 < 2; ++d2)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * d2 + 8 * g4 + 4 * h;
+      store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
+             dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
+      store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
+             dvt[d2][4 * g4 + 3]);
+    }
+}
+
+// dQ: grid (ceil(N/128), B*H), wave w owns queries q0 = 128*bx + 32w .. +31.
+__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][K|V]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+
+  const int qw = blockIdx.x * 128 + wave * 32;
+  const int q = qw + (lane & 31);
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
+    df[s] = load_row16(rdo, (uint32_t)((int64_t)q * ldo + (16 * s + 8 * h) * 2));
+  }
+  const bool qok = q < N;
+  const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : 0.f;
+  const float dl = qok ? delta[(int64_t)bh * N + q] : 0.f;
+  const float c2 = scale * LOG2E;
+  f32x16 dqt[2] = {zero16(), zero16()};
+
+  const int nt = (N + 63) / 64;
+  stage_tile<4>(smem, rk, ldb, 0, wave, lane);
+  stage_tile<4>(smem + 8192, rv, ldb, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nt) {
+      char* nb = smem + (buf ^ 1) * 16384;
+      stage_tile<4>(nb, rk, ldb, (t + 1) * 64, wave, lane);
+      stage_tile<4>(nb + 8192, rv, ldb, (t + 1) * 64, wave, lane);
+    }
+    const char* kt = smem + buf * 16384;
+    const char* vt = kt + 8192;
+    if (qw < N) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // 32-key sub-tile
+        f32x16 st = zero16(), dp = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          st = mfma32(frag_row(kt, 32 * u, s, lane), qf[s], st);  // S^T[key][q]
+          dp = mfma32(frag_row(vt, 32 * u, s, lane), df[s], dp);  // dP^T[key][q]
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = t * 64 + 32 * u + acc_row(r, h);
+          const float p = (key < N && qok) ? exp2f(st[r] * c2 - L2) : 0.f;
+          dp[r] = p * (dp[r] - dl);
+        }
+        // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 sb = pack8(dp, s);
+#pragma unroll
+          for (int d2 = 0; d2 < 2; ++d2)
+            dqt[d2] = mfma32(frag_tr(kt, 32 * u + 16 * s, 32 * d2, lane), sb, dqt[d2]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (qw >= N || !qok) return;
+  bf16* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
+#pragma unroll
+  for (int d2 = 0; d2 < 2; ++d2)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * d2 + 8 * g4 + 4 * h;
+      store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale,
+             dqt[d2][4 * g4 + 2] * scale, dqt[d2][4 * g4 + 3] * scale);
+    }
+}
+
+// =============================================================== fp32 path (VALU)
+// One thread per query row; K/V chunks of 64 rows staged in LDS (broadcast reads).
+static constexpr int F32_CH = 64;
+
+__global__ __launch_bounds__(64) void attn_fwd_f32(const float* __restrict__ qkv,
+                                                   float* __restrict__ o, float* __restrict__ lse,
+                                                   int N, int H, float scale) {
+  __shared__ float ks[F32_CH][DH], vs[F32_CH][DH];
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = qkv + (int64_t)b * N * ld;
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  float qr[DH], acc[DH];
+  const bool ok = q < N;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) {
+    qr[d] = ok ? base[(int64_t)q * ld + hd * DH + d] * scale : 0.f;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = 0; k0 < N; k0 += F32_CH) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < F32_CH * DH; i += 64) {
+      const int r = i / DH, d = i % DH, key = k0 + r;
+      ks[r][d] = key < N ? base[(int64_t)key * ld + D + hd * DH + d] : 0.f;
+      vs[r][d] = key < N ? base[(int64_t)key * ld + 2 * D + hd * DH + d] : 0.f;
+    }
+    __syncthreads();
+    const int kn = min(F32_CH, N - k0);
+    for (int r = 0; r < kn; ++r) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) s += qr[d] * ks[r][d];
+      const float mn = fmaxf(m, s);
+      const float a = expf(m - mn), p = expf(s - mn);
+      l = l * a + p;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) acc[d] = acc[d] * a + p * vs[r][d];
+      m = mn;
+    }
+  }
+  if (!ok) return;
+  const float inv = 1.f / l;
+  float* orow = o + ((int64_t)b * N + q) * D + hd * DH;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) orow[d] = acc[d] * inv;
+  lse[(int64_t)bh * N + q] = m + logf(l);
+}
+
+// dQ (thread per query) — dq = scale * sum_k P (dP - delta) K
+__global__ __launch_bounds__(64) void attn_bwd_dq_f32(const float* __restrict__ qkv,
+                                                      const float* __restrict__ dout,
+                                                      const float* __restrict__ lse,
+                                                      const float* __restrict__ delta,
+                                                      float* __restrict__ dqkv, int N, int H,
+                                                      float scale) {
+  __shared__ float ks[F32_CH][DH], vs[F32_CH][DH];
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = qkv + (int64_t)b * N * ld;
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  const bool ok = q < N;
+  float qr[DH], dor[DH], acc[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) {
+    qr[d] = ok ? base[(int64_t)q * ld + hd * DH + d] * scale : 0.f;
+    dor[d] = ok ? dout[((int64_t)b * N + q) * D + hd * DH + d] : 0.f;
+    acc[d] = 0.f;
+  }
+  const float L = ok ? lse[(int64_t)bh * N + q] : 0.f;
+  const float dl = ok ? delta[(int64_t)bh * N + q] : 0.f;
+  for (int k0 = 0; k0 < N; k0 += F32_CH) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < F32_CH * DH; i += 64) {
+      const int r = i / DH, d = i % DH, key = k0 + r;
+      ks[r][d] = key < N ? base[(int64_t)key * ld + D + hd * DH + d] : 0.f;
+      vs[r][d] = key < N ? base[(int64_t)key * ld + 2 * D + hd * DH + d] : 0.f;
+    }
+    __syncthreads();
+    const int kn = min(F32_CH, N - k0);
+    for (int r = 0; r < kn; ++r) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        s += qr[d] * ks[r][d];
+        dp += dor[d] * vs[r][d];
+      }
+      const float ds = expf(s - L) * (dp - dl);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) acc[d] += ds * ks[r][d];
+    }
+  }
+  if (!ok) return;
+  float* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) row[d] = acc[d] * scale;
+}
+
+// dK, dV (thread per key) — dv = sum_q P dO, dk = scale * sum_q P (dP - delta) Q
+__global__ __launch_bounds__(64) void attn_bwd_dkv_f32(const float* __restrict__ qkv,
+                                                       const float* __restrict__ dout,
+                                                       const float* __restrict__ lse,
+                                                       const float* __restrict__ delta,
+                                                       float* __restrict__ dqkv, int N, int H,
+                                                       float scale) {
+  __shared__ float qs[F32_CH][DH], ds_[F32_CH][DH], ls[F32_CH], dls[F32_CH];
+  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = qkv + (int64_t)b * N * ld;
+  const int key = blockIdx.x * 64 + threadIdx.x;
+  const bool ok = key < N;
+  float kr[DH], vr[DH], dk[DH], dv[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) {
+    kr[d] = ok ? base[(int64_t)key * ld + D + hd * DH + d] * scale : 0.f;
+    vr[d] = ok ? base[(int64_t)key * ld + 2 * D + hd * DH + d] : 0.f;
+    dk[d] = 0.f;
+    dv[d] = 0.f;
+  }
+  for (int q0 = 0; q0 < N; q0 += F32_CH) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < F32_CH * DH; i += 64) {
+      const int r = i / DH, d = i % DH, q = q0 + r;
+      qs[r][d] = q < N ? base[(int64_t)q * ld + hd * DH + d] : 0.f;
+      ds_[r][d] = q < N ? dout[((int64_t)b * N + q) * D + hd * DH + d] : 0.f;
+    }
+    if (threadIdx.x < F32_CH) {
+      const int q = q0 + threadIdx.x;
+      ls[threadIdx.x] = q < N ? lse[(int64_t)bh * N + q] : 0.f;
+      dls[threadIdx.x] = q < N ? delta[(int64_t)bh * N + q] : 0.f;
+    }
+    __syncthreads();
+    const int qn = min(F32_CH, N - q0);
+    for (int r = 0; r < qn; ++r) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        s += kr[d] * qs[r][d];
+        dp += vr[d] * ds_[r][d];
+      }
+      const float p = expf(s - ls[r]);
+      const float dsv = p * (dp - dls[r]);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        dv[d] += p * ds_[r][d];
+        dk[d] += dsv * qs[r][d];
+      }
+    }
+  }
+  if (!ok) return;
+  float* row = dqkv + ((int64_t)b * N + key) * ld;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) {
+    row[D + hd * DH + d] = dk[d] * scale;
+    row[2 * D + hd * DH + d] = dv[d];
+  }
+}
+
+}  // namespace vitmi
+
+using namespace vitmi;
+
+static int attn_check(int dtype, int B, int N, int H, int dh) {
+  VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "attention: bad dtype %d", dtype);
+  VITMI_CHECK_ARG(dh == DH, "attention: head dim must be 64 (got %d)", dh);
+  VITMI_CHECK_ARG(B > 0 && N > 0 && H > 0, "attention: empty problem");
+  VITMI_CHECK_ARG((int64_t)N * 3 * H * DH * (dtype == VITMI_BF16 ? 2 : 4) < 0x7fffffffLL,
+                  "attention: one batch row block exceeds 2 GiB");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float scale,
+                                   const void* qkv, void* o, float* lse, vitmi_stream_t stream) {
+  if (int rc = attn_check(dtype, B, N, H, dh)) return rc;
+  VITMI_CHECK_ARG(qkv && o && lse, "attention_fwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VITMI_BF16) {
+    dim3 grid((N + 127) / 128, B * H);
+    hipLaunchKernelGGL(attn_fwd_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (bf16*)o, lse, N, H, scale);
+  } else {
+    dim3 grid((N + 63) / 64, B * H);
+    hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(64), 0, s, (const float*)qkv, (float*)o, lse, N, H, scale);
+  }
+  VITMI_LAUNCH_CHECK("attention_fwd");
+  return VITMI_OK;
+}
+
+extern "C" size_t vitmi_attention_bwd_workspace_size(int B, int N, int H) {
+  return (size_t)B * H * N * sizeof(float);
+}
+
+extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale,
+                                   const void* qkv, const void* o, const void* dout,
+                                   const float* lse, void* dqkv, void* workspace, size_t ws_bytes,
+                                   vitmi_stream_t stream) {
+  if (int rc = attn_check(dtype, B, N, H, dh)) return rc;
+  VITMI_CHECK_ARG(qkv && o && dout && lse && dqkv, "attention_bwd: null pointer");
+  VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_attention_bwd_workspace_size(B, N, H),
+                  "attention_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* delta = (float*)workspace;
+  const int64_t rows = (int64_t)B * N * H;
+  const int blocks = (int)((rows + 255) / 256);
+  if (dtype == VITMI_BF16) {
+    hipLaunchKernelGGL(attn_bwd_delta<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)o,
+                       (const bf16*)dout, delta, B * N, N, H);
+    dim3 grid((N + 127) / 128, B * H);
+    hipLaunchKernelGGL(attn_bwd_dkv_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
+                       lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
+                       lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_delta<float>, dim3(blocks), dim3(256), 0, s, (const float*)o,
+                       (const float*)dout, delta, B * N, N, H);
+    dim3 grid((N + 63) / 64, B * H);
+    hipLaunchKernelGGL(attn_bwd_dkv_f32, grid, dim3(64), 0, s, (const float*)qkv, (const float*)dout,
+                       lse, (const float*)delta, (float*)dqkv, N, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_f32, grid, dim3(64), 0, s, (const float*)qkv, (const float*)dout,
+                       lse, (const float*)delta, (float*)dqkv, N, H, scale);
+  }
+  VITMI_LAUNCH_CHECK("attention_bwd");
+  return VITMI_OK;
+}

@@ -1,0 +1,78 @@
+// Shared device/host helpers for the gfx950 (CDNA4) kernels of libvitmi.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include "../../include/vitmi.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+namespace vitmi {
+
+// ---------------------------------------------------------------- host side
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+
+#define VITMI_CHECK_ARG(cond, ...)                                   \
+  do {                                                               \
+    if (!(cond)) return ::vitmi::fail(VITMI_ERR_INVALID, __VA_ARGS__); \
+  } while (0)
+
+#define VITMI_LAUNCH_CHECK(what)                                              \
+  do {                                                                        \
+    hipError_t e_ = hipGetLastError();                                        \
+    if (e_ != hipSuccess)                                                     \
+      return ::vitmi::fail(VITMI_ERR_HIP, "%s: %s", what, hipGetErrorString(e_)); \
+  } while (0)
+
+// ---------------------------------------------------------------- conversions
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// exact-erf GELU (tf.nn.gelu default, models/CvT(Par).py:254) and its derivative
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- buffer resources
+// A raw buffer descriptor: loads past `bytes` return 0 (the hardware range check),
+// which is how ragged M/N/reduction edges are zero-filled without branches.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ uint32_t clamp_bytes(int64_t b) {
+  return b <= 0 ? 0u : (b > 0x7fffffff ? 0x7fffffffu : (uint32_t)b);
+}
+
+}  // namespace vitmi

@@ -1,0 +1,330 @@
+// elementwise.hip — the HBM-bound glue of the ViT path: patch im2col, token
+// assembly (cls + pos-embed), bias-gradient column sums, the classifier head,
+// the loss, and the fp32 -> bf16 weight cast.  All loads/stores are 16-byte
+// vectors where the layout allows (cdna_hip_programming.md Guideline 13).
+#include "common.h"
+
+namespace vitmi {
+
+// ------------------------------------------------------------ patch im2col
+// patches[(b*np + ph*G + pw)][c*P*P + kh*P + kw] = img[b][c][ph*P+kh][pw*P+kw]
+// one thread per 4 consecutive kw (P % 4 == 0, S % 4 == 0)
+template <typename T>
+__global__ void im2col_kernel(const float* __restrict__ img, T* __restrict__ out, int B, int C,
+                              int S, int P) {
+  const int G = S / P, np = G * G, K = C * P * P;
+  const int64_t total = (int64_t)B * np * K / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    const int64_t row = e / K;
+    const int col = (int)(e % K);
+    const int b = (int)(row / np), pidx = (int)(row % np);
+    const int ph = pidx / G, pw = pidx % G;
+    const int c = col / (P * P), kh = (col / P) % P, kw = col % P;
+    const f32x4 v = *(const f32x4*)(img + (((int64_t)b * C + c) * S + ph * P + kh) * S + pw * P + kw);
+    T* o = out + e;
+    if constexpr (sizeof(T) == 2) {
+      bf16x4 w;
+      w[0] = (bf16)v[0]; w[1] = (bf16)v[1]; w[2] = (bf16)v[2]; w[3] = (bf16)v[3];
+      *(bf16x4*)o = w;
+    } else {
+      *(f32x4*)o = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------ token assembly
+__global__ void tokens_assemble_kernel(int B, int np, int D, const float* __restrict__ tok,
+                                       const float* __restrict__ cls, const float* __restrict__ pos,
+                                       float* __restrict__ x) {
+  const int N = np + 1, D4 = D / 4;
+  const int64_t total = (int64_t)B * N * D4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D4) * 4;
+    const int64_t bn = i / D4;
+    const int n = (int)(bn % N);
+    const int b = (int)(bn / N);
+    f32x4 v = n == 0 ? (cls ? *(const f32x4*)(cls + d) : f32x4{0.f, 0.f, 0.f, 0.f})
+                     : *(const f32x4*)(tok + ((int64_t)b * np + n - 1) * D + d);
+    if (pos) v += *(const f32x4*)(pos + (int64_t)n * D + d);
+    *(f32x4*)(x + bn * D + d) = v;
+  }
+}
+
+__global__ void tokens_split_bwd_kernel(int B, int np, int D, const float* __restrict__ dx,
+                                        float* __restrict__ dtok, bf16* __restrict__ dtok_lp) {
+  const int N = np + 1, D4 = D / 4;
+  const int64_t total = (int64_t)B * np * D4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D4) * 4;
+    const int64_t r = i / D4;  // b*np + p
+    const int b = (int)(r / np), p = (int)(r % np);
+    const f32x4 v = *(const f32x4*)(dx + ((int64_t)b * N + p + 1) * D + d);
+    if (dtok) *(f32x4*)(dtok + r * D + d) = v;
+    if (dtok_lp) {
+      bf16x4 w;
+      w[0] = (bf16)v[0]; w[1] = (bf16)v[1]; w[2] = (bf16)v[2]; w[3] = (bf16)v[3];
+      *(bf16x4*)(dtok_lp + r * D + d) = w;
+    }
+  }
+}
+
+// dpos[n][d] += sum_b dx[b][n][d];  dcls[d] += sum_b dx[b][0][d]
+__global__ void tokens_pos_bwd_kernel(int B, int N, int D, const float* __restrict__ dx,
+                                      float* __restrict__ dcls, float* __restrict__ dpos) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * D) return;
+  const int n = (int)(i / D), d = (int)(i % D);
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += dx[((int64_t)b * N + n) * D + d];
+  if (dpos) dpos[i] += s;
+  if (dcls && n == 0) dcls[d] += s;
+}
+
+// ------------------------------------------------------------ bias gradient
+// partial[z][n] = sum over rows of chunk z of dy[m][n]; 256 threads = 256 columns x 1
+template <typename T>
+__global__ void colsum_kernel(int64_t M, int64_t N, const T* __restrict__ dy, int64_t ldy,
+                              float* __restrict__ part, int64_t rows_per) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int64_t m0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t m1 = m0 + rows_per < M ? m0 + rows_per : M;
+  float s = 0.f;
+  for (int64_t m = m0; m < m1; ++m) s += to_f32(dy[m * ldy + n]);
+  part[(int64_t)blockIdx.y * N + n] = s;
+}
+
+__global__ void colsum_finish_kernel(int64_t N, int Z, const float* __restrict__ part,
+                                     float* __restrict__ db) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int z = 0; z < Z; ++z) s += part[(int64_t)z * N + n];
+  db[n] += s;
+}
+
+static int colsum_splits(int64_t M) {
+  int64_t z = (M + 255) / 256;
+  return (int)(z > 256 ? 256 : (z < 1 ? 1 : z));
+}
+
+// ------------------------------------------------------------ head + loss
+// logits[b][c] = y[b] . w[c] + bias[c]; one wave per (b, c)
+__global__ void head_fwd_kernel(int B, int D, int C, const float* __restrict__ y, int64_t ldy,
+                                const float* __restrict__ w, const float* __restrict__ bias,
+                                float* __restrict__ logits) {
+  const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wv >= B * C) return;
+  const int b = wv / C, c = wv % C;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += y[(int64_t)b * ldy + d] * w[(int64_t)c * D + d];
+  s = wave_sum(s);
+  if (lane == 0) logits[wv] = s + (bias ? bias[c] : 0.f);
+}
+
+// dy[b][d] = sum_c dl[b][c] w[c][d]
+__global__ void head_bwd_dy_kernel(int B, int D, int C, const float* __restrict__ dl,
+                                   const float* __restrict__ w, float* __restrict__ dy) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * D) return;
+  const int b = (int)(i / D), d = (int)(i % D);
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s += dl[b * C + c] * w[(int64_t)c * D + d];
+  dy[i] = s;
+}
+
+// dw[c][d] += sum_b dl[b][c] y[b][d];  db[c] += sum_b dl[b][c]
+__global__ void head_bwd_dw_kernel(int B, int D, int C, const float* __restrict__ dl,
+                                   const float* __restrict__ y, int64_t ldy, float* __restrict__ dw,
+                                   float* __restrict__ db) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)C * D) return;
+  const int c = (int)(i / D), d = (int)(i % D);
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += dl[b * C + c] * y[(int64_t)b * ldy + d];
+  dw[i] += s;
+  if (db && d == 0) {
+    float t = 0.f;
+    for (int b = 0; b < B; ++b) t += dl[b * C + c];
+    db[c] += t;
+  }
+}
+
+// mean-reduced loss and its gradient; one block of 256 threads
+__global__ void loss_kernel(int kind, int B, int C, const float* __restrict__ logits,
+                            const void* __restrict__ target, float* __restrict__ loss,
+                            float* __restrict__ dl) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  const float invB = 1.f / B;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float* z = logits + (int64_t)b * C;
+    if (kind == VITMI_LOSS_CE) {
+      const int64_t t = ((const int64_t*)target)[b];
+      float mx = -INFINITY;
+      for (int c = 0; c < C; ++c) mx = fmaxf(mx, z[c]);
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += expf(z[c] - mx);
+      const float lse = mx + logf(se);
+      acc += lse - z[t];
+      for (int c = 0; c < C; ++c) dl[(int64_t)b * C + c] = (expf(z[c] - lse) - (c == t ? 1.f : 0.f)) * invB;
+    } else {  // MSE over all outputs (Keras mean_squared_error, C == 1 for the reference)
+      const float* t = (const float*)target + (int64_t)b * C;
+      for (int c = 0; c < C; ++c) {
+        const float d = z[c] - t[c];
+        acc += d * d / C;
+        dl[(int64_t)b * C + c] = 2.f * d * invB / C;
+      }
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] * invB;
+}
+
+__global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16* __restrict__ dst) {
+  const int64_t n8 = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const f32x4 a = *(const f32x4*)(src + i * 8), b = *(const f32x4*)(src + i * 8 + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (bf16)a[j];
+      o[4 + j] = (bf16)b[j];
+    }
+    *(bf16x8*)(dst + i * 8) = o;
+  }
+  const int64_t t = n8 * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) dst[t] = (bf16)src[t];
+}
+
+static unsigned grid_for(int64_t work, int per_block = 256) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g > 8192) g = 8192;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+}  // namespace vitmi
+
+using namespace vitmi;
+
+extern "C" int vitmi_patch_im2col(int dtype, int B, int C, int S, int P, const float* img,
+                                  void* patches, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(P > 0 && S % P == 0 && P % 4 == 0, "im2col: need S %% P == 0 and P %% 4 == 0");
+  VITMI_CHECK_ARG(img && patches, "im2col: null pointer");
+  const int64_t work = (int64_t)B * C * S * S / 4;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VITMI_BF16)
+    hipLaunchKernelGGL(im2col_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, s, img, (bf16*)patches, B, C, S, P);
+  else
+    hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_for(work)), dim3(256), 0, s, img, (float*)patches, B, C, S, P);
+  VITMI_LAUNCH_CHECK("im2col");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_tokens_assemble(int B, int np, int D, const float* tok, const float* cls,
+                                     const float* pos, float* x, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(D % 4 == 0 && tok && x, "tokens_assemble: bad arguments");
+  const int64_t work = (int64_t)B * (np + 1) * D / 4;
+  hipLaunchKernelGGL(tokens_assemble_kernel, dim3(grid_for(work)), dim3(256), 0, (hipStream_t)stream,
+                     B, np, D, tok, cls, pos, x);
+  VITMI_LAUNCH_CHECK("tokens_assemble");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_tokens_assemble_bwd(int B, int np, int D, const float* dx, float* dtok,
+                                         void* dtok_lp, float* dcls, float* dpos,
+                                         vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(D % 4 == 0 && dx, "tokens_assemble_bwd: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtok || dtok_lp) {
+    const int64_t work = (int64_t)B * np * D / 4;
+    hipLaunchKernelGGL(tokens_split_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, B, np, D, dx,
+                       dtok, (bf16*)dtok_lp);
+  }
+  if (dcls || dpos) {
+    const int64_t work = (int64_t)(np + 1) * D;
+    hipLaunchKernelGGL(tokens_pos_bwd_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, B,
+                       np + 1, D, dx, dcls, dpos);
+  }
+  VITMI_LAUNCH_CHECK("tokens_assemble_bwd");
+  return VITMI_OK;
+}
+
+extern "C" size_t vitmi_bias_grad_workspace_size(int64_t M, int64_t N) {
+  return (size_t)colsum_splits(M) * N * sizeof(float);
+}
+
+extern "C" int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, int64_t ldy,
+                               float* db, void* workspace, size_t ws_bytes, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(dy && db, "bias_grad: null pointer");
+  VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_bias_grad_workspace_size(M, N), "bias_grad: workspace too small");
+  if (M == 0 || N == 0) return VITMI_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int Z = colsum_splits(M);
+  const int64_t rows_per = (M + Z - 1) / Z;
+  dim3 grid((unsigned)((N + 255) / 256), Z);
+  if (dtype == VITMI_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)dy, ldy,
+                       (float*)workspace, rows_per);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)dy, ldy,
+                       (float*)workspace, rows_per);
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, Z,
+                     (const float*)workspace, db);
+  VITMI_LAUNCH_CHECK("bias_grad");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_head_fwd(int B, int D, int C, const float* y, int64_t ldy, const float* w,
+                              const float* b, float* logits, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(y && w && logits && B > 0 && C > 0, "head_fwd: bad arguments");
+  const int waves = B * C;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, D, C,
+                     y, ldy, w, b, logits);
+  VITMI_LAUNCH_CHECK("head_fwd");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_head_bwd(int B, int D, int C, const float* dlogits, const float* y, int64_t ldy,
+                              const float* w, float* dy, float* dw, float* db,
+                              vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(dlogits && y && w && dy && dw, "head_bwd: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(head_bwd_dy_kernel, dim3((unsigned)(((int64_t)B * D + 255) / 256)), dim3(256), 0, s,
+                     B, D, C, dlogits, w, dy);
+  hipLaunchKernelGGL(head_bwd_dw_kernel, dim3((unsigned)(((int64_t)C * D + 255) / 256)), dim3(256), 0, s,
+                     B, D, C, dlogits, y, ldy, dw, db);
+  VITMI_LAUNCH_CHECK("head_bwd");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_loss_fwd_bwd(int kind, int B, int C, const float* logits, const void* target,
+                                  float* loss, float* dlogits, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(kind == VITMI_LOSS_CE || kind == VITMI_LOSS_MSE, "loss: bad kind %d", kind);
+  VITMI_CHECK_ARG(logits && target && loss && dlogits && B > 0 && C > 0, "loss: bad arguments");
+  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, kind, B, C, logits, target,
+                     loss, dlogits);
+  VITMI_LAUNCH_CHECK("loss");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(src && dst, "cast: null pointer");
+  VITMI_CHECK_ARG(((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % 16) == 0, "cast: 16-byte alignment required");
+  if (n == 0) return VITMI_OK;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n / 8 + 1)), dim3(256), 0, (hipStream_t)stream, n, src,
+                     (bf16*)dst);
+  VITMI_LAUNCH_CHECK("cast");
+  return VITMI_OK;
+}

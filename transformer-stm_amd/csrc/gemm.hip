@@ -1,0 +1,482 @@
+// gemm.hip — LDS-tiled MFMA GEMM for gfx950 with fused epilogues.
+//
+// C[M,N] = sum_k A(m,k) B(k,n); each operand is either k-major (rows of k, the
+// nn.Linear weight / activation layout) or m/n-major (the transposed operands of
+// the backward).  Tiles are staged global->LDS with `buffer_load ... lds`
+// (LDS-DMA, 16 B per lane, no VGPR round trip); the buffer range check zero-fills
+// ragged edges.  The LDS images are XOR-swizzled on the SOURCE address so the
+// fragment reads are bank-conflict free:
+//   k-major  [R][BK]: chunk' = chunk ^ ((row >> 1) & 7)       read by ds_read_b128
+//   mn-major [BK][R]: chunk' = chunk ^ (2*(k&3) + 8*((k>>3)&1)) read by ds_read_b64_tr_b16
+// (tools/lds_bank_check.py enumerates every access of both images.)
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 for bf16 operands, v_mfma_f32_16x16x4_f32 for
+// fp32 (exact fp32 products).  For fp32 each lane reads 8 consecutive k and the
+// j-th MFMA consumes element j from every lane group: both operands use the same
+// k permutation, so the sum is unchanged.
+#include "common.h"
+
+namespace vitmi {
+
+template <typename T> struct TT;
+template <> struct TT<bf16> { static constexpr int BK = 64, ES = 2; };
+template <> struct TT<float> { static constexpr int BK = 32, ES = 4; };
+
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;
+  int64_t M, N, K;
+  int64_t lda, ldb, ldc;
+  const float* bias;
+  void* aux;
+  int64_t ldaux;
+  const float* residual;
+  int64_t ldr;
+  int64_t k_per_split;   // reduction range of one blockIdx.z (multiple of BK)
+  int64_t split_stride;  // elements between split partial slabs (EPI_PARTIAL)
+  int tiles_n;           // number of BN tiles along N
+};
+
+enum { EPI_PARTIAL = 100 };
+
+__device__ __forceinline__ int swz_k(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int swz_mn(int k) { return 2 * (k & 3) + 8 * ((k >> 3) & 1); }
+
+// Fragment of one 16x16xK32 MFMA step for one lane.
+template <typename T> struct Frag;
+template <> struct Frag<bf16> { bf16x8 v; };
+template <> struct Frag<float> { f32x4 lo, hi; };
+
+// ---- tile staging ---------------------------------------------------------
+// Stage an R x BK tile (rows = m or n) of a k-major matrix into LDS image [R][BK].
+template <typename T, int R, int NWAVES>
+__device__ __forceinline__ void stage_kmajor(char* lds, __amdgpu_buffer_rsrc_t rs, int64_t ld,
+                                             int64_t k0, int wave, int lane) {
+  constexpr int ES = TT<T>::ES, BK = TT<T>::BK;
+  constexpr int RB = BK * ES;            // 128 bytes per row
+  constexpr int PIECES = R * RB / 1024;  // 1 KiB per wave instruction
+  static_assert(RB == 128, "k-major rows must be 128 B");
+#pragma unroll
+  for (int p = wave; p < PIECES; p += NWAVES) {
+    const int r = p * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz_k(r);
+    const uint32_t voff = (uint32_t)(r * ld * ES + k0 * ES + c * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, lds + p * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// Stage a BK x R tile (rows = k) of an m/n-major matrix into LDS image [BK][R].
+template <typename T, int R, int NWAVES>
+__device__ __forceinline__ void stage_mnmajor(char* lds, __amdgpu_buffer_rsrc_t rs, int64_t ld,
+                                              int64_t krow0, int wave, int lane) {
+  constexpr int ES = TT<T>::ES, BK = TT<T>::BK;
+  constexpr int RB = R * ES;
+  constexpr int CPR = RB / 16;        // chunks per row
+  constexpr int RPP = 64 / CPR;       // rows per 1 KiB piece
+  constexpr int PIECES = BK * RB / 1024;
+  static_assert(CPR >= 16 && CPR <= 64, "m/n-major rows must be 256..1024 B");
+#pragma unroll
+  for (int p = wave; p < PIECES; p += NWAVES) {
+    const int r = p * RPP + lane / CPR;
+    const int c = (lane % CPR) ^ swz_mn(r);
+    const uint32_t voff = (uint32_t)((krow0 + r) * ld * ES + c * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, lds + p * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// ---- fragment reads -------------------------------------------------------
+template <typename T, bool KMAJ, int R>
+struct FragReader;
+
+template <int R>
+struct FragReader<bf16, true, R> {
+  static __device__ __forceinline__ Frag<bf16> read(const char* lds, int row0, int kk, int lane) {
+    const int row = row0 + (lane & 15);
+    const int c = ((kk >> 3) + (lane >> 4)) ^ swz_k(row);
+    Frag<bf16> f;
+    f.v = *(const bf16x8*)(lds + row * 128 + c * 16);
+    return f;
+  }
+};
+
+template <int R>
+struct FragReader<float, true, R> {
+  static __device__ __forceinline__ Frag<float> read(const char* lds, int row0, int kk, int lane) {
+    const int row = row0 + (lane & 15);
+    const int c0 = (kk >> 2) + 2 * (lane >> 4);
+    const int s = swz_k(row);
+    Frag<float> f;
+    f.lo = *(const f32x4*)(lds + row * 128 + ((c0) ^ s) * 16);
+    f.hi = *(const f32x4*)(lds + row * 128 + ((c0 + 1) ^ s) * 16);
+    return f;
+  }
+};
+
+template <int R>
+struct FragReader<bf16, false, R> {
+  // image [BK][R] bf16, rows of R*2 bytes; lane gets col row0+(lane&15), k = kk+8g+j
+  static __device__ __forceinline__ Frag<bf16> read(const char* lds, int row0, int kk, int lane) {
+    constexpr int RB = R * 2;
+    const int t = lane & 15, g = lane >> 4, q = t >> 2, p = t & 3;
+    const int chunk = (row0 >> 3) + (p >> 1);
+    Frag<bf16> f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kr = kk + 8 * g + 4 * i + q;
+      const int addr = kr * RB + ((chunk ^ swz_mn(kr)) * 16) + (p & 1) * 8;
+      s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + addr));
+      bf16x4 b = __builtin_bit_cast(bf16x4, v);
+      f.v[4 * i + 0] = b[0];
+      f.v[4 * i + 1] = b[1];
+      f.v[4 * i + 2] = b[2];
+      f.v[4 * i + 3] = b[3];
+    }
+    return f;
+  }
+};
+
+template <int R>
+struct FragReader<float, false, R> {
+  static __device__ __forceinline__ Frag<float> read(const char* lds, int row0, int kk, int lane) {
+    constexpr int RB = R * 4;
+    const int col = row0 + (lane & 15), g = lane >> 4;
+    const int cb = col * 4;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kr = kk + 8 * g + j;
+      v[j] = *(const float*)(lds + kr * RB + (((cb >> 4) ^ swz_mn(kr)) << 4) + (cb & 15));
+    }
+    Frag<float> f;
+    f.lo = f32x4{v[0], v[1], v[2], v[3]};
+    f.hi = f32x4{v[4], v[5], v[6], v[7]};
+    return f;
+  }
+};
+
+__device__ __forceinline__ f32x4 mma(const Frag<bf16>& a, const Frag<bf16>& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b, f32x4 c) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
+  return c;
+}
+
+// ---- epilogue ----------------------------------------------------------------
+template <typename T, typename TC, int EPI>
+__device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_t col, float acc,
+                                          float biasv) {
+  if constexpr (EPI == EPI_PARTIAL) {
+    ((float*)g.C)[blockIdx.z * g.split_stride + row * g.ldc + col] = acc;
+  } else if constexpr (EPI == VITMI_EPI_STORE) {
+    ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc + biasv);
+  } else if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
+    const float u = acc + biasv;
+    ((T*)g.aux)[row * g.ldaux + col] = from_f32<T>(u);
+    ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(gelu_f(u));
+  } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
+    ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + acc + biasv;
+  } else if constexpr (EPI == VITMI_EPI_DGELU) {
+    const float u = to_f32(((const T*)g.aux)[row * g.ldaux + col]);
+    ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc * gelu_grad_f(u));
+  } else if constexpr (EPI == VITMI_EPI_ACCUM) {
+    ((float*)g.C)[row * g.ldc + col] += acc;
+  }
+}
+
+// ---- the kernel ------------------------------------------------------------
+template <typename T, bool AK, bool BKM, int EPI, typename TC, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
+  constexpr int ES = TT<T>::ES, BK = TT<T>::BK;
+  constexpr int NW = WM * WN;
+  constexpr int A_BYTES = BM * BK * ES, B_BYTES = BN * BK * ES;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tile = blockIdx.x;
+  const int tm_i = tile / g.tiles_n, tn_i = tile % g.tiles_n;
+  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
+  const int64_t kb = (int64_t)blockIdx.z * g.k_per_split;
+  const int64_t ke = min(g.K, kb + g.k_per_split);
+  const int nk = (int)((ke - kb + BK - 1) / BK);
+
+  // buffer descriptors rebased at this block's panel (range check = zero fill)
+  __amdgpu_buffer_rsrc_t ra, rb;
+  if (AK) {
+    const char* base = (const char*)g.A + m0 * g.lda * ES;
+    ra = make_rsrc(base, clamp_bytes((g.M - m0) * g.lda * ES));
+  } else {
+    const char* base = (const char*)g.A + (kb * g.lda + m0) * ES;
+    ra = make_rsrc(base, clamp_bytes(((g.K - kb) * g.lda - m0) * ES));
+  }
+  if (BKM) {
+    const char* base = (const char*)g.B + n0 * g.ldb * ES;
+    rb = make_rsrc(base, clamp_bytes((g.N - n0) * g.ldb * ES));
+  } else {
+    const char* base = (const char*)g.B + (kb * g.ldb + n0) * ES;
+    rb = make_rsrc(base, clamp_bytes(((g.K - kb) * g.ldb - n0) * ES));
+  }
+
+  auto stage = [&](int t, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    if (AK) stage_kmajor<T, BM, NW>(sa, ra, g.lda, kb + (int64_t)t * BK, wave, lane);
+    else stage_mnmajor<T, BM, NW>(sa, ra, g.lda, (int64_t)t * BK, wave, lane);
+    if (BKM) stage_kmajor<T, BN, NW>(sb, rb, g.ldb, kb + (int64_t)t * BK, wave, lane);
+    else stage_mnmajor<T, BN, NW>(sb, rb, g.ldb, (int64_t)t * BK, wave, lane);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) stage(t + 1, buf ^ 1);
+    const char* sa = smem + buf * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      Frag<T> af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = FragReader<T, AK, BM>::read(sa, wm * (BM / WM) + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = FragReader<T, BKM, BN>::read(sb, wn * (BN / WN) + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mma(af[i], bfr[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: C layout of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + i
+  const int cl = lane & 15, rg = 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int64_t col = n0 + wn * (BN / WN) + j * 16 + cl;
+    if (col >= g.N) continue;
+    const float bv = (g.bias && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM &&
+                      EPI != VITMI_EPI_DGELU) ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 16 + rg + r;
+        if (row < g.M) epi_store<T, TC, EPI>(g, row, col, acc[i][j][r], bv);
+      }
+    }
+  }
+}
+
+// split-K reduction: dst[i] += sum_z ws[z][i]
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dst,
+                                     int64_t n, int splits, int64_t stride) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * 4;
+  for (; i < n; i += step) {
+    if (i + 4 <= n) {
+      f32x4 s = *(const f32x4*)(dst + i);
+      for (int z = 0; z < splits; ++z) s += *(const f32x4*)(ws + z * stride + i);
+      *(f32x4*)(dst + i) = s;
+    } else {
+      for (int64_t e = i; e < n; ++e) {
+        float s = dst[e];
+        for (int z = 0; z < splits; ++z) s += ws[z * stride + e];
+        dst[e] = s;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- host launch
+template <typename T, bool AK, bool BKM, int EPI, typename TC>
+static int launch_t(GemmArgs g, int splits, hipStream_t s) {
+  constexpr int BM = 128, BN = 128, WM = 2, WN = 2;
+  g.tiles_n = (int)((g.N + BN - 1) / BN);
+  const int tiles_m = (int)((g.M + BM - 1) / BM);
+  dim3 grid(tiles_m * g.tiles_n, 1, splits);
+  hipLaunchKernelGGL((gemm_kernel<T, AK, BKM, EPI, TC, BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, s, g);
+  VITMI_LAUNCH_CHECK("gemm_kernel");
+  return VITMI_OK;
+}
+
+template <typename T, int EPI, typename TC>
+static int launch_layout(int ak, int bk, GemmArgs g, int splits, hipStream_t s) {
+  if (ak && bk) return launch_t<T, true, true, EPI, TC>(g, splits, s);
+  if (ak && !bk) return launch_t<T, true, false, EPI, TC>(g, splits, s);
+  if (!ak && !bk) return launch_t<T, false, false, EPI, TC>(g, splits, s);
+  return fail(VITMI_ERR_UNSUPPORTED, "gemm: layout A m-major x B k-major not instantiated");
+}
+
+template <typename T>
+static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits, hipStream_t s) {
+  const bool cbf = (c_dtype == VITMI_BF16);
+  switch (epi) {
+    case VITMI_EPI_STORE:
+      return cbf ? launch_layout<T, VITMI_EPI_STORE, bf16>(ak, bk, g, splits, s)
+                 : launch_layout<T, VITMI_EPI_STORE, float>(ak, bk, g, splits, s);
+    case VITMI_EPI_BIAS_GELU:
+      return cbf ? launch_layout<T, VITMI_EPI_BIAS_GELU, bf16>(ak, bk, g, splits, s)
+                 : launch_layout<T, VITMI_EPI_BIAS_GELU, float>(ak, bk, g, splits, s);
+    case VITMI_EPI_RESIDUAL:
+      return launch_layout<T, VITMI_EPI_RESIDUAL, float>(ak, bk, g, splits, s);
+    case VITMI_EPI_DGELU:
+      return cbf ? launch_layout<T, VITMI_EPI_DGELU, bf16>(ak, bk, g, splits, s)
+                 : launch_layout<T, VITMI_EPI_DGELU, float>(ak, bk, g, splits, s);
+    case VITMI_EPI_ACCUM:
+      return launch_layout<T, VITMI_EPI_ACCUM, float>(ak, bk, g, splits, s);
+    case EPI_PARTIAL:
+      return launch_layout<T, EPI_PARTIAL, float>(ak, bk, g, splits, s);
+  }
+  return fail(VITMI_ERR_INVALID, "gemm: unknown epilogue %d", epi);
+}
+
+static int bk_of(int dtype) { return dtype == VITMI_BF16 ? 64 : 32; }
+
+// split count for a reduction-heavy GEMM: fill ~2 blocks per CU
+static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const int64_t ktiles = (K + bk_of(dtype) - 1) / bk_of(dtype);
+  int64_t want = (512 + tiles - 1) / tiles;
+  int64_t maxs = ktiles / 8;  // at least 8 k-tiles per split
+  if (want > maxs) want = maxs;
+  if (want > 64) want = 64;
+  return want < 1 ? 1 : (int)want;
+}
+
+static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K, const void* A,
+                     int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
+                     int epi, const float* bias, void* aux, int64_t ldaux, const float* residual,
+                     int64_t ldr, void* ws, size_t ws_bytes, hipStream_t s, bool allow_split) {
+  VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "gemm: bad dtype %d", dtype);
+  VITMI_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
+  if (M == 0 || N == 0) return VITMI_OK;
+  VITMI_CHECK_ARG(A && B && C, "gemm: null operand");
+  const int BK = bk_of(dtype);
+  if (ak) VITMI_CHECK_ARG(K % BK == 0, "gemm: k-major A needs K %% %d == 0 (K=%lld)", BK, (long long)K);
+  if (bk) VITMI_CHECK_ARG(K % BK == 0, "gemm: k-major B needs K %% %d == 0 (K=%lld)", BK, (long long)K);
+  const int es = dtype == VITMI_BF16 ? 2 : 4;
+  VITMI_CHECK_ARG((lda * es) % 16 == 0 && (ldb * es) % 16 == 0, "gemm: lda/ldb must be 16-byte multiples");
+  VITMI_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "gemm: A/B must be 16-byte aligned");
+  VITMI_CHECK_ARG(ak ? lda >= K : lda >= M, "gemm: lda too small");
+  VITMI_CHECK_ARG(bk ? ldb >= K : ldb >= N, "gemm: ldb too small");
+  VITMI_CHECK_ARG(ldc >= N, "gemm: ldc too small");
+  if (epi == VITMI_EPI_BIAS_GELU || epi == VITMI_EPI_DGELU)
+    VITMI_CHECK_ARG(aux != nullptr && ldaux >= N, "gemm: epilogue needs aux");
+  if (epi == VITMI_EPI_RESIDUAL) VITMI_CHECK_ARG(residual != nullptr && ldr >= N, "gemm: residual missing");
+  if (epi == VITMI_EPI_RESIDUAL || epi == VITMI_EPI_ACCUM)
+    VITMI_CHECK_ARG(c_dtype == VITMI_F32, "gemm: residual/accum epilogues write fp32");
+  // 32-bit buffer offsets: one block's panel must stay under 2 GiB
+  VITMI_CHECK_ARG((ak ? 128 * lda : K * lda) * es < 0x7fffffffLL, "gemm: A panel exceeds 2 GiB");
+
+  GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.bias = bias; g.aux = aux; g.ldaux = ldaux;
+  g.residual = residual; g.ldr = ldr;
+  int splits = 1;
+  if (allow_split && epi == VITMI_EPI_ACCUM) splits = choose_splits(dtype, M, N, K);
+  const int64_t ktiles = (K + BK - 1) / BK;
+  g.k_per_split = ((ktiles + splits - 1) / splits) * BK;
+  if (K == 0) g.k_per_split = BK;
+  splits = (int)((K + g.k_per_split - 1) / g.k_per_split);
+  if (splits < 1) splits = 1;
+  if (splits > 1) {
+    const size_t need = (size_t)splits * M * N * sizeof(float);
+    if (ws == nullptr || ws_bytes < need) splits = 1, g.k_per_split = ktiles * BK;
+  }
+  if (splits == 1) {
+    g.k_per_split = (K > 0 ? ktiles : 1) * BK;
+    if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, s);
+    return dispatch<float>(ak, bk, c_dtype, epi, g, 1, s);
+  }
+  // split-K: partial slabs then one reduction pass into C (+=)
+  GemmArgs gp = g;
+  gp.C = ws; gp.ldc = N; gp.split_stride = M * N;
+  int rc = dtype == VITMI_BF16 ? dispatch<bf16>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, s)
+                               : dispatch<float>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, s);
+  if (rc) return rc;
+  VITMI_CHECK_ARG(ldc == N, "gemm: split-K accumulate needs a dense C");
+  const int64_t n = M * N;
+  int blocks = (int)((n / 4 + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)ws,
+                     (float*)C, n, splits, M * N);
+  VITMI_LAUNCH_CHECK("splitk_reduce_kernel");
+  return VITMI_OK;
+}
+
+}  // namespace vitmi
+
+using namespace vitmi;
+
+extern "C" int vitmi_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
+                          const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
+                          int64_t ldc, int c_dtype, int epilogue, const float* bias, void* aux,
+                          int64_t ldaux, const float* residual, int64_t ldr, void* workspace,
+                          size_t ws_bytes, vitmi_stream_t stream) {
+  return gemm_impl(dtype, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, C, ldc, c_dtype, epilogue,
+                   bias, aux, ldaux, residual, ldr, workspace, ws_bytes, (hipStream_t)stream, true);
+}
+
+extern "C" size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajor, int64_t M,
+                                            int64_t N, int64_t K, int epilogue) {
+  (void)a_kmajor; (void)b_kmajor;
+  if (epilogue != VITMI_EPI_ACCUM) return 0;
+  const int splits = choose_splits(dtype, M, N, K);
+  return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+}
+
+extern "C" int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, const void* x,
+                                const void* w, const float* bias, void* y, int y_dtype,
+                                int epilogue, void* aux, const float* residual,
+                                vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_BIAS_GELU ||
+                      epilogue == VITMI_EPI_RESIDUAL, "linear_fwd: bad epilogue %d", epilogue);
+  return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, N, y_dtype, epilogue, bias, aux, N,
+                   residual, N, nullptr, 0, (hipStream_t)stream, false);
+}
+
+extern "C" int vitmi_linear_dgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy,
+                                  const void* w, void* dx, int dx_dtype, int epilogue,
+                                  const void* aux, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_DGELU,
+                  "linear_dgrad: bad epilogue %d", epilogue);
+  // dx[M,K] = dy[M,N] . W[N,K]: reduction over N; A = dy (k-major), B = W as [N][K] (n-major)
+  return gemm_impl(dtype, 1, 0, M, K, N, dy, N, w, K, dx, K, dx_dtype, epilogue, nullptr,
+                   const_cast<void*>(aux), K, nullptr, 0, nullptr, 0, (hipStream_t)stream, false);
+}
+
+extern "C" size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
+  // dW[N,K]: GEMM rows N, cols K, reduction M
+  const int splits = choose_splits(dtype, N, K, M);
+  return splits > 1 ? (size_t)splits * N * K * sizeof(float) : 0;
+}
+
+extern "C" int vitmi_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy,
+                                  const void* x, float* dw, void* workspace, size_t ws_bytes,
+                                  vitmi_stream_t stream) {
+  // dW[N,K] += sum_m dy[m][n] x[m][k]: A(n,m) = dy (m-major rows of n), B(m,k) = x (k contiguous)
+  return gemm_impl(dtype, 0, 0, N, K, M, dy, N, x, K, dw, K, VITMI_F32, VITMI_EPI_ACCUM, nullptr,
+                   nullptr, 0, nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, true);
+}

@@ -1,0 +1,258 @@
+// layernorm.hip — LayerNorm forward/backward (layers.LayerNormalization(epsilon=1e-6),
+// models/CvT(Par).py:248,272,278,328; nn.LayerNorm old_codes/MS_CvT.py:39-45,307,315).
+//
+// HBM-bound: one wave per row, the row held in registers as float4 (D <= 2048),
+// fp32 statistics.  Forward writes y in the GEMM operand dtype plus mean/rstd;
+// backward fuses the residual-gradient add (dx = dres + LN'(dy)) and the bf16 copy
+// the next GEMM consumes, and produces per-block dgamma/dbeta partials that a
+// second pass folds into the fp32 parameter gradients (+=).
+#include "common.h"
+
+namespace vitmi {
+
+template <typename TY>
+__device__ __forceinline__ void store4(TY* p, f32x4 v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, f32x4 v) { *(f32x4*)p = v; }
+template <>
+__device__ __forceinline__ void store4<bf16>(bf16* p, f32x4 v) {
+  bf16x4 b;
+  b[0] = (bf16)v[0]; b[1] = (bf16)v[1]; b[2] = (bf16)v[2]; b[3] = (bf16)v[3];
+  *(bf16x4*)p = b;
+}
+template <typename T>
+__device__ __forceinline__ f32x4 load4(const T* p);
+template <>
+__device__ __forceinline__ f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
+template <>
+__device__ __forceinline__ f32x4 load4<bf16>(const bf16* p) {
+  bf16x4 b = *(const bf16x4*)p;
+  return f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+}
+
+// ---------------------------------------------------------------- forward
+template <int NV, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const float* __restrict__ x,
+                                                     int64_t ldx, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     TY* __restrict__ y, int64_t ldy,
+                                                     float* __restrict__ mean, float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + row * ldx;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    v[i] = c < D ? *(const f32x4*)(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    if (c < D) {
+      const f32x4 d = v[i] - mu;
+      q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+  TY* yr = y + row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    if (c < D) {
+      const f32x4 g = *(const f32x4*)(gamma + c);
+      const f32x4 b = *(const f32x4*)(beta + c);
+      store4<TY>(yr + c, (v[i] - mu) * rs * g + b);
+    }
+  }
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// grid = G blocks x 256 threads; wave w of block b handles rows b*4+w, +4G, ...
+template <int NV, typename TDY, bool LP>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    int64_t M, int D, const TDY* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
+    int64_t ldx, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, const float* __restrict__ dres, int64_t ldres,
+    float* __restrict__ dx, int64_t lddx, bf16* __restrict__ dx_lp, int64_t lddx_lp,
+    float* __restrict__ part) {
+  __shared__ f32x4 red[4][64 * NV * 2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x4 g[NV], dg[NV], db[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    g[i] = c < D ? *(const f32x4*)(gamma + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    dg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    db[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < M; row += (int64_t)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    f32x4 xh[NV], gy[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 4;
+      if (c < D) {
+        const f32x4 xv = *(const f32x4*)(x + row * ldx + c);
+        const f32x4 dyv = load4<TDY>(dy + row * lddy + c);
+        xh[i] = (xv - mu) * rs;
+        gy[i] = dyv * g[i];
+        dg[i] += dyv * xh[i];
+        db[i] += dyv;
+        s1 += gy[i][0] + gy[i][1] + gy[i][2] + gy[i][3];
+        const f32x4 t = gy[i] * xh[i];
+        s2 += t[0] + t[1] + t[2] + t[3];
+      } else {
+        xh[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        gy[i] = xh[i];
+      }
+    }
+    const float c1 = wave_sum(s1) / D, c2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 4;
+      if (c < D) {
+        f32x4 o = (gy[i] - c1 - xh[i] * c2) * rs;
+        if (dres) o += *(const f32x4*)(dres + row * ldres + c);
+        *(f32x4*)(dx + row * lddx + c) = o;
+        if (LP) store4<bf16>(dx_lp + row * lddx_lp + c, o);
+      }
+    }
+  }
+  // block-reduce dgamma/dbeta partials over the 4 waves
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    red[wave][i * 64 + lane] = dg[i];
+    red[wave][(NV + i) * 64 + lane] = db[i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NV * 2 * 64; e += 256) {
+    const f32x4 t = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+    const int which = e / (NV * 64);          // 0 = dgamma, 1 = dbeta
+    const int i = (e % (NV * 64)) / 64, l = e % 64;
+    const int c = (l + 64 * i) * 4;
+    if (c < D) *(f32x4*)(part + ((int64_t)which * gridDim.x + blockIdx.x) * D + c) = t;
+  }
+}
+
+// out[d] += sum_b part[b][d]   for dgamma (rows 0..G-1) and dbeta (rows G..2G-1)
+__global__ void ln_param_reduce(const float* __restrict__ part, int G, int D,
+                                float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float a = 0.f, b = 0.f;
+  for (int i = 0; i < G; ++i) {
+    a += part[(int64_t)i * D + d];
+    b += part[(int64_t)(G + i) * D + d];
+  }
+  if (dgamma) dgamma[d] += a;
+  if (dbeta) dbeta[d] += b;
+}
+
+static int ln_blocks_bwd(int64_t M) {
+  int64_t g = (M + 3) / 4;
+  return (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+}
+
+template <int NV>
+static void ln_fwd_launch(hipStream_t s, int64_t M, int D, const float* x, int64_t ldx,
+                          const float* gamma, const float* beta, float eps, void* y, int ydt,
+                          int64_t ldy, float* mean, float* rstd) {
+  dim3 grid((unsigned)((M + 3) / 4));
+  if (ydt == VITMI_BF16)
+    hipLaunchKernelGGL((ln_fwd_kernel<NV, bf16>), grid, dim3(256), 0, s, M, D, x, ldx, gamma, beta,
+                       eps, (bf16*)y, ldy, mean, rstd);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<NV, float>), grid, dim3(256), 0, s, M, D, x, ldx, gamma, beta,
+                       eps, (float*)y, ldy, mean, rstd);
+}
+
+template <int NV, typename TDY>
+static void ln_bwd_launch(hipStream_t s, int G, int64_t M, int D, const void* dy, int64_t lddy,
+                          const float* x, int64_t ldx, const float* mean, const float* rstd,
+                          const float* gamma, const float* dres, int64_t ldres, float* dx,
+                          int64_t lddx, void* dx_lp, int64_t lddx_lp, float* part) {
+  if (dx_lp)
+    hipLaunchKernelGGL((ln_bwd_kernel<NV, TDY, true>), dim3(G), dim3(256), 0, s, M, D,
+                       (const TDY*)dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx,
+                       (bf16*)dx_lp, lddx_lp, part);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<NV, TDY, false>), dim3(G), dim3(256), 0, s, M, D,
+                       (const TDY*)dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx,
+                       (bf16*)nullptr, 0, part);
+}
+
+}  // namespace vitmi
+
+using namespace vitmi;
+
+extern "C" int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx,
+                                   const float* gamma, const float* beta, float eps, void* y,
+                                   int y_dtype, int64_t ldy, float* mean, float* rstd,
+                                   vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "layernorm: D must be a multiple of 4 in [4, 2048]");
+  VITMI_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "layernorm: strides must be multiples of 4");
+  if (M == 0) return VITMI_OK;
+  VITMI_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int nv = (D + 255) / 256;
+  switch (nv) {
+    case 1: ln_fwd_launch<1>(s, M, D, x, ldx, gamma, beta, eps, y, y_dtype, ldy, mean, rstd); break;
+    case 2: ln_fwd_launch<2>(s, M, D, x, ldx, gamma, beta, eps, y, y_dtype, ldy, mean, rstd); break;
+    case 3: ln_fwd_launch<3>(s, M, D, x, ldx, gamma, beta, eps, y, y_dtype, ldy, mean, rstd); break;
+    case 4: ln_fwd_launch<4>(s, M, D, x, ldx, gamma, beta, eps, y, y_dtype, ldy, mean, rstd); break;
+    default: ln_fwd_launch<8>(s, M, D, x, ldx, gamma, beta, eps, y, y_dtype, ldy, mean, rstd); break;
+  }
+  VITMI_LAUNCH_CHECK("layernorm_fwd");
+  return VITMI_OK;
+}
+
+extern "C" size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D) {
+  return (size_t)2 * ln_blocks_bwd(M) * D * sizeof(float);
+}
+
+extern "C" int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtype, int64_t lddy,
+                                   const float* x, int64_t ldx, const float* mean,
+                                   const float* rstd, const float* gamma, const float* dres,
+                                   int64_t ldres, float* dx, int64_t lddx, void* dx_lp,
+                                   int64_t lddx_lp, float* dgamma, float* dbeta, void* workspace,
+                                   size_t ws_bytes, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "layernorm: D must be a multiple of 4 in [4, 2048]");
+  if (M == 0) return VITMI_OK;
+  VITMI_CHECK_ARG(dy && x && mean && rstd && gamma && dx, "layernorm_bwd: null pointer");
+  VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_layernorm_bwd_workspace_size(M, D),
+                  "layernorm_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int G = ln_blocks_bwd(M);
+  float* part = (float*)workspace;
+  const int nv = (D + 255) / 256;
+#define LNB(NV)                                                                                  \
+  if (dy_dtype == VITMI_BF16)                                                                    \
+    ln_bwd_launch<NV, bf16>(s, G, M, D, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx,    \
+                            lddx, dx_lp, lddx_lp, part);                                         \
+  else                                                                                           \
+    ln_bwd_launch<NV, float>(s, G, M, D, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx,   \
+                             lddx, dx_lp, lddx_lp, part);
+  switch (nv) {
+    case 1: LNB(1) break;
+    case 2: LNB(2) break;
+    case 3: LNB(3) break;
+    case 4: LNB(4) break;
+    default: LNB(8) break;
+  }
+#undef LNB
+  hipLaunchKernelGGL(ln_param_reduce, dim3((D + 255) / 256), dim3(256), 0, s, (const float*)part, G,
+                     D, dgamma, dbeta);
+  VITMI_LAUNCH_CHECK("layernorm_bwd");
+  return VITMI_OK;
+}

@@ -1,0 +1,79 @@
+"""ctypes loader for libvitmi.so (the C ABI declared in include/vitmi.h).
+
+torch is imported first on purpose: it loads its bundled ``libamdhip64.so``
+(SONAME ``libamdhip64.so.7``), so the library's own DT_NEEDED on that SONAME
+resolves to the SAME HIP runtime instance and torch's streams / device pointers
+are valid inside the kernels.  There is no fallback: if the library is missing
+every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvitmi.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_int64
+F = ctypes.c_float
+S = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/vitmi.h one to one
+SIGNATURES = {
+    "vitmi_version": (I, []),
+    "vitmi_last_error": (ctypes.c_char_p, []),
+    "vitmi_device_cus": (I, []),
+    "vitmi_gemm": (I, [I, I, I, L, L, L, P, L, P, L, P, L, I, I, P, P, L, P, L, P, S, P]),
+    "vitmi_gemm_workspace_size": (S, [I, I, I, L, L, L, I]),
+    "vitmi_linear_fwd": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P]),
+    "vitmi_linear_dgrad": (I, [I, L, L, L, P, P, P, I, I, P, P]),
+    "vitmi_linear_wgrad": (I, [I, L, L, L, P, P, P, P, S, P]),
+    "vitmi_linear_wgrad_workspace_size": (S, [I, L, L, L]),
+    "vitmi_bias_grad": (I, [I, L, L, P, L, P, P, S, P]),
+    "vitmi_bias_grad_workspace_size": (S, [L, L]),
+    "vitmi_layernorm_fwd": (I, [L, I, P, L, P, P, F, P, I, L, P, P, P]),
+    "vitmi_layernorm_bwd": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, P, P, S, P]),
+    "vitmi_layernorm_bwd_workspace_size": (S, [L, I]),
+    "vitmi_attention_fwd": (I, [I, I, I, I, I, F, P, P, P, P]),
+    "vitmi_attention_bwd": (I, [I, I, I, I, I, F, P, P, P, P, P, P, S, P]),
+    "vitmi_attention_bwd_workspace_size": (S, [I, I, I]),
+    "vitmi_patch_im2col": (I, [I, I, I, I, I, P, P, P]),
+    "vitmi_tokens_assemble": (I, [I, I, I, P, P, P, P, P]),
+    "vitmi_tokens_assemble_bwd": (I, [I, I, I, P, P, P, P, P, P]),
+    "vitmi_head_fwd": (I, [I, I, I, P, L, P, P, P, P]),
+    "vitmi_head_bwd": (I, [I, I, I, P, P, L, P, P, P, P, P]),
+    "vitmi_loss_fwd_bwd": (I, [I, I, I, P, P, P, P, P]),
+    "vitmi_cast_f32_bf16": (I, [L, P, P, P]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"vitmi: native library not built ({LIB_PATH}); run "
+                "`make -C transformer-stm_amd` or __graft_entry__.build()")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().vitmi_last_error().decode(errors="replace")
+        raise RuntimeError(f"vitmi {what} failed (code {rc}): {msg}")
+
+
+def exported_symbols():
+    return list(SIGNATURES)

@@ -1,0 +1,619 @@
+"""nn.Module API of the MI355X ViT path.
+
+Module tree and names follow the reference's layers (Keras ``ConvEmbed`` /
+``ConvAttention`` / ``ConvTransformerBlock`` / ``create_cvt_model``,
+``models/CvT(Par).py:194-354``) in the nn.Module form of the vendored Microsoft
+CvT (``old_codes/MS_CvT.py``: ``Mlp`` :53, ``Attention`` :77, ``Block`` :289,
+``ConvEmbed`` :336, ``VisionTransformer`` :372, head :605-623):
+
+    VisionTransformer(cfg)
+      patch_embed: ConvEmbed      (.proj Conv2d-shaped params, optional .norm)
+      cls_token, pos_embed
+      blocks[i]: Block            (.norm1, .attn: Attention(.qkv, .proj), .norm2, .mlp: Mlp(.fc1, .fc2))
+      norm: LayerNorm, head: Linear
+
+Every forward and backward runs the hand-written gfx950 kernels of libvitmi.so
+through fused ``torch.autograd.Function``s (one per block: LN1 -> QKV -> attention
+-> out-proj + residual -> LN2 -> fc1 + GELU -> fc2 + residual).  Parameters are
+ordinary fp32 ``nn.Parameter``s, so ``torch.optim``, ``state_dict`` and the DP
+reducer work unchanged.  Parameter gradients are accumulated (+=) by the kernels
+directly into ``param.grad`` (fp32); the autograd Functions return ``None`` for
+parameters.  In ``bf16`` mode GEMM/attention operands are bf16 (fp32 accumulate,
+fp32 residual stream, LN statistics, softmax and head); in ``fp32`` mode every
+product is exact fp32 (f32-input MFMA).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .config import ViTConfig
+
+Tensor = torch.Tensor
+F32 = torch.float32
+
+# bf16 copies of dx produced by a backward, keyed by the fp32 tensor's address, so
+# the next backward up the chain does not re-cast its incoming gradient.
+_LP_STASH: Dict[int, Tensor] = {}
+
+
+def _grad(p: nn.Parameter) -> Tensor:
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+def _lp(mod: nn.Module, p: Tensor, T: torch.dtype) -> Tensor:
+    """Operand copy of a weight in the compute dtype."""
+    if T == F32:
+        return p.detach()
+    arena = getattr(mod, "_arena", None)
+    if arena is not None:
+        return arena.lp(p)
+    return ops.cast_bf16(p.detach().contiguous())
+
+
+def _take_lp(g: Tensor, T: torch.dtype) -> Tensor:
+    if T == F32:
+        return g
+    lp = _LP_STASH.pop(g.data_ptr(), None)
+    if lp is not None and lp.shape == g.shape:
+        return lp
+    return ops.cast_bf16(g.contiguous())
+
+
+def _stash(g: Tensor, lp: Optional[Tensor]) -> None:
+    if lp is not None:
+        _LP_STASH[g.data_ptr()] = lp
+
+
+def _check_cuda(x: Tensor):
+    if not x.is_cuda:
+        raise RuntimeError("vitmi modules run only on the GPU (HIP); there is no CPU path")
+
+
+# ======================================================================= leaves
+class LayerNorm(nn.Module):
+    """layers.LayerNormalization(epsilon=eps) over the last dim (models/CvT(Par).py:248)."""
+
+    def __init__(self, dim: int, eps: float = 1e-6):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.bias = nn.Parameter(torch.zeros(dim))
+
+    def forward(self, x: Tensor) -> Tensor:
+        _check_cuda(x)
+        return _LayerNormFn.apply(x, self, self.weight, self.bias)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mod, w, b):
+        xs = x.contiguous().float()
+        y, mean, rstd = ops.layernorm_fwd(xs, w, b, mod.eps, F32)
+        ctx.save_for_backward(xs, mean, rstd)
+        ctx.mod = mod
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, mean, rstd = ctx.saved_tensors
+        mod = ctx.mod
+        dx, _ = ops.layernorm_bwd(dy.contiguous().float(), xs, mean, rstd, mod.weight,
+                                  _grad(mod.weight), _grad(mod.bias))
+        return dx.view(xs.shape), None, None, None
+
+
+class Linear(nn.Linear):
+    """Parameter container with nn.Linear's names/shapes (keras Dense); the math runs in
+    the fused Functions below or, standalone, through vitmi GEMMs."""
+
+    def forward(self, x: Tensor) -> Tensor:  # standalone use: fp32 GEMM
+        _check_cuda(x)
+        return _LinearFn.apply(x, self, self.weight, self.bias)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mod, w, b):
+        xs = x.contiguous().float()
+        y = ops.linear_fwd(xs.view(-1, xs.shape[-1]), w.detach(), b, F32)
+        ctx.save_for_backward(xs)
+        ctx.mod = mod
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xs,) = ctx.saved_tensors
+        mod = ctx.mod
+        dy2 = dy.contiguous().float().view(-1, dy.shape[-1])
+        x2 = xs.view(-1, xs.shape[-1])
+        dx = ops.linear_dgrad(dy2, mod.weight.detach(), F32)
+        ops.linear_wgrad(dy2, x2, _grad(mod.weight))
+        if mod.bias is not None:
+            ops.bias_grad(dy2, _grad(mod.bias))
+        return dx.view(xs.shape), None, None, None
+
+
+# ======================================================================= attention / MLP
+class Attention(nn.Module):
+    """ConvAttention with identity ('linear') projections (models/CvT(Par).py:115-191):
+    fused Q/K/V linear [D -> 3D], softmax(QK^T * scale) V, out-projection.
+    ``forward(x, h, w)`` mirrors old_codes/MS_CvT.py:190 (h, w unused for 'linear')."""
+
+    def __init__(self, dim: int, num_heads: int, qkv_bias: bool = True, attn_scale: str = "head",
+                 dtype: str = "bf16"):
+        super().__init__()
+        if dim % num_heads or dim // num_heads != 64:
+            raise ValueError("vitmi Attention needs head_dim == 64")
+        self.dim, self.num_heads = dim, num_heads
+        self.scale = (dim // num_heads) ** -0.5 if attn_scale == "head" else dim ** -0.5
+        self.qkv = Linear(dim, 3 * dim, bias=qkv_bias)
+        self.proj = Linear(dim, dim)
+        self.dtype = dtype
+
+    def forward(self, x: Tensor, h: Optional[int] = None, w: Optional[int] = None) -> Tensor:
+        _check_cuda(x)
+        return _AttentionFn.apply(x, self, *self._params())
+
+    def _params(self):
+        return [p for p in (self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias) if p is not None]
+
+
+class _AttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        T = ops.torch_dtype(mod.dtype)
+        B, N, D = x.shape
+        x2 = x.contiguous().float().view(B * N, D)
+        xo = x2 if T == F32 else ops.cast_bf16(x2)
+        wq, wo = _lp(mod, mod.qkv.weight, T), _lp(mod, mod.proj.weight, T)
+        qkv = ops.linear_fwd(xo, wq, mod.qkv.bias, T)
+        o, lse = ops.attention_fwd(qkv, B, N, mod.num_heads, mod.scale)
+        y = ops.linear_fwd(o, wo, mod.proj.bias, F32)
+        ctx.save_for_backward(xo, qkv, o, lse, wq, wo)
+        ctx.mod, ctx.shape = mod, (B, N, D)
+        return y.view(B, N, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xo, qkv, o, lse, wq, wo = ctx.saved_tensors
+        mod, (B, N, D) = ctx.mod, ctx.shape
+        T = xo.dtype
+        g = dy.contiguous().float().view(B * N, D)
+        g_lp = _take_lp(g, T)
+        do = ops.linear_dgrad(g_lp, wo, T)
+        ops.linear_wgrad(g_lp, o, _grad(mod.proj.weight))
+        ops.bias_grad(g_lp, _grad(mod.proj.bias))
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, mod.num_heads, mod.scale)
+        dx = ops.linear_dgrad(dqkv, wq, F32)
+        ops.linear_wgrad(dqkv, xo, _grad(mod.qkv.weight))
+        if mod.qkv.bias is not None:
+            ops.bias_grad(dqkv, _grad(mod.qkv.bias))
+        return (dx.view(B, N, D), None) + (None,) * len(mod._params())
+
+
+class Mlp(nn.Module):
+    """Dense(hidden, exact GELU) -> Dense(out)  (models/CvT(Par).py:253-258; MS_CvT.py:53-74)."""
+
+    def __init__(self, in_features: int, hidden_features: int, dtype: str = "bf16"):
+        super().__init__()
+        self.fc1 = Linear(in_features, hidden_features)
+        self.fc2 = Linear(hidden_features, in_features)
+        self.dtype = dtype
+
+    def forward(self, x: Tensor) -> Tensor:
+        _check_cuda(x)
+        return _MlpFn.apply(x, self, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
+
+
+class _MlpFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        T = ops.torch_dtype(mod.dtype)
+        shp = x.shape
+        x2 = x.contiguous().float().view(-1, shp[-1])
+        xo = x2 if T == F32 else ops.cast_bf16(x2)
+        w1, w2 = _lp(mod, mod.fc1.weight, T), _lp(mod, mod.fc2.weight, T)
+        a, u = ops.linear_fwd(xo, w1, mod.fc1.bias, T, ops.EPI_BIAS_GELU)
+        y = ops.linear_fwd(a, w2, mod.fc2.bias, F32)
+        ctx.save_for_backward(xo, a, u, w1, w2)
+        ctx.mod, ctx.shape = mod, shp
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xo, a, u, w1, w2 = ctx.saved_tensors
+        mod = ctx.mod
+        T = xo.dtype
+        g = dy.contiguous().float().view(-1, dy.shape[-1])
+        g_lp = _take_lp(g, T)
+        du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u)
+        ops.linear_wgrad(g_lp, a, _grad(mod.fc2.weight))
+        ops.bias_grad(g_lp, _grad(mod.fc2.bias))
+        dx = ops.linear_dgrad(du, w1, F32)
+        ops.linear_wgrad(du, xo, _grad(mod.fc1.weight))
+        ops.bias_grad(du, _grad(mod.fc1.bias))
+        return (dx.view(ctx.shape), None, None, None, None, None)
+
+
+# ======================================================================= block
+class Block(nn.Module):
+    """Pre-LN transformer block ``x += Attn(LN1(x)); x += MLP(LN2(x))``
+    (ConvTransformerBlock.call, models/CvT(Par).py:261-289; Block.forward, MS_CvT.py:325-333).
+    ``tie_norms=True`` reproduces the Keras model's single ``norm1`` used twice (:248,272,278)."""
+
+    def __init__(self, dim: int, num_heads: int, mlp_ratio: float = 4.0, qkv_bias: bool = True,
+                 eps: float = 1e-6, attn_scale: str = "head", tie_norms: bool = False, dtype: str = "bf16"):
+        super().__init__()
+        self.norm1 = LayerNorm(dim, eps)
+        self.attn = Attention(dim, num_heads, qkv_bias, attn_scale, dtype)
+        self.tie_norms = tie_norms
+        if not tie_norms:
+            self.norm2 = LayerNorm(dim, eps)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio), dtype)
+        self.dtype = dtype
+        self.eps = eps
+
+    @property
+    def _norm2(self) -> LayerNorm:
+        return self.norm1 if self.tie_norms else self.norm2
+
+    def forward(self, x: Tensor, h: Optional[int] = None, w: Optional[int] = None) -> Tensor:
+        _check_cuda(x)
+        return _BlockFn.apply(x, self, *self.parameters())
+
+
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, blk, *params):
+        T = ops.torch_dtype(blk.dtype)
+        B, N, D = x.shape
+        M = B * N
+        H = blk.attn.num_heads
+        x2 = x.contiguous().view(M, D)
+        assert x2.dtype == F32
+        n1, n2 = blk.norm1, blk._norm2
+        a_ = blk.attn
+        wq, wo = _lp(blk, a_.qkv.weight, T), _lp(blk, a_.proj.weight, T)
+        w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
+        h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
+        qkv = ops.linear_fwd(h1, wq, a_.qkv.bias, T)
+        o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
+        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2)
+        h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
+        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU)
+        out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
+        ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
+        ctx.blk, ctx.shape = blk, (B, N, D)
+        return out.view(B, N, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2) = ctx.saved_tensors
+        blk, (B, N, D) = ctx.blk, ctx.shape
+        M = B * N
+        T = h1.dtype
+        lpT = None if T == F32 else T
+        n1, n2 = blk.norm1, blk._norm2
+        a_, mlp = blk.attn, blk.mlp
+        g2 = dout.contiguous().view(M, D)
+        g2_lp = _take_lp(g2, T)
+        # MLP branch
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u)
+        ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
+        ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
+        dh2 = ops.linear_dgrad(du, w1, F32)
+        ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
+        ops.bias_grad(du, _grad(mlp.fc1.bias))
+        dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias),
+                                        dres=g2, lp_dtype=lpT)
+        if dx1_lp is None:
+            dx1_lp = dx1
+        # attention branch
+        do = ops.linear_dgrad(dx1_lp, wo, T)
+        ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
+        ops.bias_grad(dx1_lp, _grad(a_.proj.bias))
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale)
+        dh1 = ops.linear_dgrad(dqkv, wq, F32)
+        ops.linear_wgrad(dqkv, h1, _grad(a_.qkv.weight))
+        if a_.qkv.bias is not None:
+            ops.bias_grad(dqkv, _grad(a_.qkv.bias))
+        dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
+                                      dres=dx1, lp_dtype=lpT)
+        _stash(dx, dx_lp)
+        hook = getattr(blk, "_grad_ready_hook", None)
+        if hook is not None:
+            hook(blk)
+        return (dx.view(B, N, D), None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+# ======================================================================= embedding
+class ConvEmbed(nn.Module):
+    """Conv2D(embed_dim, k=patch, s=patch) patch embedding (models/CvT(Par).py:194-217;
+    old_codes/MS_CvT.py:336-369).  ``forward(x[B,C,H,W]) -> [B,D,h,w]`` like MS_CvT."""
+
+    def __init__(self, patch_size: int = 16, in_chans: int = 3, embed_dim: int = 768,
+                 norm: bool = False, eps: float = 1e-6, dtype: str = "bf16"):
+        super().__init__()
+        self.patch_size = patch_size
+        self.proj = nn.Conv2d(in_chans, embed_dim, kernel_size=patch_size, stride=patch_size)
+        self.norm = LayerNorm(embed_dim, eps) if norm else None
+        self.dtype = dtype
+
+    def forward(self, x: Tensor) -> Tensor:
+        _check_cuda(x)
+        B, C, S, _ = x.shape
+        G = S // self.patch_size
+        tok = _EmbedFn.apply(x, self, None, None, *self.parameters())  # [B, 1+np, D] w/o cls
+        return tok[:, 1:].transpose(1, 2).reshape(B, -1, G, G)
+
+
+class _EmbedFn(torch.autograd.Function):
+    """im2col -> patch GEMM (+bias) [-> LN] -> cls concat + pos-embed, one token tensor."""
+
+    @staticmethod
+    def forward(ctx, img, emb, cls, pos, *params):
+        T = ops.torch_dtype(emb.dtype)
+        B, C, S, _ = img.shape
+        P = emb.patch_size
+        G = S // P
+        np_ = G * G
+        D = emb.proj.weight.shape[0]
+        patches = ops.patch_im2col(img.contiguous().float(), P, T)
+        w = _lp(emb, emb.proj.weight, T).reshape(D, -1)
+        conv = ops.linear_fwd(patches, w, emb.proj.bias, F32)
+        saved = [patches]
+        if emb.norm is not None:
+            y, mean, rstd = ops.layernorm_fwd(conv, emb.norm.weight, emb.norm.bias, emb.norm.eps, F32)
+            saved += [conv, mean, rstd]
+            conv = y
+        x = ops.tokens_assemble(conv, B, np_, cls.detach().reshape(-1) if cls is not None else None,
+                                pos.detach().reshape(-1) if pos is not None else None)
+        ctx.save_for_backward(*saved)
+        ctx.emb, ctx.cls, ctx.pos, ctx.dims = emb, cls, pos, (B, np_, D)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        emb, cls, pos, (B, np_, D) = ctx.emb, ctx.cls, ctx.pos, ctx.dims
+        saved = ctx.saved_tensors
+        patches = saved[0]
+        T = patches.dtype
+        lpT = None if T == F32 else T
+        dx = dx.contiguous()
+        dcls = _grad(cls).view(-1) if cls is not None else None
+        dpos = _grad(pos).view(-1) if pos is not None else None
+        if emb.norm is not None:
+            conv, mean, rstd = saved[1:]
+            dy, _ = ops.tokens_assemble_bwd(dx, B, np_, True, None, dcls, dpos)
+            dconv, dconv_lp = ops.layernorm_bwd(dy, conv, mean, rstd, emb.norm.weight,
+                                                _grad(emb.norm.weight), _grad(emb.norm.bias), lp_dtype=lpT)
+            g = dconv_lp if dconv_lp is not None else dconv
+        else:
+            dtok, dtok_lp = ops.tokens_assemble_bwd(dx, B, np_, T == F32, lpT, dcls, dpos)
+            g = dtok_lp if dtok_lp is not None else dtok
+        ops.linear_wgrad(g, patches, _grad(emb.proj.weight).view(D, -1))
+        ops.bias_grad(g, _grad(emb.proj.bias))
+        hook = getattr(emb, "_grad_ready_hook", None)
+        if hook is not None:
+            hook(emb)
+        n_params = len(ctx.needs_input_grad) - 4
+        return (None, None, None, None) + (None,) * n_params
+
+
+# ======================================================================= head + loss
+class _HeadFn(torch.autograd.Function):
+    """LN(cls) -> Dense(num_classes)  (models/CvT(Par).py:326-329,350)."""
+
+    @staticmethod
+    def forward(ctx, x, model, *params):
+        norm, head = model.norm, model.head
+        xc = x[:, 0]                                      # strided rows [B, D]
+        y, mean, rstd = ops.layernorm_fwd(xc, norm.weight, norm.bias, norm.eps, F32)
+        logits = ops.head_fwd(y, head.weight.detach(), head.bias)
+        ctx.save_for_backward(x, y, mean, rstd)
+        ctx.model = model
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        _LP_STASH.clear()
+        x, y, mean, rstd = ctx.saved_tensors
+        model = ctx.model
+        norm, head = model.norm, model.head
+        dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), _grad(head.weight),
+                          _grad(head.bias) if head.bias is not None else None)
+        dx = torch.zeros_like(x)
+        ops.layernorm_bwd(dy, x[:, 0], mean, rstd, norm.weight, _grad(norm.weight), _grad(norm.bias),
+                          dx=dx[:, 0])
+        hook = getattr(model, "_head_ready_hook", None)
+        if hook is not None:
+            hook()
+        return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+class _LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, kind):
+        loss, dl = ops.loss_fwd_bwd(logits.float(), target, kind)
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return dl * g, None, None
+
+
+def cross_entropy(logits: Tensor, target: Tensor) -> Tensor:
+    """Mean softmax cross-entropy on the vitmi loss kernel."""
+    return _LossFn.apply(logits, target, ops.LOSS_CE)
+
+
+def mse_loss(logits: Tensor, target: Tensor) -> Tensor:
+    """Keras 'mean_squared_error' (models/CvT(Par).py:464-466) on the vitmi loss kernel."""
+    t = target.reshape(logits.shape[0], -1)
+    return _LossFn.apply(logits, t, ops.LOSS_MSE)
+
+
+# ======================================================================= parameter arena
+class ParamArena:
+    """All parameters of a model as views into ONE fp32 buffer (plus one fp32 gradient
+    buffer and one bf16 operand shadow with the same offsets), laid out in the order
+    the backward finishes them (head first, patch-embed last) so DP buckets become
+    ready front to back."""
+
+    ALIGN = 64  # elements: 256 B fp32 / 128 B bf16
+
+    def __init__(self, ordered: List[nn.Parameter], device, want_lp: bool):
+        self.params = ordered
+        offs, n = [], 0
+        for p in ordered:
+            offs.append(n)
+            n += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.numel = n
+        self.offsets = {id(p): o for p, o in zip(ordered, offs)}
+        self.flat = torch.zeros(n, dtype=F32, device=device)
+        self.grad = torch.zeros(n, dtype=F32, device=device)
+        self.flat_lp = torch.empty(n, dtype=torch.bfloat16, device=device) if want_lp else None
+        with torch.no_grad():
+            for p, o in zip(ordered, offs):
+                self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + p.numel()].view(p.shape)
+        self._grad_views = [self.grad[o:o + p.numel()].view(p.shape) for p, o in zip(ordered, offs)]
+
+    def owns(self, ps: List[nn.Parameter]) -> bool:
+        for p in ps:
+            o = self.offsets.get(id(p))
+            if o is None or p.data_ptr() != self.flat.data_ptr() + 4 * o:
+                return False
+        return True
+
+    def view(self, buf: Tensor, p: Tensor) -> Tensor:
+        o = self.offsets[id(p)]
+        return buf[o:o + p.numel()].view(p.shape)
+
+    def lp(self, p: Tensor) -> Tensor:
+        return self.view(self.flat_lp, p)
+
+    def refresh_lp(self) -> None:
+        if self.flat_lp is not None:
+            ops.cast_bf16(self.flat, self.flat_lp)
+
+    def bind_grads(self) -> None:
+        ps, views = self.params, self._grad_views
+        if all(p.grad is None for p in ps):
+            self.grad.zero_()
+            for p, v in zip(ps, views):
+                p.grad = v
+            return
+        for p, v in zip(ps, views):
+            g = p.grad
+            if g is None:
+                v.zero_()
+                p.grad = v
+            elif g.data_ptr() != v.data_ptr():
+                v.copy_(g)
+                p.grad = v
+
+
+# ======================================================================= model
+class VisionTransformer(nn.Module):
+    """One-stage ViT in the reference's vocabulary: ConvEmbed(P, s=P) -> depth x
+    ConvTransformerBlock(qkv_method='linear') -> LN(cls) -> Dense(num_classes)
+    (create_cvt_model, models/CvT(Par).py:292-354; MS_CvT VisionTransformer :372-488 +
+    head :605-623).  ``forward(x) -> logits``."""
+
+    def __init__(self, cfg: ViTConfig):
+        super().__init__()
+        if not cfg.with_cls_token:
+            raise NotImplementedError("vitmi: only the cls-token head is implemented")
+        self.cfg = cfg
+        D = cfg.embed_dim
+        self.patch_embed = ConvEmbed(cfg.patch_size, cfg.in_chans, D, cfg.embed_norm, cfg.ln_eps, cfg.dtype)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, D))
+        self.pos_embed = nn.Parameter(torch.zeros(1, cfg.seq_len, D)) if cfg.pos_embed else None
+        self.blocks = nn.ModuleList([
+            Block(D, cfg.num_heads, cfg.mlp_ratio, cfg.qkv_bias, cfg.ln_eps, cfg.attn_scale, cfg.tie_norms,
+                  cfg.dtype) for _ in range(cfg.depth)])
+        self.norm = LayerNorm(D, cfg.ln_eps)
+        self.head = Linear(D, cfg.num_classes)
+        self._arena: Optional[ParamArena] = None
+        self.reset_parameters()
+
+    # -- init: trunc_normal(.02) weights, zero biases, LN (1, 0)  (old_codes/MS_CvT.py:437-454)
+    def reset_parameters(self, seed: Optional[int] = None) -> None:
+        g = torch.Generator().manual_seed(seed) if seed is not None else None
+        with torch.no_grad():
+            for name, p in self.named_parameters():
+                if "norm" in name:
+                    p.fill_(1.0 if name.endswith("weight") else 0.0)
+                elif name.endswith("bias"):
+                    p.zero_()
+                else:
+                    t = torch.randn(p.shape, generator=g).clamp_(-2, 2) * 0.02
+                    p.copy_(t)
+
+    def named_param_dict(self) -> Dict[str, nn.Parameter]:
+        return dict(self.named_parameters())
+
+    def load_param_dict(self, d: Dict[str, Tensor]) -> None:
+        mine = self.named_param_dict()
+        missing = set(mine) - set(d)
+        if missing:
+            raise KeyError(f"missing parameters: {sorted(missing)[:5]}")
+        with torch.no_grad():
+            for k, p in mine.items():
+                p.copy_(d[k].reshape(p.shape).to(p.device, p.dtype))
+
+    # -- arena
+    def backward_order(self) -> List[nn.Parameter]:
+        order: List[nn.Parameter] = []
+        order += list(self.head.parameters()) + list(self.norm.parameters())
+        for blk in reversed(self.blocks):
+            order += list(blk.parameters())
+        order += list(self.patch_embed.parameters())
+        order += [self.cls_token] + ([self.pos_embed] if self.pos_embed is not None else [])
+        assert len(order) == len(list(self.parameters()))
+        return order
+
+    def arena(self) -> ParamArena:
+        ps = self.backward_order()
+        if self._arena is None or not self._arena.owns(ps) or self._arena.flat.device != ps[0].device:
+            self._arena = ParamArena(ps, ps[0].device, self.cfg.dtype == "bf16")
+            for m in self.modules():
+                if m is not self:
+                    object.__setattr__(m, "_arena", self._arena)
+        return self._arena
+
+    # -- forward
+    def forward_features(self, x: Tensor) -> Tensor:
+        """Token stream after the last block, [B, N, D] fp32."""
+        _check_cuda(x)
+        arena = self.arena()
+        arena.refresh_lp()
+        if torch.is_grad_enabled():
+            arena.bind_grads()
+        pe = self.patch_embed
+        t = _EmbedFn.apply(x, pe, self.cls_token, self.pos_embed, *pe.parameters())
+        for blk in self.blocks:
+            t = _BlockFn.apply(t, blk, *blk.parameters())
+        return t
+
+    def forward(self, x: Tensor) -> Tensor:
+        t = self.forward_features(x)
+        return _HeadFn.apply(t, self, *self.norm.parameters(), *self.head.parameters())
+
+
+def build_model(cfg: ViTConfig, device="cuda") -> VisionTransformer:
+    return VisionTransformer(cfg).to(device)
+
+
+__all__ = ["LayerNorm", "Linear", "Attention", "Mlp", "Block", "ConvEmbed", "VisionTransformer",
+           "cross_entropy", "mse_loss", "build_model", "ParamArena"]
+

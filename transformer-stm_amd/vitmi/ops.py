@@ -1,0 +1,271 @@
+"""Tensor-level wrappers over the C ABI (include/vitmi.h).
+
+Every function here launches hand-written gfx950 kernels from libvitmi.so on
+torch's current HIP stream; torch only allocates the buffers (caching
+allocator).  Inputs must be CUDA(HIP) tensors; there is no CPU or eager
+fallback — a missing library or a bad shape raises.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._lib import check, lib
+
+Tensor = torch.Tensor
+
+F32, BF16 = 0, 1
+EPI_STORE, EPI_BIAS_GELU, EPI_RESIDUAL, EPI_DGELU, EPI_ACCUM = 0, 1, 2, 3, 4
+LOSS_CE, LOSS_MSE = 0, 1
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dt(t: torch.dtype) -> int:
+    try:
+        return _DT[t]
+    except KeyError:
+        raise TypeError(f"vitmi: unsupported dtype {t}") from None
+
+
+def torch_dtype(name: str) -> torch.dtype:
+    return {"bf16": torch.bfloat16, "fp32": torch.float32}[name]
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+# Optional live probe: HIP events around every linear_fwd launch of one (M, N, K)
+# shape, recorded on the stream the kernel runs on (bench.py's roofline leg).
+_PROBE = None
+
+
+def set_probe(key):
+    """key = (M, N, K) to time, or None to disable.  Returns the event-pair list."""
+    global _PROBE
+    _PROBE = None if key is None else {"key": tuple(key), "events": []}
+    return None if _PROBE is None else _PROBE["events"]
+
+
+def _p(t: Optional[Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("vitmi: tensors must live on the GPU (no CPU fallback)")
+    return t.data_ptr()
+
+
+def _ws(nbytes: int, like: Tensor) -> Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
+
+
+def _rows(t: Tensor) -> Tuple[int, int]:
+    """(rows, row stride) of a tensor viewed as [rows, last-dim] with unit inner stride."""
+    if t.stride(-1) != 1:
+        raise RuntimeError("vitmi: last dim must be contiguous")
+    return t.numel() // t.shape[-1], t.stride(-2) if t.dim() > 1 else t.shape[-1]
+
+
+# ---------------------------------------------------------------- GEMM
+def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dtype,
+               epilogue: int = EPI_STORE, residual: Optional[Tensor] = None):
+    """y = x W^T + b (+GELU, +residual).  x [M,K], w [N,K] (same dtype).  Returns y
+    (and the pre-activation for EPI_BIAS_GELU)."""
+    assert x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype
+    M, K = x.numel() // x.shape[-1], x.shape[-1]
+    N = w.shape[0]
+    assert w.shape[1] == K
+    y = torch.empty(*x.shape[:-1], N, dtype=out_dtype, device=x.device)
+    aux = None
+    if epilogue == EPI_BIAS_GELU:
+        aux = torch.empty(*x.shape[:-1], N, dtype=x.dtype, device=x.device)
+    if residual is not None:
+        assert residual.is_contiguous() and residual.dtype == torch.float32
+    probe = _PROBE is not None and _PROBE["key"] == (M, N, K)
+    if probe:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    check(lib().vitmi_linear_fwd(dt(x.dtype), M, N, K, _p(x), _p(w), _p(bias), _p(y), dt(out_dtype),
+                                 epilogue, _p(aux), _p(residual), _s()), "linear_fwd")
+    if probe:
+        e1.record()
+        _PROBE["events"].append((e0, e1))
+    return (y, aux) if epilogue == EPI_BIAS_GELU else y
+
+
+def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = EPI_STORE,
+                 aux: Optional[Tensor] = None) -> Tensor:
+    """dx[M,K] = dy[M,N] W[N,K] (optionally * gelu'(aux))."""
+    assert dy.is_contiguous() and w.is_contiguous() and dy.dtype == w.dtype
+    M, N = dy.numel() // dy.shape[-1], dy.shape[-1]
+    K = w.shape[1]
+    dx = torch.empty(*dy.shape[:-1], K, dtype=out_dtype, device=dy.device)
+    check(lib().vitmi_linear_dgrad(dt(dy.dtype), M, N, K, _p(dy), _p(w), _p(dx), dt(out_dtype),
+                                   epilogue, _p(aux), _s()), "linear_dgrad")
+    return dx
+
+
+def linear_wgrad(dy: Tensor, x: Tensor, dw: Tensor) -> None:
+    """dw[N,K] (fp32) += dy[M,N]^T x[M,K]."""
+    assert dy.is_contiguous() and x.is_contiguous() and dy.dtype == x.dtype
+    assert dw.dtype == torch.float32 and dw.is_contiguous()
+    M, N, K = dy.numel() // dy.shape[-1], dy.shape[-1], x.shape[-1]
+    ws_n = lib().vitmi_linear_wgrad_workspace_size(dt(dy.dtype), M, N, K)
+    ws = _ws(ws_n, dy)
+    check(lib().vitmi_linear_wgrad(dt(dy.dtype), M, N, K, _p(dy), _p(x), _p(dw), _p(ws), ws.numel(),
+                                   _s()), "linear_wgrad")
+
+
+def bias_grad(dy: Tensor, db: Tensor) -> None:
+    """db[N] (fp32) += sum over rows of dy[..., N]."""
+    M, ld = _rows(dy)
+    N = dy.shape[-1]
+    ws = _ws(lib().vitmi_bias_grad_workspace_size(M, N), dy)
+    check(lib().vitmi_bias_grad(dt(dy.dtype), M, N, _p(dy), ld, _p(db), _p(ws), ws.numel(), _s()),
+          "bias_grad")
+
+
+def gemm(a: Tensor, b: Tensor, a_kmajor: bool, b_kmajor: bool, M: int, N: int, K: int,
+         out: Tensor, epilogue: int = EPI_STORE, bias=None, aux=None, residual=None) -> Tensor:
+    """Generic C[M,N] = A(m,k) B(k,n) (see vitmi_gemm in include/vitmi.h)."""
+    lda = a.stride(0)
+    ldb = b.stride(0)
+    ws_n = lib().vitmi_gemm_workspace_size(dt(a.dtype), int(a_kmajor), int(b_kmajor), M, N, K, epilogue)
+    ws = _ws(ws_n, a)
+    check(lib().vitmi_gemm(dt(a.dtype), int(a_kmajor), int(b_kmajor), M, N, K, _p(a), lda, _p(b), ldb,
+                           _p(out), out.stride(0), dt(out.dtype), epilogue, _p(bias), _p(aux),
+                           aux.stride(0) if aux is not None else 0, _p(residual),
+                           residual.stride(0) if residual is not None else 0, _p(ws), ws.numel(), _s()),
+          "gemm")
+    return out
+
+
+# ---------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.dtype):
+    """x fp32 [..., D] (rows may be strided) -> (y [rows, D] contiguous, mean, rstd)."""
+    assert x.dtype == torch.float32
+    M, ldx = _rows(x)
+    D = x.shape[-1]
+    y = torch.empty(M, D, dtype=out_dtype, device=x.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    check(lib().vitmi_layernorm_fwd(M, D, _p(x), ldx, _p(w), _p(b), float(eps), _p(y), dt(out_dtype), D,
+                                    _p(mean), _p(rstd), _s()), "layernorm_fwd")
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
+                  dgamma: Optional[Tensor], dbeta: Optional[Tensor], dres: Optional[Tensor] = None,
+                  dx: Optional[Tensor] = None, lp_dtype: Optional[torch.dtype] = None):
+    """dx = dres + LN'(dy); dgamma/dbeta (fp32) +=.  Returns (dx fp32, dx_lp or None).
+
+    ``dx`` may be a pre-allocated (possibly row-strided) fp32 destination."""
+    M, ldy = _rows(dy)
+    _, ldx = _rows(x)
+    D = x.shape[-1]
+    if dx is None:
+        dx = torch.empty(M, D, dtype=torch.float32, device=x.device)
+    _, lddx = _rows(dx)
+    dx_lp = None
+    if lp_dtype is not None and lp_dtype != torch.float32:
+        dx_lp = torch.empty(M, D, dtype=lp_dtype, device=x.device)
+    ldres = _rows(dres)[1] if dres is not None else 0
+    ws = _ws(lib().vitmi_layernorm_bwd_workspace_size(M, D), x)
+    check(lib().vitmi_layernorm_bwd(M, D, _p(dy), dt(dy.dtype), ldy, _p(x), ldx, _p(mean), _p(rstd), _p(w),
+                                    _p(dres), ldres, _p(dx), lddx, _p(dx_lp), D, _p(dgamma), _p(dbeta),
+                                    _p(ws), ws.numel(), _s()), "layernorm_bwd")
+    return dx, dx_lp
+
+
+# ---------------------------------------------------------------- attention
+def attention_fwd(qkv: Tensor, B: int, N: int, H: int, scale: float):
+    """qkv [B*N, 3*H*64] -> (o [B*N, H*64], lse fp32 [B*H, N])."""
+    D3 = qkv.shape[-1]
+    D = D3 // 3
+    assert qkv.is_contiguous() and qkv.numel() == B * N * D3
+    o = torch.empty(B * N, D, dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty(B * H, N, dtype=torch.float32, device=qkv.device)
+    check(lib().vitmi_attention_fwd(dt(qkv.dtype), B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(lse),
+                                    _s()), "attention_fwd")
+    return o, lse
+
+
+def attention_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, B: int, N: int, H: int,
+                  scale: float) -> Tensor:
+    D = o.shape[-1]
+    assert do.is_contiguous() and do.dtype == qkv.dtype
+    dqkv = torch.empty_like(qkv)
+    ws = _ws(lib().vitmi_attention_bwd_workspace_size(B, N, H), qkv)
+    check(lib().vitmi_attention_bwd(dt(qkv.dtype), B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(do),
+                                    _p(lse), _p(dqkv), _p(ws), ws.numel(), _s()), "attention_bwd")
+    return dqkv
+
+
+# ---------------------------------------------------------------- patch embed / tokens
+def patch_im2col(img: Tensor, P: int, out_dtype: torch.dtype) -> Tensor:
+    B, C, S, S2 = img.shape
+    assert S == S2 and img.dtype == torch.float32 and img.is_contiguous()
+    G = S // P
+    out = torch.empty(B * G * G, C * P * P, dtype=out_dtype, device=img.device)
+    check(lib().vitmi_patch_im2col(dt(out_dtype), B, C, S, P, _p(img), _p(out), _s()), "patch_im2col")
+    return out
+
+
+def tokens_assemble(tok: Tensor, B: int, np_: int, cls: Optional[Tensor], pos: Optional[Tensor]) -> Tensor:
+    D = tok.shape[-1]
+    x = torch.empty(B, np_ + 1, D, dtype=torch.float32, device=tok.device)
+    check(lib().vitmi_tokens_assemble(B, np_, D, _p(tok), _p(cls), _p(pos), _p(x), _s()), "tokens_assemble")
+    return x
+
+
+def tokens_assemble_bwd(dx: Tensor, B: int, np_: int, want_f32: bool, lp_dtype: Optional[torch.dtype],
+                        dcls: Optional[Tensor], dpos: Optional[Tensor]):
+    D = dx.shape[-1]
+    dtok = torch.empty(B * np_, D, dtype=torch.float32, device=dx.device) if want_f32 else None
+    dtok_lp = None
+    if lp_dtype is not None and lp_dtype != torch.float32:
+        dtok_lp = torch.empty(B * np_, D, dtype=lp_dtype, device=dx.device)
+    check(lib().vitmi_tokens_assemble_bwd(B, np_, D, _p(dx.contiguous()), _p(dtok), _p(dtok_lp), _p(dcls),
+                                          _p(dpos), _s()), "tokens_assemble_bwd")
+    return dtok, dtok_lp
+
+
+# ---------------------------------------------------------------- head / loss / cast
+def head_fwd(y: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
+    B, D = y.shape
+    C = w.shape[0]
+    logits = torch.empty(B, C, dtype=torch.float32, device=y.device)
+    check(lib().vitmi_head_fwd(B, D, C, _p(y), y.stride(0), _p(w), _p(b), _p(logits), _s()), "head_fwd")
+    return logits
+
+
+def head_bwd(dlogits: Tensor, y: Tensor, w: Tensor, dw: Tensor, db: Optional[Tensor]) -> Tensor:
+    B, D = y.shape
+    C = w.shape[0]
+    dy = torch.empty(B, D, dtype=torch.float32, device=y.device)
+    check(lib().vitmi_head_bwd(B, D, C, _p(dlogits.contiguous()), _p(y), y.stride(0), _p(w), _p(dy), _p(dw),
+                               _p(db), _s()), "head_bwd")
+    return dy
+
+
+def loss_fwd_bwd(logits: Tensor, target: Tensor, kind: int):
+    B, C = logits.shape
+    loss = torch.empty((), dtype=torch.float32, device=logits.device)
+    dl = torch.empty_like(logits)
+    if kind == LOSS_CE:
+        target = target.to(torch.int64).contiguous()
+    else:
+        target = target.to(torch.float32).contiguous()
+    check(lib().vitmi_loss_fwd_bwd(kind, B, C, _p(logits.contiguous()), _p(target), _p(loss), _p(dl), _s()),
+          "loss")
+    return loss, dl
+
+
+def cast_bf16(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
+    assert src.dtype == torch.float32 and src.is_contiguous()
+    if dst is None:
+        dst = torch.empty(src.shape, dtype=torch.bfloat16, device=src.device)
+    check(lib().vitmi_cast_f32_bf16(src.numel(), _p(src), _p(dst), _s()), "cast")
+    return dst
