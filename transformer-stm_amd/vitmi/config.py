@@ -113,16 +113,16 @@ def preset(name: str, **kw) -> ViTConfig:
 
 # BASELINE.json configs (C1..C5)
 def config_c1(**kw) -> ViTConfig:
-    return preset("vit_tiny_16", img_size=64, num_classes=2, dtype="fp32", **kw)
+    return preset("vit_tiny_16", **{**dict(img_size=64, num_classes=2, dtype="fp32"), **kw})
 
 
 def config_c2(**kw) -> ViTConfig:
-    return preset("vit_small_16", img_size=224, num_classes=2, dtype="fp32", **kw)
+    return preset("vit_small_16", **{**dict(img_size=224, num_classes=2, dtype="fp32"), **kw})
 
 
 def config_c3(**kw) -> ViTConfig:
-    return preset("vit_base_16", img_size=224, num_classes=2, dtype="bf16", **kw)
+    return preset("vit_base_16", **{**dict(img_size=224, num_classes=2, dtype="bf16"), **kw})
 
 
 def config_c5(**kw) -> ViTConfig:
-    return preset("vit_large_16", img_size=384, num_classes=2, dtype="bf16", **kw)
+    return preset("vit_large_16", **{**dict(img_size=384, num_classes=2, dtype="bf16"), **kw})
