@@ -25,12 +25,21 @@ def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
 
 
 # ------------------------------------------------------------------ GEMM
+@pytest.fixture(params=[1, 2], ids=["tile128", "tile256"])
+def policy(request):
+    """Run each GEMM case through both kernels (vitmi_gemm_set_policy)."""
+    from vitmi._lib import lib
+    lib().vitmi_gemm_set_policy(request.param)
+    yield request.param
+    lib().vitmi_gemm_set_policy(0)
+
+
 FWD_SHAPES = [(197 * 3, 320, 192), (256, 384, 64), (1000, 2304, 768), (5, 64, 128)]
 
 
 @pytest.mark.parametrize("M,N,K", FWD_SHAPES)
 @pytest.mark.parametrize("T", [BF, torch.float32])
-def test_linear_fwd_store(M, N, K, T):
+def test_linear_fwd_store(M, N, K, T, policy):
     x, w, b = rnd(M, K, dtype=T, seed=1), rnd(N, K, dtype=T, seed=2, scale=0.05), rnd(N, seed=3)
     ref = x.float() @ w.float().t() + b
     y32 = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), torch.float32)
@@ -40,7 +49,7 @@ def test_linear_fwd_store(M, N, K, T):
 
 
 @pytest.mark.parametrize("T", [BF, torch.float32])
-def test_linear_fwd_gelu_and_residual(T):
+def test_linear_fwd_gelu_and_residual(T, policy):
     M, N, K = 394, 768, 192
     x, w, b = rnd(M, K, dtype=T, seed=4), rnd(N, K, dtype=T, seed=5, scale=0.05), rnd(N, seed=6)
     u_ref = x.float() @ w.float().t() + b
@@ -54,7 +63,7 @@ def test_linear_fwd_gelu_and_residual(T):
 
 @pytest.mark.parametrize("M,N,K", [(394, 768, 192), (197 * 4, 2304, 768), (64, 192, 576)])
 @pytest.mark.parametrize("T", [BF, torch.float32])
-def test_linear_dgrad(M, N, K, T):
+def test_linear_dgrad(M, N, K, T, policy):
     dy, w = rnd(M, N, dtype=T, seed=8), rnd(N, K, dtype=T, seed=9, scale=0.05)
     ref = dy.float() @ w.float()
     dx = ops.linear_dgrad(dy.to(DEV), w.to(DEV), torch.float32)
@@ -68,7 +77,7 @@ def test_linear_dgrad(M, N, K, T):
 
 @pytest.mark.parametrize("M,N,K", [(197 * 2, 384, 192), (4000, 384, 768), (50, 64, 64), (20000, 192, 576)])
 @pytest.mark.parametrize("T", [BF, torch.float32])
-def test_linear_wgrad_accumulates(M, N, K, T):
+def test_linear_wgrad_accumulates(M, N, K, T, policy):
     dy, x = rnd(M, N, dtype=T, seed=11), rnd(M, K, dtype=T, seed=12)
     prev = rnd(N, K, seed=13)
     ref = prev + dy.float().t() @ x.float()

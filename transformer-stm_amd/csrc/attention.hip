@@ -245,7 +245,10 @@ __global__ void attn_bwd_delta(const T* __restrict__ o, const T* __restrict__ do
 __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][Q|dO]
+  // [buf][Q tile | dO tile] 2 x 16 KiB, then [buf][lse*log2e | delta] 2 x 512 B (one array: the
+  // compiler must see a single LDS object next to the DMA, cdna_hip_programming.md §5 trap (a))
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192 + 2 * 512];
+  float* rowst = (float*)(smem + 32768);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int bh = blockIdx.y, b = bh / H, hd = bh % H;
@@ -261,6 +264,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
   __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
   const float* lse_bh = lse + (int64_t)bh * N;
   const float* del_bh = delta + (int64_t)bh * N;
+  // per-query row constants of tile t into rowst[buf]: q >= N get L2 = +inf -> p = 0
+  auto stage_rows = [&](int t, int buf) {
+    if (wave == 0) {
+      const int qi = t * 64 + lane;
+      rowst[buf * 128 + lane] = qi < N ? lse_bh[qi] * LOG2E : INFINITY;
+      rowst[buf * 128 + 64 + lane] = qi < N ? del_bh[qi] : 0.f;
+    }
+  };
 
   const int kw = blockIdx.x * 128 + wave * 32;
   const int key = kw + (lane & 31);
@@ -277,6 +288,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
   const int nt = (N + 63) / 64;
   stage_tile<4>(smem, rq, ldb, 0, wave, lane);
   stage_tile<4>(smem + 8192, rdo, ldo, 0, wave, lane);
+  stage_rows(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
@@ -288,8 +300,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
     }
     const char* qt = smem + buf * 16384;
     const char* dt_ = qt + 8192;
+    const float* rl = rowst + buf * 128;
     if (kw < N) {
-#pragma unroll
+#pragma unroll 1
       for (int u = 0; u < 2; ++u) {  // 32-query sub-tile
         f32x16 sa = zero16(), dp = zero16();
 #pragma unroll
@@ -298,14 +311,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
           dp = mfma32(frag_row(dt_, 32 * u, s, lane), vf[s], dp);  // dP[q][key]
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qi = t * 64 + 32 * u + acc_row(r, h);
-          const bool ok = qi < N;
-          const float L2 = ok ? lse_bh[qi] * LOG2E : 0.f;
-          const float dl = ok ? del_bh[qi] : 0.f;
-          const float p = ok ? exp2f(sa[r] * c2 - L2) : 0.f;
-          sa[r] = p;
-          dp[r] = p * (dp[r] - dl);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int q4 = 32 * u + 8 * g4 + 4 * h;           // rows acc_row(4*g4 + i, h) = q4 + i
+          const f32x4 L2 = *(const f32x4*)(rl + q4);
+          const f32x4 dl = *(const f32x4*)(rl + 64 + q4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = exp2f(sa[4 * g4 + i] * c2 - L2[i]);
+            sa[4 * g4 + i] = p;
+            dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
+          }
         }
         // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
 #pragma unroll
@@ -320,6 +335,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t + 1 < nt) stage_rows(t + 1, buf ^ 1);
     __syncthreads();
   }
   if (kw >= N || key >= N) return;
@@ -337,9 +353,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
 }
 
 // dQ: grid (ceil(N/128), B*H), wave w owns queries q0 = 128*bx + 32w .. +31.
+// Also produces delta[bh][q] = sum_d dO[q][d] O[q][d] (consumed here and by the dK/dV
+// kernel, which therefore runs after this one).
 __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
+    float scale) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][K|V]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -365,7 +384,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
   }
   const bool qok = q < N;
   const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : 0.f;
-  const float dl = qok ? delta[(int64_t)bh * N + q] : 0.f;
+  // delta: this lane holds d = 16s + 8h + j of dO[q]; the xor-32 partner the other half
+  float dl;
+  {
+    __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 ov = load_row16(ro, (uint32_t)((int64_t)q * ldo + (16 * s + 8 * h) * 2));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)ov[j] * (float)df[s][j];
+    }
+    dl = part + __shfl_xor(part, 32, 64);
+    if (qok && h == 0) delta[(int64_t)bh * N + q] = dl;
+  }
   const float c2 = scale * LOG2E;
   f32x16 dqt[2] = {zero16(), zero16()};
 
@@ -630,12 +662,11 @@ extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float
   const int64_t rows = (int64_t)B * N * H;
   const int blocks = (int)((rows + 255) / 256);
   if (dtype == VITMI_BF16) {
-    hipLaunchKernelGGL(attn_bwd_delta<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)o,
-                       (const bf16*)dout, delta, B * N, N, H);
+    // dQ first: it also writes delta, which the dK/dV kernel consumes
     dim3 grid((N + 127) / 128, B * H);
+    hipLaunchKernelGGL(attn_bwd_dq_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)o,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale);
     hipLaunchKernelGGL(attn_bwd_dkv_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
-                       lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
-    hipLaunchKernelGGL(attn_bwd_dq_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
                        lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
   } else {
     hipLaunchKernelGGL(attn_bwd_delta<float>, dim3(blocks), dim3(256), 0, s, (const float*)o,

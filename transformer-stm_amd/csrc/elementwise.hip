@@ -85,7 +85,45 @@ __global__ void tokens_pos_bwd_kernel(int B, int N, int D, const float* __restri
 }
 
 // ------------------------------------------------------------ bias gradient
-// partial[z][n] = sum over rows of chunk z of dy[m][n]; 256 threads = 256 columns x 1
+// partial[z][n] = sum over the rows of chunk z of dy[m][n].  256 threads = 4 row groups x
+// 64 lanes x 8 columns (one 16-byte load of bf16 / two of fp32 per row per lane).
+template <typename T>
+__global__ __launch_bounds__(256) void colsum8_kernel(int64_t M, int64_t N, const T* __restrict__ dy,
+                                                      int64_t ldy, float* __restrict__ part,
+                                                      int64_t rows_per) {
+  __shared__ f32x4 red[4][64][2];
+  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 8;
+  const int64_t m0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t m1 = m0 + rows_per < M ? m0 + rows_per : M;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  if (c < N) {
+#pragma unroll 4
+    for (int64_t m = m0 + rg; m < m1; m += 4) {
+      const T* p = dy + m * ldy + c;
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8 v = *(const bf16x8*)p;
+        a0 += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+        a1 += f32x4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+      } else {
+        a0 += *(const f32x4*)p;
+        a1 += *(const f32x4*)(p + 4);
+      }
+    }
+  }
+  red[rg][lane][0] = a0;
+  red[rg][lane][1] = a1;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    f32x4 s0 = red[0][lane][0] + red[1][lane][0] + red[2][lane][0] + red[3][lane][0];
+    f32x4 s1 = red[0][lane][1] + red[1][lane][1] + red[2][lane][1] + red[3][lane][1];
+    float* o = part + (int64_t)blockIdx.y * N + c;
+    *(f32x4*)o = s0;
+    *(f32x4*)(o + 4) = s1;
+  }
+}
+
+// generic (any N / alignment) variant: one thread per column
 template <typename T>
 __global__ void colsum_kernel(int64_t M, int64_t N, const T* __restrict__ dy, int64_t ldy,
                               float* __restrict__ part, int64_t rows_per) {
@@ -98,18 +136,35 @@ __global__ void colsum_kernel(int64_t M, int64_t N, const T* __restrict__ dy, in
   part[(int64_t)blockIdx.y * N + n] = s;
 }
 
-__global__ void colsum_finish_kernel(int64_t N, int Z, const float* __restrict__ part,
-                                     float* __restrict__ db) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+// db[n] += sum_z part[z][n]; 16 waves x 64 columns per block, fixed summation order
+__global__ __launch_bounds__(1024) void colsum_finish_kernel(int64_t N, int Z, const float* __restrict__ part,
+                                                             float* __restrict__ db) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int z = 0; z < Z; ++z) s += part[(int64_t)z * N + n];
-  db[n] += s;
+  if (n < N) {
+#pragma unroll 4
+    for (int z = w; z < Z; z += 16) s += part[(int64_t)z * N + n];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    db[n] += t;
+  }
 }
 
-static int colsum_splits(int64_t M) {
-  int64_t z = (M + 255) / 256;
-  return (int)(z > 256 ? 256 : (z < 1 ? 1 : z));
+// number of row chunks: enough blocks to fill the chip (~1024) for the vector kernel
+static int colsum_splits(int64_t M, int64_t N) {
+  const int64_t colblocks = (N + 511) / 512;
+  int64_t z = 1024 / (colblocks < 1 ? 1 : colblocks);
+  const int64_t zmax = (M + 31) / 32;   // >= 32 rows per chunk
+  if (z > zmax) z = zmax;
+  if (z > 256) z = 256;
+  return (int)(z < 1 ? 1 : z);
 }
 
 // ------------------------------------------------------------ head + loss
@@ -262,7 +317,7 @@ extern "C" int vitmi_tokens_assemble_bwd(int B, int np, int D, const float* dx, 
 }
 
 extern "C" size_t vitmi_bias_grad_workspace_size(int64_t M, int64_t N) {
-  return (size_t)colsum_splits(M) * N * sizeof(float);
+  return (size_t)colsum_splits(M, N) * N * sizeof(float);
 }
 
 extern "C" int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, int64_t ldy,
@@ -271,16 +326,27 @@ extern "C" int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, 
   VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_bias_grad_workspace_size(M, N), "bias_grad: workspace too small");
   if (M == 0 || N == 0) return VITMI_OK;
   hipStream_t s = (hipStream_t)stream;
-  const int Z = colsum_splits(M);
+  const int Z = colsum_splits(M, N);
   const int64_t rows_per = (M + Z - 1) / Z;
-  dim3 grid((unsigned)((N + 255) / 256), Z);
-  if (dtype == VITMI_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)dy, ldy,
-                       (float*)workspace, rows_per);
-  else
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)dy, ldy,
-                       (float*)workspace, rows_per);
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, Z,
+  const bool vec = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)dy % 16 == 0);
+  if (vec) {
+    dim3 grid((unsigned)((N + 511) / 512), Z);
+    if (dtype == VITMI_BF16)
+      hipLaunchKernelGGL(colsum8_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)dy, ldy,
+                         (float*)workspace, rows_per);
+    else
+      hipLaunchKernelGGL(colsum8_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)dy, ldy,
+                         (float*)workspace, rows_per);
+  } else {
+    dim3 grid((unsigned)((N + 255) / 256), Z);
+    if (dtype == VITMI_BF16)
+      hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)dy, ldy,
+                         (float*)workspace, rows_per);
+    else
+      hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)dy, ldy,
+                         (float*)workspace, rows_per);
+  }
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, N, Z,
                      (const float*)workspace, db);
   VITMI_LAUNCH_CHECK("bias_grad");
   return VITMI_OK;

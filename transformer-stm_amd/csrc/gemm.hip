@@ -288,6 +288,246 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
   }
 }
 
+// =============================================================================
+// gemm256: the bf16 workhorse.  256x256 block tile, BK = 64, 8 waves (2 along M x
+// 4 along N, 128x64 outputs each), one block per CU (LDS 136 KiB).
+//
+// Each operand tile is held as two 16 KiB "half" sub-images so that one wave
+// quadrant (64 rows x 32 cols x K64 = 16 MFMAs) needs exactly one A half and one
+// B half.  A half h holds tile rows {128*w + 64*h + i}, B half h holds tile cols
+// {64*w + 32*h + i}.  A K-tile runs in 4 phases over the quadrants
+//   p0 (A0,B0)  p1 (A0,B1)  p2 (A1,B1)  p3 (A1,B0)
+// (A fragments re-used p0->p1 and p2->p3, B p1->p2), and each phase issues ONE
+// half-tile of the NEXT K-tile by LDS-DMA in the same order A0,B0,A1,B1 — so the
+// only waits are a counted `s_waitcnt vmcnt(2)` after p0 and `vmcnt(4)` after p3;
+// DMA stays in flight across the raw `s_barrier`s (cdna_hip_programming.md §5
+// "Pipelining across barriers", 8-phase template T3/T4/T5).
+// Block ids are remapped so consecutive tiles of one XCD share an A row panel.
+// =============================================================================
+namespace g256 {
+// raw s_barrier that the compiler may not move memory operations across; DMA (vmcnt)
+// stays in flight (a __syncthreads() would drain it).
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+constexpr int BM = 256, BN = 256, BK = 64, NWAVES = 8;
+constexpr int HALF = 16384;                 // bytes per half sub-image
+constexpr int STAGE = 4 * HALF;             // A0 A1 B0 B1
+constexpr int EPI_LD = 68;                  // fp32 row stride of the epilogue staging (64 + 4)
+constexpr int EPI_WAVE = 64 * EPI_LD * 4;   // 17408 bytes per wave
+constexpr int SMEM = (2 * STAGE > NWAVES * EPI_WAVE) ? 2 * STAGE : NWAVES * EPI_WAVE;
+
+// tile line of sub-image line i in half h: A (blocks of 64 per wave-row), B (blocks of 32)
+template <bool IS_A>
+__device__ __forceinline__ int line_of(int i, int h) {
+  return IS_A ? ((i >> 6) << 7) + (h << 6) + (i & 63) : ((i >> 5) << 6) + (h << 5) + (i & 31);
+}
+
+// Issue the LDS-DMA of one half sub-image (16 pieces of 1 KiB, 2 per wave).
+template <bool IS_A, bool KMAJ>
+__device__ __forceinline__ void stage_half(char* sub, __amdgpu_buffer_rsrc_t rs, int64_t ld,
+                                           int64_t k0, int krow0, int h, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = wave + NWAVES * j;
+    uint32_t voff;
+    if (KMAJ) {  // image [128 lines][64 k], 128-B rows
+      const int i = p * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ swz_k(i);
+      voff = (uint32_t)((int64_t)line_of<IS_A>(i, h) * ld * 2 + k0 * 2 + c * 16);
+    } else {     // image [64 k][128 lines], 256-B rows
+      const int r = p * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ swz_mn(r);
+      voff = (uint32_t)((int64_t)(krow0 + r) * ld * 2 + (int64_t)line_of<IS_A>(c * 8, h) * 2);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, sub + p * 1024), 16, voff, 0, 0, 0);
+  }
+}
+}  // namespace g256
+
+template <bool AK, bool BKM, int EPI, typename TC>
+__global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // XCD-aware remap (bijective for any nwg): blocks b, b+8, ... share an XCD.
+  const int bid = blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm_i = tile / g.tiles_n, tn_i = tile % g.tiles_n;
+  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
+  const int64_t kb = (int64_t)blockIdx.z * g.k_per_split;
+  const int64_t ke = min(g.K, kb + g.k_per_split);
+  const int nk = (int)((ke - kb + BK - 1) / BK);
+
+  __amdgpu_buffer_rsrc_t ra, rb;
+  if (AK) ra = make_rsrc((const char*)g.A + m0 * g.lda * 2, clamp_bytes((g.M - m0) * g.lda * 2));
+  else ra = make_rsrc((const char*)g.A + (kb * g.lda + m0) * 2, clamp_bytes(((g.K - kb) * g.lda - m0) * 2));
+  if (BKM) rb = make_rsrc((const char*)g.B + n0 * g.ldb * 2, clamp_bytes((g.N - n0) * g.ldb * 2));
+  else rb = make_rsrc((const char*)g.B + (kb * g.ldb + n0) * 2, clamp_bytes(((g.K - kb) * g.ldb - n0) * 2));
+
+  // sub-image addresses: buffer b, [A0 A1 B0 B1]
+  auto sub = [&](int buf, int which) -> char* { return smem + buf * STAGE + which * HALF; };
+  auto issue = [&](int t, int which) {  // which: 0=A0 1=B0 2=A1 3=B1
+    const int buf = t & 1;
+    const int64_t k0 = kb + (int64_t)t * BK;
+    const int krow0 = t * BK;
+    if (which == 0) stage_half<true, AK>(sub(buf, 0), ra, g.lda, k0, krow0, 0, wave, lane);
+    if (which == 1) stage_half<false, BKM>(sub(buf, 2), rb, g.ldb, k0, krow0, 0, wave, lane);
+    if (which == 2) stage_half<true, AK>(sub(buf, 1), ra, g.lda, k0, krow0, 1, wave, lane);
+    if (which == 3) stage_half<false, BKM>(sub(buf, 3), rb, g.ldb, k0, krow0, 1, wave, lane);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Frag<bf16> af[4][2], bfr[2][2];   // [m-tile][k-step], [n-tile][k-step]
+  auto read_a = [&](int buf, int h) {
+    const char* s = sub(buf, h);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[mt][ks] = FragReader<bf16, AK, 128>::read(s, wm * 64 + mt * 16, ks * 32, lane);
+  };
+  auto read_b = [&](int buf, int h) {
+    const char* s = sub(buf, 2 + h);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bfr[nt][ks] = FragReader<bf16, BKM, 128>::read(s, wn * 32 + nt * 16, ks * 32, lane);
+  };
+#define G256_MMA(MH, NH)                                                                        \
+  do {                                                                                          \
+    barrier();                                                               \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                          \
+    __builtin_amdgcn_s_setprio(1);                                                              \
+    _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
+    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                            \
+      acc[MH * 4 + mt][NH * 2 + nt] = mma(af[mt][ks], bfr[nt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
+    __builtin_amdgcn_s_setprio(0);                                                              \
+  } while (0)
+
+  if (nk > 0) {
+    issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A0, B0 of tile 0 landed
+    barrier();
+  }
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool more = t + 1 < nk;
+    // p0: quadrant (A0, B0)
+    read_a(buf, 0); read_b(buf, 0);
+    if (more) { issue(t + 1, 0); asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    G256_MMA(0, 0);
+    barrier();
+    // p1: (A0, B1)
+    read_b(buf, 1);
+    if (more) issue(t + 1, 1);
+    G256_MMA(0, 1);
+    barrier();
+    // p2: (A1, B1)
+    read_a(buf, 1);
+    if (more) issue(t + 1, 2);
+    G256_MMA(1, 1);
+    barrier();
+    // p3: (A1, B0)
+    read_b(buf, 0);
+    if (more) { issue(t + 1, 3); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+    G256_MMA(1, 0);
+    barrier();
+  }
+#undef G256_MMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: stage fp32 accumulators through LDS, then row-contiguous stores
+  float* stg = (float*)(smem + wave * EPI_WAVE);
+  const int cl = lane & 15, rg = 4 * (lane >> 4);
+  const float* bias = (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL) ? g.bias : nullptr;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lr = mt * 16 + rg + i;                // local row 0..63
+          const int lc = (ni >> 1) * 32 + (ni & 1) * 16 + cl;  // local col 0..63 (nh*32 + nt*16)
+          stg[lr * EPI_LD + lc] = acc[mh * 4 + mt][ni][i];
+        }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own stores visible to own reads
+    // each lane: 8 consecutive columns of rows (lane>>3) + 8*it
+    const int c8 = (lane & 7) * 8;
+    // local col c8 -> tile col: local [nh*32 + nt*16 + x] == tile wn*64 + local (B half layout is per wave)
+    const int64_t col = n0 + wn * 64 + c8;
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int lr = it * 8 + (lane >> 3);
+      const int64_t row = m0 + wm * 128 + mh * 64 + lr;
+      if (row >= g.M || col >= g.N) continue;
+      const f32x4 v0 = *(const f32x4*)(stg + lr * EPI_LD + c8);
+      const f32x4 v1 = *(const f32x4*)(stg + lr * EPI_LD + c8 + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      if (bias) {
+        const f32x4 b0 = *(const f32x4*)(bias + col), b1 = *(const f32x4*)(bias + col + 4);
+        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
+        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
+      }
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* d = (float*)g.C + blockIdx.z * g.split_stride + row * g.ldc + col;
+        *(f32x4*)d = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else if constexpr (EPI == VITMI_EPI_ACCUM) {
+        float* d = (float*)g.C + row * g.ldc + col;
+        f32x4 o0 = *(f32x4*)d, o1 = *(f32x4*)(d + 4);
+        *(f32x4*)d = o0 + f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(d + 4) = o1 + f32x4{v[4], v[5], v[6], v[7]};
+      } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
+        const float* rr = g.residual + row * g.ldr + col;
+        const f32x4 r0 = *(const f32x4*)rr, r1 = *(const f32x4*)(rr + 4);
+        float* d = (float*)g.C + row * g.ldc + col;
+        *(f32x4*)d = r0 + f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(d + 4) = r1 + f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
+          bf16x8 u;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) u[e] = (bf16)v[e];
+          *(bf16x8*)((bf16*)g.aux + row * g.ldaux + col) = u;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+        } else if constexpr (EPI == VITMI_EPI_DGELU) {
+          const bf16x8 u = *(const bf16x8*)((const bf16*)g.aux + row * g.ldaux + col);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f((float)u[e]);
+        }
+        if constexpr (sizeof(TC) == 2) {
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+          *(bf16x8*)((bf16*)g.C + row * g.ldc + col) = o;
+        } else {
+          float* d = (float*)g.C + row * g.ldc + col;
+          *(f32x4*)d = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+}
+
 // split-K reduction: dst[i] += sum_z ws[z][i]
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dst,
                                      int64_t n, int splits, int64_t stride) {
@@ -309,8 +549,28 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
 }
 
 // ---------------------------------------------------------------- host launch
+// GEMM kernel policy: 0 = auto, 1 = always the 128x128 kernel, 2 = always gemm256 (bf16)
+static int g_policy = 0;
+
+static bool use256(int dtype, int64_t M, int64_t N) {
+  if (dtype != VITMI_BF16 || (N % 8) != 0) return false;
+  if (g_policy == 1) return false;
+  if (g_policy == 2) return true;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  return tiles >= 16;
+}
+
 template <typename T, bool AK, bool BKM, int EPI, typename TC>
-static int launch_t(GemmArgs g, int splits, hipStream_t s) {
+static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (big) {
+      g.tiles_n = (int)((g.N + 255) / 256);
+      const int nwg = (int)((g.M + 255) / 256) * g.tiles_n;
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(nwg, 1, splits), dim3(512), 0, s, g, nwg);
+      VITMI_LAUNCH_CHECK("gemm256_kernel");
+      return VITMI_OK;
+    }
+  }
   constexpr int BM = 128, BN = 128, WM = 2, WN = 2;
   g.tiles_n = (int)((g.N + BN - 1) / BN);
   const int tiles_m = (int)((g.M + BM - 1) / BM);
@@ -321,44 +581,48 @@ static int launch_t(GemmArgs g, int splits, hipStream_t s) {
 }
 
 template <typename T, int EPI, typename TC>
-static int launch_layout(int ak, int bk, GemmArgs g, int splits, hipStream_t s) {
-  if (ak && bk) return launch_t<T, true, true, EPI, TC>(g, splits, s);
-  if (ak && !bk) return launch_t<T, true, false, EPI, TC>(g, splits, s);
-  if (!ak && !bk) return launch_t<T, false, false, EPI, TC>(g, splits, s);
+static int launch_layout(int ak, int bk, GemmArgs g, int splits, bool big, hipStream_t s) {
+  if (ak && bk) return launch_t<T, true, true, EPI, TC>(g, splits, big, s);
+  if (ak && !bk) return launch_t<T, true, false, EPI, TC>(g, splits, big, s);
+  if (!ak && !bk) return launch_t<T, false, false, EPI, TC>(g, splits, big, s);
   return fail(VITMI_ERR_UNSUPPORTED, "gemm: layout A m-major x B k-major not instantiated");
 }
 
 template <typename T>
-static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits, hipStream_t s) {
+static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits, bool big, hipStream_t s) {
   const bool cbf = (c_dtype == VITMI_BF16);
   switch (epi) {
     case VITMI_EPI_STORE:
-      return cbf ? launch_layout<T, VITMI_EPI_STORE, bf16>(ak, bk, g, splits, s)
-                 : launch_layout<T, VITMI_EPI_STORE, float>(ak, bk, g, splits, s);
+      return cbf ? launch_layout<T, VITMI_EPI_STORE, bf16>(ak, bk, g, splits, big, s)
+                 : launch_layout<T, VITMI_EPI_STORE, float>(ak, bk, g, splits, big, s);
     case VITMI_EPI_BIAS_GELU:
-      return cbf ? launch_layout<T, VITMI_EPI_BIAS_GELU, bf16>(ak, bk, g, splits, s)
-                 : launch_layout<T, VITMI_EPI_BIAS_GELU, float>(ak, bk, g, splits, s);
+      return cbf ? launch_layout<T, VITMI_EPI_BIAS_GELU, bf16>(ak, bk, g, splits, big, s)
+                 : launch_layout<T, VITMI_EPI_BIAS_GELU, float>(ak, bk, g, splits, big, s);
     case VITMI_EPI_RESIDUAL:
-      return launch_layout<T, VITMI_EPI_RESIDUAL, float>(ak, bk, g, splits, s);
+      return launch_layout<T, VITMI_EPI_RESIDUAL, float>(ak, bk, g, splits, big, s);
     case VITMI_EPI_DGELU:
-      return cbf ? launch_layout<T, VITMI_EPI_DGELU, bf16>(ak, bk, g, splits, s)
-                 : launch_layout<T, VITMI_EPI_DGELU, float>(ak, bk, g, splits, s);
+      return cbf ? launch_layout<T, VITMI_EPI_DGELU, bf16>(ak, bk, g, splits, big, s)
+                 : launch_layout<T, VITMI_EPI_DGELU, float>(ak, bk, g, splits, big, s);
     case VITMI_EPI_ACCUM:
-      return launch_layout<T, VITMI_EPI_ACCUM, float>(ak, bk, g, splits, s);
+      return launch_layout<T, VITMI_EPI_ACCUM, float>(ak, bk, g, splits, big, s);
     case EPI_PARTIAL:
-      return launch_layout<T, EPI_PARTIAL, float>(ak, bk, g, splits, s);
+      return launch_layout<T, EPI_PARTIAL, float>(ak, bk, g, splits, big, s);
   }
   return fail(VITMI_ERR_INVALID, "gemm: unknown epilogue %d", epi);
 }
 
 static int bk_of(int dtype) { return dtype == VITMI_BF16 ? 64 : 32; }
 
-// split count for a reduction-heavy GEMM: fill ~2 blocks per CU
+// split count for a reduction-heavy GEMM (wgrad): about one full round of blocks
+// (1 block/CU for gemm256, ~2 for the 128 kernel), at least 4 k-tiles per split.
 static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const bool big = use256(dtype, M, N);
+  const int64_t t = big ? 256 : 128;
+  const int64_t tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
   const int64_t ktiles = (K + bk_of(dtype) - 1) / bk_of(dtype);
-  int64_t want = (512 + tiles - 1) / tiles;
-  int64_t maxs = ktiles / 8;  // at least 8 k-tiles per split
+  const int64_t target = big ? 256 : 512;
+  int64_t want = target / tiles;
+  int64_t maxs = ktiles / 4;
   if (want > maxs) want = maxs;
   if (want > 64) want = 64;
   return want < 1 ? 1 : (int)want;
@@ -389,6 +653,13 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   // 32-bit buffer offsets: one block's panel must stay under 2 GiB
   VITMI_CHECK_ARG((ak ? 128 * lda : K * lda) * es < 0x7fffffffLL, "gemm: A panel exceeds 2 GiB");
 
+  const bool big = use256(dtype, M, N);
+  if (big) {
+    VITMI_CHECK_ARG(ldc % 8 == 0 && (ldr % 4) == 0 && (ldaux % 8) == 0 && ((uintptr_t)C % 16) == 0,
+                    "gemm: 16-byte aligned C/aux/residual rows required");
+    VITMI_CHECK_ARG(bias == nullptr || ((uintptr_t)bias % 16) == 0, "gemm: bias must be 16-byte aligned");
+    VITMI_CHECK_ARG((ak ? 256 * lda : K * lda) * 2 < 0x7fffffffLL, "gemm: A panel exceeds 2 GiB");
+  }
   GemmArgs g{};
   g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.bias = bias; g.aux = aux; g.ldaux = ldaux;
@@ -406,14 +677,14 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   }
   if (splits == 1) {
     g.k_per_split = (K > 0 ? ktiles : 1) * BK;
-    if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, s);
-    return dispatch<float>(ak, bk, c_dtype, epi, g, 1, s);
+    if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, big, s);
+    return dispatch<float>(ak, bk, c_dtype, epi, g, 1, big, s);
   }
   // split-K: partial slabs then one reduction pass into C (+=)
   GemmArgs gp = g;
   gp.C = ws; gp.ldc = N; gp.split_stride = M * N;
-  int rc = dtype == VITMI_BF16 ? dispatch<bf16>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, s)
-                               : dispatch<float>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, s);
+  int rc = dtype == VITMI_BF16 ? dispatch<bf16>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big, s)
+                               : dispatch<float>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big, s);
   if (rc) return rc;
   VITMI_CHECK_ARG(ldc == N, "gemm: split-K accumulate needs a dense C");
   const int64_t n = M * N;
@@ -429,6 +700,12 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
 }  // namespace vitmi
 
 using namespace vitmi;
+
+extern "C" int vitmi_gemm_set_policy(int policy) {
+  VITMI_CHECK_ARG(policy >= 0 && policy <= 2, "gemm_set_policy: policy must be 0, 1 or 2");
+  g_policy = policy;
+  return VITMI_OK;
+}
 
 extern "C" int vitmi_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K,
                           const void* A, int64_t lda, const void* B, int64_t ldb, void* C,

@@ -145,23 +145,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// out[d] += sum_b part[b][d]   for dgamma (rows 0..G-1) and dbeta (rows G..2G-1)
-__global__ void ln_param_reduce(const float* __restrict__ part, int G, int D,
-                                float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
+// out[d] += sum_b part[b][d] for dgamma (rows 0..G-1) and dbeta (rows G..2G-1).
+// 1024 threads = 16 waves x 64 columns; wave w sums rows w, w+16, ... (fixed order:
+// deterministic), then a 16-way LDS reduction.
+__global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int G, int D,
+                                                        float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta) {
+  __shared__ float red[2][16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int d = blockIdx.x * 64 + lane;
   float a = 0.f, b = 0.f;
-  for (int i = 0; i < G; ++i) {
-    a += part[(int64_t)i * D + d];
-    b += part[(int64_t)(G + i) * D + d];
+  if (d < D) {
+#pragma unroll 4
+    for (int i = w; i < G; i += 16) {
+      a += part[(int64_t)i * D + d];
+      b += part[(int64_t)(G + i) * D + d];
+    }
   }
-  if (dgamma) dgamma[d] += a;
-  if (dbeta) dbeta[d] += b;
+  red[0][w][lane] = a;
+  red[1][w][lane] = b;
+  __syncthreads();
+  if (w < 2 && d < D) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[w][i][lane];
+    float* out = w == 0 ? dgamma : dbeta;
+    if (out) out[d] += s;
+  }
 }
 
 static int ln_blocks_bwd(int64_t M) {
   int64_t g = (M + 3) / 4;
-  return (int)(g < 1024 ? (g < 1 ? 1 : g) : 1024);
+  return (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
 }
 
 template <int NV>
@@ -251,7 +266,7 @@ extern "C" int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtyp
     default: LNB(8) break;
   }
 #undef LNB
-  hipLaunchKernelGGL(ln_param_reduce, dim3((D + 255) / 256), dim3(256), 0, s, (const float*)part, G,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((D + 63) / 64), dim3(1024), 0, s, (const float*)part, G,
                      D, dgamma, dbeta);
   VITMI_LAUNCH_CHECK("layernorm_bwd");
   return VITMI_OK;

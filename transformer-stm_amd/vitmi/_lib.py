@@ -29,6 +29,7 @@ SIGNATURES = {
     "vitmi_device_cus": (I, []),
     "vitmi_gemm": (I, [I, I, I, L, L, L, P, L, P, L, P, L, I, I, P, P, L, P, L, P, S, P]),
     "vitmi_gemm_workspace_size": (S, [I, I, I, L, L, L, I]),
+    "vitmi_gemm_set_policy": (I, [I]),
     "vitmi_linear_fwd": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P]),
     "vitmi_linear_dgrad": (I, [I, L, L, L, P, P, P, I, I, P, P]),
     "vitmi_linear_wgrad": (I, [I, L, L, L, P, P, P, P, S, P]),
