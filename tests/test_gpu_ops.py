@@ -16,7 +16,7 @@ BF = torch.bfloat16
 
 def rel(a, b):
     a, b = a.double().cpu(), b.double().cpu()
-    return ((a - b).norm() / b.norm().clamp_min(1e-3)).item()
+    return ((a - b).norm() / b.norm().clamp_min(1.0)).item()
 
 
 def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
