@@ -66,7 +66,8 @@ int vitmi_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int6
                const float* residual, int64_t ldr, void* workspace, size_t ws_bytes,
                vitmi_stream_t stream);
 /* Kernel selection (process-wide): 0 = auto (default), 1 = always the 128x128 tile kernel,
- * 2 = always the 256x256 8-wave bf16 kernel where the dtype allows.  For tests/diagnostics. */
+ * 2 = always the 256x256 8-wave bf16 kernel where the dtype allows, 3 = as 2 on an 8-block
+ * persistent grid (each block walks many tiles).  For tests/diagnostics. */
 int vitmi_gemm_set_policy(int policy);
 size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajor, int64_t M, int64_t N,
                                  int64_t K, int epilogue);

@@ -25,7 +25,7 @@ def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[1, 2], ids=["tile128", "tile256"])
+@pytest.fixture(params=[1, 2, 3], ids=["tile128", "tile256", "tile256-persistent8"])
 def policy(request):
     """Run each GEMM case through both kernels (vitmi_gemm_set_policy)."""
     from vitmi._lib import lib

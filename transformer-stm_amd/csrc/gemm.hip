@@ -315,9 +315,6 @@ __device__ __forceinline__ void barrier() {
 constexpr int BM = 256, BN = 256, BK = 64, NWAVES = 8;
 constexpr int HALF = 16384;                 // bytes per half sub-image
 constexpr int STAGE = 4 * HALF;             // A0 A1 B0 B1
-constexpr int EPI_LD = 68;                  // fp32 row stride of the epilogue staging (64 + 4)
-constexpr int EPI_WAVE = 64 * EPI_LD * 4;   // 17408 bytes per wave
-constexpr int SMEM = (2 * STAGE > NWAVES * EPI_WAVE) ? 2 * STAGE : NWAVES * EPI_WAVE;
 
 // tile line of sub-image line i in half h: A (blocks of 64 per wave-row), B (blocks of 32)
 template <bool IS_A>
@@ -347,34 +344,59 @@ __device__ __forceinline__ void stage_half(char* sub, __amdgpu_buffer_rsrc_t rs,
 }
 }  // namespace g256
 
+// erf with |error| <= 1.5e-7 (Abramowitz-Stegun 7.1.26): one exp, one rcp, 6 FMAs.  Used
+// only where the result is rounded to bf16; the fp32 path keeps erff.
+__device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float e = __expf(-z * z);
+  const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
+                      0.254829592f) * t;
+  const float erfz = 1.0f - poly * e;
+  cdf = 0.5f * (1.0f + (x < 0.f ? -erfz : erfz));
+  pdf = 0.39894228040143268f * e;   // e == exp(-x^2/2)
+}
+
+// Persistent variant: gridDim.x blocks (<= one per CU) walk the tiles; blocks with equal
+// blockIdx.x % 8 (one XCD under round-robin dispatch) take consecutive tiles of one
+// contiguous range, so the XCD's concurrent tiles share A row panels in its L2.  The last
+// K-step of a tile prefetches K-step 0 of the block's next tile, so that DMA overlaps the
+// epilogue.  MFMA operands are swapped (B first): the 16x16 accumulator then holds C^T,
+// i.e. every lane owns 4 consecutive output COLUMNS of one row -> 8/16-byte vector stores
+// straight from registers.
 template <bool AK, bool BKM, int EPI, typename TC>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   using namespace g256;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
-  // XCD-aware remap (bijective for any nwg): blocks b, b+8, ... share an XCD.
-  const int bid = blockIdx.x;
-  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
-  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm_i = tile / g.tiles_n, tn_i = tile % g.tiles_n;
-  const int64_t m0 = (int64_t)tm_i * BM, n0 = (int64_t)tn_i * BN;
+  // tile range of this block's XCD group, and the block's stride inside it
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, jx = blockIdx.x >> 3;
+  const int gq = G >> 3, gr = G & 7;
+  const int nbx = gq + (xcd < gr ? 1 : 0);              // blocks in this group
+  const int q = nwg >> 3, r = nwg & 7;
+  const int t_begin = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int t_end = t_begin + q + (xcd < r ? 1 : 0);
+
   const int64_t kb = (int64_t)blockIdx.z * g.k_per_split;
   const int64_t ke = min(g.K, kb + g.k_per_split);
   const int nk = (int)((ke - kb + BK - 1) / BK);
+  if (nk <= 0) return;
 
-  __amdgpu_buffer_rsrc_t ra, rb;
-  if (AK) ra = make_rsrc((const char*)g.A + m0 * g.lda * 2, clamp_bytes((g.M - m0) * g.lda * 2));
-  else ra = make_rsrc((const char*)g.A + (kb * g.lda + m0) * 2, clamp_bytes(((g.K - kb) * g.lda - m0) * 2));
-  if (BKM) rb = make_rsrc((const char*)g.B + n0 * g.ldb * 2, clamp_bytes((g.N - n0) * g.ldb * 2));
-  else rb = make_rsrc((const char*)g.B + (kb * g.ldb + n0) * 2, clamp_bytes(((g.K - kb) * g.ldb - n0) * 2));
-
-  // sub-image addresses: buffer b, [A0 A1 B0 B1]
+  auto rsrc_a = [&](int64_t m0) {
+    return AK ? make_rsrc((const char*)g.A + m0 * g.lda * 2, clamp_bytes((g.M - m0) * g.lda * 2))
+              : make_rsrc((const char*)g.A + (kb * g.lda + m0) * 2, clamp_bytes(((g.K - kb) * g.lda - m0) * 2));
+  };
+  auto rsrc_b = [&](int64_t n0) {
+    return BKM ? make_rsrc((const char*)g.B + n0 * g.ldb * 2, clamp_bytes((g.N - n0) * g.ldb * 2))
+               : make_rsrc((const char*)g.B + (kb * g.ldb + n0) * 2, clamp_bytes(((g.K - kb) * g.ldb - n0) * 2));
+  };
   auto sub = [&](int buf, int which) -> char* { return smem + buf * STAGE + which * HALF; };
-  auto issue = [&](int t, int which) {  // which: 0=A0 1=B0 2=A1 3=B1
-    const int buf = t & 1;
+  // issue half `which` (0=A0 1=B0 2=A1 3=B1) of K-step t into buffer buf
+  auto issue = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int t, int buf, int which) {
     const int64_t k0 = kb + (int64_t)t * BK;
     const int krow0 = t * BK;
     if (which == 0) stage_half<true, AK>(sub(buf, 0), ra, g.lda, k0, krow0, 0, wave, lane);
@@ -383,13 +405,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     if (which == 3) stage_half<false, BKM>(sub(buf, 3), rb, g.ldb, k0, krow0, 1, wave, lane);
   };
 
+  Frag<bf16> af[4][2], bfr[2][2];
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  Frag<bf16> af[4][2], bfr[2][2];   // [m-tile][k-step], [n-tile][k-step]
   auto read_a = [&](int buf, int h) {
     const char* s = sub(buf, h);
 #pragma unroll
@@ -406,126 +423,126 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   };
 #define G256_MMA(MH, NH)                                                                        \
   do {                                                                                          \
-    barrier();                                                               \
+    barrier();                                                                                  \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                          \
     __builtin_amdgcn_s_setprio(1);                                                              \
     _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
     _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                            \
-      acc[MH * 4 + mt][NH * 2 + nt] = mma(af[mt][ks], bfr[nt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
+      acc[MH * 4 + mt][NH * 2 + nt] = mma(bfr[nt][ks], af[mt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
     __builtin_amdgcn_s_setprio(0);                                                              \
   } while (0)
 
-  if (nk > 0) {
-    issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A0, B0 of tile 0 landed
-    barrier();
-  }
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    const bool more = t + 1 < nk;
-    // p0: quadrant (A0, B0)
-    read_a(buf, 0); read_b(buf, 0);
-    if (more) { issue(t + 1, 0); asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    G256_MMA(0, 0);
-    barrier();
-    // p1: (A0, B1)
-    read_b(buf, 1);
-    if (more) issue(t + 1, 1);
-    G256_MMA(0, 1);
-    barrier();
-    // p2: (A1, B1)
-    read_a(buf, 1);
-    if (more) issue(t + 1, 2);
-    G256_MMA(1, 1);
-    barrier();
-    // p3: (A1, B0)
-    read_b(buf, 0);
-    if (more) { issue(t + 1, 3); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
-    G256_MMA(1, 0);
-    barrier();
-  }
-#undef G256_MMA
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  int tile = t_begin + jx;
+  if (tile >= t_end) return;
+  int64_t m0 = (int64_t)(tile / g.tiles_n) * BM, n0 = (int64_t)(tile % g.tiles_n) * BN;
+  __amdgpu_buffer_rsrc_t ra = rsrc_a(m0), rb = rsrc_b(n0);
+  int buf = 0;
+  issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 2); issue(ra, rb, 0, 0, 3);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A0, B0 of the first K-step landed
+  barrier();
 
-  // ---- epilogue: stage fp32 accumulators through LDS, then row-contiguous stores
-  float* stg = (float*)(smem + wave * EPI_WAVE);
-  const int cl = lane & 15, rg = 4 * (lane >> 4);
-  const float* bias = (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL) ? g.bias : nullptr;
+  const int lc4 = 4 * (lane >> 4), lr = lane & 15;
+  for (;;) {
+    const int next = tile + nbx;
+    const bool has_next = next < t_end;
+    const int64_t m0n = has_next ? (int64_t)(next / g.tiles_n) * BM : 0;
+    const int64_t n0n = has_next ? (int64_t)(next % g.tiles_n) * BN : 0;
+    const __amdgpu_buffer_rsrc_t ran = rsrc_a(m0n), rbn = rsrc_b(n0n);
 #pragma unroll
-  for (int mh = 0; mh < 2; ++mh) {
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int t = 0; t < nk; ++t) {
+      // the K-step staged next: (this tile, t+1) or (next tile, 0)
+      const bool more = (t + 1 < nk) || has_next;
+      const __amdgpu_buffer_rsrc_t sa = (t + 1 < nk) ? ra : ran;
+      const __amdgpu_buffer_rsrc_t sb = (t + 1 < nk) ? rb : rbn;
+      const int tn = (t + 1 < nk) ? t + 1 : 0;
+      const int nbuf = buf ^ 1;
+      // p0 (A0,B0)
+      read_a(buf, 0); read_b(buf, 0);
+      if (more) { issue(sa, sb, tn, nbuf, 0); asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      G256_MMA(0, 0);
+      barrier();
+      // p1 (A0,B1)
+      read_b(buf, 1);
+      if (more) issue(sa, sb, tn, nbuf, 1);
+      G256_MMA(0, 1);
+      barrier();
+      // p2 (A1,B1)
+      read_a(buf, 1);
+      if (more) issue(sa, sb, tn, nbuf, 2);
+      G256_MMA(1, 1);
+      barrier();
+      // p3 (A1,B0)
+      read_b(buf, 0);
+      if (more) { issue(sa, sb, tn, nbuf, 3); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+      G256_MMA(1, 0);
+      barrier();
+      buf = nbuf;
+    }
+
+    // ---- epilogue straight from registers: acc[mi][ni] = C^T tile; lane owns row
+    // m0 + wm*128 + mi*16 + lr, columns n0 + wn*64 + ni*16 + lc4 .. +3
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < 4; ++ni) {
+      const int64_t col = n0 + wn * 64 + ni * 16 + lc4;
+      if (col >= g.N) continue;
+      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL)
+        if (g.bias) bv = *(const f32x4*)(g.bias + col);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int lr = mt * 16 + rg + i;                // local row 0..63
-          const int lc = (ni >> 1) * 32 + (ni & 1) * 16 + cl;  // local col 0..63 (nh*32 + nt*16)
-          stg[lr * EPI_LD + lc] = acc[mh * 4 + mt][ni][i];
-        }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own stores visible to own reads
-    // each lane: 8 consecutive columns of rows (lane>>3) + 8*it
-    const int c8 = (lane & 7) * 8;
-    // local col c8 -> tile col: local [nh*32 + nt*16 + x] == tile wn*64 + local (B half layout is per wave)
-    const int64_t col = n0 + wn * 64 + c8;
-#pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
-      const int lr = it * 8 + (lane >> 3);
-      const int64_t row = m0 + wm * 128 + mh * 64 + lr;
-      if (row >= g.M || col >= g.N) continue;
-      const f32x4 v0 = *(const f32x4*)(stg + lr * EPI_LD + c8);
-      const f32x4 v1 = *(const f32x4*)(stg + lr * EPI_LD + c8 + 4);
-      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      if (bias) {
-        const f32x4 b0 = *(const f32x4*)(bias + col), b1 = *(const f32x4*)(bias + col + 4);
-        v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
-        v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
-      }
-      if constexpr (EPI == EPI_PARTIAL) {
-        float* d = (float*)g.C + blockIdx.z * g.split_stride + row * g.ldc + col;
-        *(f32x4*)d = f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      } else if constexpr (EPI == VITMI_EPI_ACCUM) {
-        float* d = (float*)g.C + row * g.ldc + col;
-        f32x4 o0 = *(f32x4*)d, o1 = *(f32x4*)(d + 4);
-        *(f32x4*)d = o0 + f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)(d + 4) = o1 + f32x4{v[4], v[5], v[6], v[7]};
-      } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
-        const float* rr = g.residual + row * g.ldr + col;
-        const f32x4 r0 = *(const f32x4*)rr, r1 = *(const f32x4*)(rr + 4);
-        float* d = (float*)g.C + row * g.ldc + col;
-        *(f32x4*)d = r0 + f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)(d + 4) = r1 + f32x4{v[4], v[5], v[6], v[7]};
-      } else {
-        if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
-          bf16x8 u;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) u[e] = (bf16)v[e];
-          *(bf16x8*)((bf16*)g.aux + row * g.ldaux + col) = u;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
-        } else if constexpr (EPI == VITMI_EPI_DGELU) {
-          const bf16x8 u = *(const bf16x8*)((const bf16*)g.aux + row * g.ldaux + col);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f((float)u[e]);
-        }
-        if constexpr (sizeof(TC) == 2) {
-          bf16x8 o;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-          *(bf16x8*)((bf16*)g.C + row * g.ldc + col) = o;
-        } else {
+      for (int mi = 0; mi < 8; ++mi) {
+        const int64_t row = m0 + wm * 128 + mi * 16 + lr;
+        if (row >= g.M) continue;
+        f32x4 v = acc[mi][ni] + bv;
+        if constexpr (EPI == EPI_PARTIAL) {
+          *(f32x4*)((float*)g.C + blockIdx.z * g.split_stride + row * g.ldc + col) = v;
+        } else if constexpr (EPI == VITMI_EPI_ACCUM) {
           float* d = (float*)g.C + row * g.ldc + col;
-          *(f32x4*)d = f32x4{v[0], v[1], v[2], v[3]};
-          *(f32x4*)(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+          *(f32x4*)d = *(const f32x4*)d + v;
+        } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
+          const f32x4 rv = *(const f32x4*)(g.residual + row * g.ldr + col);
+          *(f32x4*)((float*)g.C + row * g.ldc + col) = rv + v;
+        } else {
+          if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
+            bf16x4 u;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              u[e] = (bf16)v[e];
+              float cdf, pdf;
+              gelu_fast_parts(v[e], cdf, pdf);
+              v[e] = v[e] * cdf;
+            }
+            *(bf16x4*)((bf16*)g.aux + row * g.ldaux + col) = u;
+          } else if constexpr (EPI == VITMI_EPI_DGELU) {
+            const bf16x4 u = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float uf = (float)u[e];
+              float cdf, pdf;
+              gelu_fast_parts(uf, cdf, pdf);
+              v[e] *= cdf + uf * pdf;
+            }
+          }
+          if constexpr (sizeof(TC) == 2) {
+            bf16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+            *(bf16x4*)((bf16*)g.C + row * g.ldc + col) = o;
+          } else {
+            *(f32x4*)((float*)g.C + row * g.ldc + col) = v;
+          }
         }
       }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if (!has_next) break;
+    tile = next; m0 = m0n; n0 = n0n; ra = ran; rb = rbn;
   }
+#undef G256_MMA
 }
 
 // split-K reduction: dst[i] += sum_z ws[z][i]
@@ -549,13 +566,25 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
 }
 
 // ---------------------------------------------------------------- host launch
-// GEMM kernel policy: 0 = auto, 1 = always the 128x128 kernel, 2 = always gemm256 (bf16)
+// GEMM kernel policy: 0 = auto, 1 = always the 128x128 kernel, 2 = always gemm256 (bf16),
+// 3 = gemm256 on an 8-block persistent grid (every block walks many tiles; tests only)
 static int g_policy = 0;
+static int g_cus = 256;   // compute units of the current device (set on first use)
+
+static void init_cus() {
+  static bool done = false;
+  if (done) return;
+  int dev = 0;
+  hipDeviceProp_t p;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
+    g_cus = p.multiProcessorCount;
+  done = true;
+}
 
 static bool use256(int dtype, int64_t M, int64_t N) {
   if (dtype != VITMI_BF16 || (N % 8) != 0) return false;
   if (g_policy == 1) return false;
-  if (g_policy == 2) return true;
+  if (g_policy >= 2) return true;
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   return tiles >= 16;
 }
@@ -566,7 +595,11 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
     if (big) {
       g.tiles_n = (int)((g.N + 255) / 256);
       const int nwg = (int)((g.M + 255) / 256) * g.tiles_n;
-      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(nwg, 1, splits), dim3(512), 0, s, g, nwg);
+      // persistent: about one block per CU over all splits
+      int gx = g_cus / splits;
+      if (gx < 8 || g_policy == 3) gx = 8;   // policy 3: force many tiles per block (tests)
+      if (gx > nwg) gx = nwg;
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, nwg);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
       return VITMI_OK;
     }
@@ -655,6 +688,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
 
   const bool big = use256(dtype, M, N);
   if (big) {
+    init_cus();
     VITMI_CHECK_ARG(ldc % 8 == 0 && (ldr % 4) == 0 && (ldaux % 8) == 0 && ((uintptr_t)C % 16) == 0,
                     "gemm: 16-byte aligned C/aux/residual rows required");
     VITMI_CHECK_ARG(bias == nullptr || ((uintptr_t)bias % 16) == 0, "gemm: bias must be 16-byte aligned");
@@ -702,7 +736,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
 using namespace vitmi;
 
 extern "C" int vitmi_gemm_set_policy(int policy) {
-  VITMI_CHECK_ARG(policy >= 0 && policy <= 2, "gemm_set_policy: policy must be 0, 1 or 2");
+  VITMI_CHECK_ARG(policy >= 0 && policy <= 3, "gemm_set_policy: policy must be 0..3");
   g_policy = policy;
   return VITMI_OK;
 }
