@@ -15,6 +15,7 @@
 // j-th MFMA consumes element j from every lane group: both operands use the same
 // k permutation, so the sum is unchanged.
 #include "common.h"
+#include <stdlib.h>
 
 namespace vitmi {
 
@@ -571,9 +572,12 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
 static int g_policy = 0;
 static int g_cus = 256;   // compute units of the current device (set on first use)
 
+static int g_grid_override = 0;   // VITMI_GEMM_GRID: 0 = persistent (one block per CU), -1 = one block per tile
+
 static void init_cus() {
   static bool done = false;
   if (done) return;
+  if (const char* e = getenv("VITMI_GEMM_GRID")) g_grid_override = atoi(e);
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
@@ -598,6 +602,8 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       // persistent: about one block per CU over all splits
       int gx = g_cus / splits;
       if (gx < 8 || g_policy == 3) gx = 8;   // policy 3: force many tiles per block (tests)
+      if (g_grid_override < 0) gx = nwg;
+      else if (g_grid_override > 0) gx = g_grid_override;
       if (gx > nwg) gx = nwg;
       hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, nwg);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
