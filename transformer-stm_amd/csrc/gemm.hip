@@ -349,8 +349,8 @@ __device__ __forceinline__ void stage_half(char* sub, __amdgpu_buffer_rsrc_t rs,
 // only where the result is rounded to bf16; the fp32 path keeps erff.
 __device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf) {
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __frcp_rn(1.0f + 0.3275911f * z);
-  const float e = __expf(-z * z);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
   const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
                       0.254829592f) * t;
   const float erfz = 1.0f - poly * e;
@@ -424,8 +424,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   };
 #define G256_MMA(MH, NH)                                                                        \
   do {                                                                                          \
-    barrier();                                                                                  \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                          \
     __builtin_amdgcn_s_setprio(1);                                                              \
     _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
     _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
@@ -462,53 +460,69 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       const __amdgpu_buffer_rsrc_t sb = (t + 1 < nk) ? rb : rbn;
       const int tn = (t + 1 < nk) ? t + 1 : 0;
       const int nbuf = buf ^ 1;
+      // Barriers only where a DMA wait must become visible to every wave (after p0's and
+      // p3's counted waits); between them the next phase's ds_reads may overlap MFMAs.
       // p0 (A0,B0)
       read_a(buf, 0); read_b(buf, 0);
       if (more) { issue(sa, sb, tn, nbuf, 0); asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      G256_MMA(0, 0);
       barrier();
+      G256_MMA(0, 0);
       // p1 (A0,B1)
       read_b(buf, 1);
       if (more) issue(sa, sb, tn, nbuf, 1);
       G256_MMA(0, 1);
-      barrier();
       // p2 (A1,B1)
       read_a(buf, 1);
       if (more) issue(sa, sb, tn, nbuf, 2);
       G256_MMA(1, 1);
-      barrier();
       // p3 (A1,B0)
       read_b(buf, 0);
       if (more) { issue(sa, sb, tn, nbuf, 3); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
-      G256_MMA(1, 0);
       barrier();
+      G256_MMA(1, 0);
       buf = nbuf;
     }
 
     // ---- epilogue straight from registers: acc[mi][ni] = C^T tile; lane owns row
-    // m0 + wm*128 + mi*16 + lr, columns n0 + wn*64 + ni*16 + lc4 .. +3
+    // m0 + wm*128 + mi*16 + lr, columns n0 + wn*64 + ni*16 + lc4 .. +3.
+    // Stores are inline-asm buffer stores: hipcc would otherwise put `s_waitcnt vmcnt(0)`
+    // before every store (it cannot prove C does not alias the in-flight DMA sources),
+    // serialising the epilogue.  C never aliases A/B here (host contract).  The range
+    // check drops rows >= M; the row offset is a scalar per mi, the column an immediate.
+    {
+      constexpr int CES = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM &&
+                                  EPI != VITMI_EPI_RESIDUAL ? 2 : 4;
+      const int64_t zoff = EPI == EPI_PARTIAL ? (int64_t)blockIdx.z * g.split_stride : 0;
+      char* cbase = (char*)g.C + (zoff + m0 * g.ldc + n0) * CES;
+      const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, clamp_bytes(((g.M - m0) * g.ldc - n0) * CES));
+      const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
+      const uint32_t vbase = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldc + wn * 64 + lc4) * CES);
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int64_t col = n0 + wn * 64 + ni * 16 + lc4;
-      if (col >= g.N) continue;
-      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL)
-        if (g.bias) bv = *(const f32x4*)(g.bias + col);
+      for (int ni = 0; ni < 4; ++ni) {
+        const int64_t col = n0 + wn * 64 + ni * 16 + lc4;
+        if (col >= g.N) continue;
+        f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL)
+          if (g.bias) bv = *(const f32x4*)(g.bias + col);
+        // batch the epilogue's global loads for this column group (one wait for all 8)
+        f32x4 ld4[8];
+        bf16x4 ldu[8];
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const int64_t row = m0 + wm * 128 + mi * 16 + lr;
-        if (row >= g.M) continue;
-        f32x4 v = acc[mi][ni] + bv;
-        if constexpr (EPI == EPI_PARTIAL) {
-          *(f32x4*)((float*)g.C + blockIdx.z * g.split_stride + row * g.ldc + col) = v;
-        } else if constexpr (EPI == VITMI_EPI_ACCUM) {
-          float* d = (float*)g.C + row * g.ldc + col;
-          *(f32x4*)d = *(const f32x4*)d + v;
-        } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
-          const f32x4 rv = *(const f32x4*)(g.residual + row * g.ldr + col);
-          *(f32x4*)((float*)g.C + row * g.ldc + col) = rv + v;
-        } else {
+        for (int mi = 0; mi < 8; ++mi) {
+          const int64_t row = min(m0 + wm * 128 + mi * 16 + lr, g.M - 1);
+          if constexpr (EPI == VITMI_EPI_RESIDUAL) ld4[mi] = *(const f32x4*)(g.residual + row * g.ldr + col);
+          if constexpr (EPI == VITMI_EPI_ACCUM) ld4[mi] = *(const f32x4*)((const float*)g.C + row * g.ldc + col);
+          if constexpr (EPI == VITMI_EPI_DGELU) ldu[mi] = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + col);
+        }
+        __amdgpu_buffer_rsrc_t ru = rc;
+        if constexpr (EPI == VITMI_EPI_BIAS_GELU)
+          ru = make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+          f32x4 v = acc[mi][ni] + bv;
+          const int soff = mi * rstride;
+          if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM) v += ld4[mi];
           if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
             bf16x4 u;
 #pragma unroll
@@ -518,24 +532,30 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
               gelu_fast_parts(v[e], cdf, pdf);
               v[e] = v[e] * cdf;
             }
-            *(bf16x4*)((bf16*)g.aux + row * g.ldaux + col) = u;
+            const uint32_t uoff = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldaux + wn * 64 + lc4) * 2);
+            const int usoff = (int)(mi * 16 * g.ldaux * 2);
+            asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                         :: "v"(__builtin_bit_cast(unsigned long long, u)), "v"(uoff), "s"(ru),
+                            "s"(usoff), "i"(ni * 32) : "memory");
           } else if constexpr (EPI == VITMI_EPI_DGELU) {
-            const bf16x4 u = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + col);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float uf = (float)u[e];
+              const float uf = (float)ldu[mi][e];
               float cdf, pdf;
               gelu_fast_parts(uf, cdf, pdf);
               v[e] *= cdf + uf * pdf;
             }
           }
-          if constexpr (sizeof(TC) == 2) {
+          if constexpr (CES == 4) {
+            asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                         :: "v"(v), "v"(vbase), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
+          } else {
             bf16x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-            *(bf16x4*)((bf16*)g.C + row * g.ldc + col) = o;
-          } else {
-            *(f32x4*)((float*)g.C + row * g.ldc + col) = v;
+            asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                         :: "v"(__builtin_bit_cast(unsigned long long, o)), "v"(vbase), "s"(rc),
+                            "s"(soff), "i"(ni * 32) : "memory");
           }
         }
       }
