@@ -406,40 +406,144 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     if (which == 3) stage_half<false, BKM>(sub(buf, 3), rb, g.ldb, k0, krow0, 1, wave, lane);
   };
 
-  Frag<bf16> af[4][2], bfr[2][2];
+  // Fragment registers, double-buffered so each phase's ds_reads overlap the previous
+  // phase's MFMAs: A sets X/Y (A0 halves in X, A1 in Y); B sets 0/1 alternate per K-step
+  // (B0 of a K-step is read once, used by p0 AND p3; B1 lives in the other set).
+  Frag<bf16> ax[4][2], ay[4][2], b0[2][2], b1[2][2];
   f32x4 acc[8][4];
-  auto read_a = [&](int buf, int h) {
-    const char* s = sub(buf, h);
+  // Lane-constant LDS offsets (the swizzles depend only on the lane, not on the fragment):
+  //  k-major image [128][64]: frag (tile j, ks) at line w*TW + 16j + l15, chunk (4ks+g)^s,
+  //    s = (l15>>1)&7  -> offset kofs[ks] + (w*TW + 16j)*128
+  //  m/n-major image [64][128] (transposed reads): lane (t=l&15, g, q=t>>2, p=t&3) reads
+  //    k-row ks*32 + 8g + 4i + q, chunk ((w*TW/8 + 2j + (p>>1)) ^ (2q + 8(g&1))) ->
+  //    offset mofs[j] + (ks*32 + 4i)*256
+  const int l15 = lane & 15, lg = lane >> 4, lq = l15 >> 2, lp = l15 & 3;
+  int kofs[2];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[mt][ks] = FragReader<bf16, AK, 128>::read(s, wm * 64 + mt * 16, ks * 32, lane);
+  for (int ks = 0; ks < 2; ++ks) kofs[ks] = l15 * 128 + (((4 * ks + lg) ^ ((l15 >> 1) & 7)) << 4);
+  auto mofs = [&](int cw, int j) {
+    return (8 * lg + lq) * 256 + (((cw + 2 * j + (lp >> 1)) ^ (2 * lq + 8 * (lg & 1))) << 4) + (lp & 1) * 8;
   };
-  auto read_b = [&](int buf, int h) {
-    const char* s = sub(buf, 2 + h);
+  int amofs[4], bmofs[2];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+  for (int j = 0; j < 4; ++j) amofs[j] = mofs(wm * 8, j);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bfr[nt][ks] = FragReader<bf16, BKM, 128>::read(s, wn * 32 + nt * 16, ks * 32, lane);
+  for (int j = 0; j < 2; ++j) bmofs[j] = mofs(wn * 4, j);
+  auto tr_read = [&](const char* p, int ofs) -> bf16x8 {
+    bf16x8 f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p + ofs + i * 1024));
+      bf16x4 b = __builtin_bit_cast(bf16x4, v);
+      f[4 * i + 0] = b[0]; f[4 * i + 1] = b[1]; f[4 * i + 2] = b[2]; f[4 * i + 3] = b[3];
+    }
+    return f;
   };
-#define G256_MMA(MH, NH)                                                                        \
+#define RD_A(DST, BUF, H)                                                                       \
+  do {                                                                                          \
+    const char* s_ = sub(BUF, H);                                                               \
+    _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                          \
+      if constexpr (AK) DST[mt][ks].v = *(const bf16x8*)(s_ + kofs[ks] + (wm * 64 + 16 * mt) * 128); \
+      else DST[mt][ks].v = tr_read(s_ + ks * 32 * 256, amofs[mt]);                              \
+    }                                                                                           \
+  } while (0)
+#define RD_B(DST, BUF, H)                                                                       \
+  do {                                                                                          \
+    const char* s_ = sub(BUF, 2 + H);                                                           \
+    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                          \
+      if constexpr (BKM) DST[nt][ks].v = *(const bf16x8*)(s_ + kofs[ks] + (wn * 32 + 16 * nt) * 128); \
+      else DST[nt][ks].v = tr_read(s_ + ks * 32 * 256, bmofs[nt]);                              \
+    }                                                                                           \
+  } while (0)
+#define MMA4(MH, NH, AS, BS)                                                                    \
   do {                                                                                          \
     __builtin_amdgcn_s_setprio(1);                                                              \
     _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
     _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                            \
-      acc[MH * 4 + mt][NH * 2 + nt] = mma(bfr[nt][ks], af[mt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
+      acc[MH * 4 + mt][NH * 2 + nt] = mma(BS[nt][ks], AS[mt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
     __builtin_amdgcn_s_setprio(0);                                                              \
   } while (0)
+  // One K-step s (buffer buf = s & 1).  Entry: A0(s) in ax, B0(s) in BP (preloaded).
+  // Each half of buffer buf is refilled for step s+2 right after its last ds_read, so every
+  // DMA has ~2 K-steps to land:  p0 refills A0,B0 (read at p3 of s-1);  p3 refills B1,A1
+  // (read at p0/p1 of s).  Issue order per step: [A0,B0]@p0 [B1,A1]@p3, 2 instr per half.
+  // Waits: p0 needs B1(s),A1(s) -> leave the 8 younger instr of step s+1 in flight;
+  //        p3 needs A0(s+1),B0(s+1) -> leave B1,A1(s+1) [+ A0,B0(s+2)] in flight.
+  // lgkmcnt(0) before each barrier retires this wave's reads of the halves about to be
+  // refilled (WAR).  Leaves A0(s+1) in ax, B0(s+1) in BQ.
+#define KSTEP(BP, BQ)                                                                           \
+  do {                                                                                          \
+    /* p0 (A0,B0) */                                                                            \
+    if (has1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");                       \
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                            \
+    barrier();                                                                                  \
+    if (has2) { issue(s2a, s2b, s2t, buf, 0); issue(s2a, s2b, s2t, buf, 1); }                   \
+    RD_B(BQ, buf, 1);                                                                           \
+    MMA4(0, 0, ax, BP);                                                                         \
+    /* p1 (A0,B1) */                                                                            \
+    RD_A(ay, buf, 1);                                                                           \
+    MMA4(0, 1, ax, BQ);                                                                         \
+    /* p2 (A1,B1) */                                                                            \
+    MMA4(1, 1, ay, BQ);                                                                         \
+    /* p3 (A1,B0): refill B1/A1 for s+2, preload A0/B0 of s+1 from the other buffer */          \
+    if (has1) {                                                                                 \
+      if (has2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");                     \
+      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");                          \
+    } else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
+    barrier();                                                                                  \
+    if (has2) { issue(s2a, s2b, s2t, buf, 3); issue(s2a, s2b, s2t, buf, 2); }                   \
+    if (has1) { RD_A(ax, buf ^ 1, 0); RD_B(BQ, buf ^ 1, 0); }                                   \
+    MMA4(1, 0, ay, BP);                                                                         \
+  } while (0)
+
+  // Shallow variant (1 K-step ahead): each phase stages one half of step s+1 into the
+  // other buffer (A0@p0 B0@p1 A1@p2 B1@p3); waits vmcnt(2) at p0, vmcnt(4) at p3.  Measured
+  // faster than KSTEP for layouts with m/n-major operands (transposed LDS reads).
+#define KSTEP1(BP, BQ)                                                                          \
+  do {                                                                                          \
+    if (has1) { issue(s1a, s1b, s1t, buf ^ 1, 0); asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); } \
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                       \
+    barrier();                                                                                  \
+    RD_B(BQ, buf, 1);                                                                           \
+    MMA4(0, 0, ax, BP);                                                                         \
+    if (has1) issue(s1a, s1b, s1t, buf ^ 1, 1);                                                 \
+    RD_A(ay, buf, 1);                                                                           \
+    MMA4(0, 1, ax, BQ);                                                                         \
+    if (has1) issue(s1a, s1b, s1t, buf ^ 1, 2);                                                 \
+    MMA4(1, 1, ay, BQ);                                                                         \
+    if (has1) {                                                                                 \
+      issue(s1a, s1b, s1t, buf ^ 1, 3);                                                         \
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                          \
+      barrier();                                                                                \
+      RD_A(ax, buf ^ 1, 0);                                                                     \
+      RD_B(BQ, buf ^ 1, 0);                                                                     \
+    }                                                                                           \
+    MMA4(1, 0, ay, BP);                                                                         \
+  } while (0)
+  constexpr bool DEEP = AK && BKM;
 
   int tile = t_begin + jx;
   if (tile >= t_end) return;
   int64_t m0 = (int64_t)(tile / g.tiles_n) * BM, n0 = (int64_t)(tile % g.tiles_n) * BN;
   __amdgpu_buffer_rsrc_t ra = rsrc_a(m0), rb = rsrc_b(n0);
   int buf = 0;
-  issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 2); issue(ra, rb, 0, 0, 3);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A0, B0 of the first K-step landed
-  barrier();
+  {
+    // prologue: steps 0 and 1 of the first tile (nk >= 2 is a launch precondition)
+    if constexpr (DEEP) {
+      issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 3); issue(ra, rb, 0, 0, 2);
+      issue(ra, rb, 1, 1, 0); issue(ra, rb, 1, 1, 1); issue(ra, rb, 1, 1, 3); issue(ra, rb, 1, 1, 2);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // A0(0), B0(0) landed
+    } else {
+      issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 2); issue(ra, rb, 0, 0, 3);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");    // A0(0), B0(0) landed
+    }
+    barrier();
+    RD_A(ax, 0, 0);
+    RD_B(b0, 0, 0);
+  }
 
   const int lc4 = 4 * (lane >> 4), lr = lane & 15;
   for (;;) {
@@ -453,36 +557,40 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int t = 0; t < nk; ++t) {
-      // the K-step staged next: (this tile, t+1) or (next tile, 0)
-      const bool more = (t + 1 < nk) || has_next;
-      const __amdgpu_buffer_rsrc_t sa = (t + 1 < nk) ? ra : ran;
-      const __amdgpu_buffer_rsrc_t sb = (t + 1 < nk) ? rb : rbn;
-      const int tn = (t + 1 < nk) ? t + 1 : 0;
-      const int nbuf = buf ^ 1;
-      // Barriers only where a DMA wait must become visible to every wave (after p0's and
-      // p3's counted waits); between them the next phase's ds_reads may overlap MFMAs.
-      // p0 (A0,B0)
-      read_a(buf, 0); read_b(buf, 0);
-      if (more) { issue(sa, sb, tn, nbuf, 0); asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      barrier();
-      G256_MMA(0, 0);
-      // p1 (A0,B1)
-      read_b(buf, 1);
-      if (more) issue(sa, sb, tn, nbuf, 1);
-      G256_MMA(0, 1);
-      // p2 (A1,B1)
-      read_a(buf, 1);
-      if (more) issue(sa, sb, tn, nbuf, 2);
-      G256_MMA(1, 1);
-      // p3 (A1,B0)
-      read_b(buf, 0);
-      if (more) { issue(sa, sb, tn, nbuf, 3); asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
-      barrier();
-      G256_MMA(1, 0);
-      buf = nbuf;
+    // K-loop unrolled by 2 so the B register sets alternate statically
+#define STEP_SETUP(T)                                                                           \
+    const bool has1 = ((T) + 1 < nk) || has_next;                                               \
+    const bool has2 = ((T) + 2 < nk) || has_next;                                               \
+    const __amdgpu_buffer_rsrc_t s2a = ((T) + 2 < nk) ? ra : ran;                               \
+    const __amdgpu_buffer_rsrc_t s2b = ((T) + 2 < nk) ? rb : rbn;                               \
+    const int s2t = ((T) + 2 < nk) ? (T) + 2 : (T) + 2 - nk;                                    \
+    const __amdgpu_buffer_rsrc_t s1a = ((T) + 1 < nk) ? ra : ran;                               \
+    const __amdgpu_buffer_rsrc_t s1b = ((T) + 1 < nk) ? rb : rbn;                               \
+    const int s1t = ((T) + 1 < nk) ? (T) + 1 : 0;
+    for (int t = 0; t < nk; t += 2) {
+      {
+        STEP_SETUP(t)
+        if constexpr (DEEP) KSTEP(b0, b1); else KSTEP1(b0, b1);
+        buf ^= 1;
+      }
+      if (t + 1 < nk) {
+        STEP_SETUP(t + 1)
+        if constexpr (DEEP) KSTEP(b1, b0); else KSTEP1(b1, b0);
+        buf ^= 1;
+      } else {
+        // odd step count: the next tile's B0 was preloaded into b1
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) b0[nt][ks] = b1[nt][ks];
+      }
     }
+#undef STEP_SETUP
+#undef KSTEP
+#undef KSTEP1
+#undef MMA4
+#undef RD_A
+#undef RD_B
 
     // ---- epilogue straight from registers: acc[mi][ni] = C^T tile; lane owns row
     // m0 + wm*128 + mi*16 + lr, columns n0 + wn*64 + ni*16 + lc4 .. +3.
@@ -735,16 +843,33 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
     const size_t need = (size_t)splits * M * N * sizeof(float);
     if (ws == nullptr || ws_bytes < need) splits = 1, g.k_per_split = ktiles * BK;
   }
+  bool big2 = big;
+  if (big2) {
+    // gemm256 keeps two K-steps in flight: every split must span >= 2 k-tiles
+    const int64_t kps = g.k_per_split / BK;
+    const int64_t last = ktiles - (int64_t)(splits - 1) * kps;
+    if (ktiles < 2 || kps < 2 || last < 2) {
+      if (splits > 1 && ktiles >= 4) {
+        int64_t k2 = kps + 1;
+        while (ktiles - ((ktiles + k2 - 1) / k2 - 1) * k2 < 2) ++k2;
+        g.k_per_split = k2 * BK;
+        splits = (int)((ktiles + k2 - 1) / k2);
+      } else {
+        big2 = false;
+      }
+    }
+  }
+  const bool big_ok = big2;
   if (splits == 1) {
     g.k_per_split = (K > 0 ? ktiles : 1) * BK;
-    if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, big, s);
-    return dispatch<float>(ak, bk, c_dtype, epi, g, 1, big, s);
+    if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
+    return dispatch<float>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
   }
   // split-K: partial slabs then one reduction pass into C (+=)
   GemmArgs gp = g;
   gp.C = ws; gp.ldc = N; gp.split_stride = M * N;
-  int rc = dtype == VITMI_BF16 ? dispatch<bf16>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big, s)
-                               : dispatch<float>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big, s);
+  int rc = dtype == VITMI_BF16 ? dispatch<bf16>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big_ok, s)
+                               : dispatch<float>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big_ok, s);
   if (rc) return rc;
   VITMI_CHECK_ARG(ldc == N, "gemm: split-K accumulate needs a dense C");
   const int64_t n = M * N;
