@@ -97,12 +97,14 @@ size_t vitmi_bias_grad_workspace_size(int64_t M, int64_t N);
 int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const float* gamma,
                         const float* beta, float eps, void* y, int y_dtype, int64_t ldy,
                         float* mean, float* rstd, vitmi_stream_t stream);
-/* dx = dres + LN'(dy); optional low-precision copy dx_lp (bf16); dgamma/dbeta += (fp32). */
+/* dx = dres + LN'(dy); optional low-precision copy dx_lp (bf16); dgamma/dbeta += (fp32);
+ * optional dxsum[D] += column sums of dx (the bias gradient of the Dense layer whose output
+ * gradient dx is: fused so that gradient is never re-read). NULL pointers skip outputs. */
 int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtype, int64_t lddy,
                         const float* x, int64_t ldx, const float* mean, const float* rstd,
                         const float* gamma, const float* dres, int64_t ldres, float* dx,
                         int64_t lddx, void* dx_lp, int64_t lddx_lp, float* dgamma, float* dbeta,
-                        void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+                        float* dxsum, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D);
 
 /* ---------------------------------------------------------------------------

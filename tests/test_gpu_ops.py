@@ -107,14 +107,16 @@ def test_layernorm_fwd_bwd(D, T):
     dy = rnd(M, D, seed=18).to(T)
     dres = rnd(M, D, seed=19)
     dg, dbb = torch.full((D,), 0.5, device=DEV), torch.full((D,), -0.5, device=DEV)
+    dsum = torch.full((D,), 2.0, device=DEV)
     dx, dx_lp = ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, w.to(DEV), dg, dbb, dres=dres.to(DEV),
-                                  lp_dtype=BF)
+                                  lp_dtype=BF, dxsum=dsum)
     xx, ww, bb = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
     F.layer_norm(xx, (D,), ww, bb, 1e-6).backward(dy.float())
     assert rel(dx, xx.grad + dres) < 1e-5
     assert rel(dx_lp.float(), xx.grad + dres) < 5e-3
     assert rel(dg, 0.5 + ww.grad) < 1e-5
     assert rel(dbb, -0.5 + bb.grad) < 1e-5
+    assert rel(dsum, 2.0 + (xx.grad + dres).sum(0)) < 1e-5   # fused bias-grad column sums
 
 
 def test_layernorm_strided_rows():

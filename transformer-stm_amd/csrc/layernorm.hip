@@ -85,15 +85,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float* __restrict__ gamma, const float* __restrict__ dres, int64_t ldres,
     float* __restrict__ dx, int64_t lddx, bf16* __restrict__ dx_lp, int64_t lddx_lp,
     float* __restrict__ part) {
-  __shared__ f32x4 red[4][64 * NV * 2];
+  __shared__ f32x4 red[4][64 * NV * 3];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  f32x4 g[NV], dg[NV], db[NV];
+  f32x4 g[NV], dg[NV], db[NV], ds[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 4;
     g[i] = c < D ? *(const f32x4*)(gamma + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     dg[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     db[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ds[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < M; row += (int64_t)gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
@@ -124,52 +125,57 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       if (c < D) {
         f32x4 o = (gy[i] - c1 - xh[i] * c2) * rs;
         if (dres) o += *(const f32x4*)(dres + row * ldres + c);
+        ds[i] += o;
         *(f32x4*)(dx + row * lddx + c) = o;
         if (LP) store4<bf16>(dx_lp + row * lddx_lp + c, o);
       }
     }
   }
-  // block-reduce dgamma/dbeta partials over the 4 waves
+  // block-reduce dgamma / dbeta / colsum(dx) partials over the 4 waves
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     red[wave][i * 64 + lane] = dg[i];
     red[wave][(NV + i) * 64 + lane] = db[i];
+    red[wave][(2 * NV + i) * 64 + lane] = ds[i];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < NV * 2 * 64; e += 256) {
+  for (int e = threadIdx.x; e < NV * 3 * 64; e += 256) {
     const f32x4 t = red[0][e] + red[1][e] + red[2][e] + red[3][e];
-    const int which = e / (NV * 64);          // 0 = dgamma, 1 = dbeta
+    const int which = e / (NV * 64);          // 0 = dgamma, 1 = dbeta, 2 = colsum(dx)
     const int i = (e % (NV * 64)) / 64, l = e % 64;
     const int c = (l + 64 * i) * 4;
     if (c < D) *(f32x4*)(part + ((int64_t)which * gridDim.x + blockIdx.x) * D + c) = t;
   }
 }
 
-// out[d] += sum_b part[b][d] for dgamma (rows 0..G-1) and dbeta (rows G..2G-1).
+// out[d] += sum_b part[b][d] for dgamma (rows 0..G-1), dbeta (G..2G-1), colsum(dx) (2G..3G-1).
 // 1024 threads = 16 waves x 64 columns; wave w sums rows w, w+16, ... (fixed order:
 // deterministic), then a 16-way LDS reduction.
 __global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int G, int D,
                                                         float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta) {
-  __shared__ float red[2][16][64];
+                                                        float* __restrict__ dbeta,
+                                                        float* __restrict__ dxsum) {
+  __shared__ float red[3][16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int d = blockIdx.x * 64 + lane;
-  float a = 0.f, b = 0.f;
+  float a = 0.f, b = 0.f, c = 0.f;
   if (d < D) {
 #pragma unroll 4
     for (int i = w; i < G; i += 16) {
       a += part[(int64_t)i * D + d];
       b += part[(int64_t)(G + i) * D + d];
+      if (dxsum) c += part[(int64_t)(2 * G + i) * D + d];
     }
   }
   red[0][w][lane] = a;
   red[1][w][lane] = b;
+  red[2][w][lane] = c;
   __syncthreads();
-  if (w < 2 && d < D) {
+  if (w < 3 && d < D) {
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += red[w][i][lane];
-    float* out = w == 0 ? dgamma : dbeta;
+    float* out = w == 0 ? dgamma : (w == 1 ? dbeta : dxsum);
     if (out) out[d] += s;
   }
 }
@@ -233,15 +239,15 @@ extern "C" int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx
 }
 
 extern "C" size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D) {
-  return (size_t)2 * ln_blocks_bwd(M) * D * sizeof(float);
+  return (size_t)3 * ln_blocks_bwd(M) * D * sizeof(float);
 }
 
 extern "C" int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtype, int64_t lddy,
                                    const float* x, int64_t ldx, const float* mean,
                                    const float* rstd, const float* gamma, const float* dres,
                                    int64_t ldres, float* dx, int64_t lddx, void* dx_lp,
-                                   int64_t lddx_lp, float* dgamma, float* dbeta, void* workspace,
-                                   size_t ws_bytes, vitmi_stream_t stream) {
+                                   int64_t lddx_lp, float* dgamma, float* dbeta, float* dxsum,
+                                   void* workspace, size_t ws_bytes, vitmi_stream_t stream) {
   VITMI_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "layernorm: D must be a multiple of 4 in [4, 2048]");
   if (M == 0) return VITMI_OK;
   VITMI_CHECK_ARG(dy && x && mean && rstd && gamma && dx, "layernorm_bwd: null pointer");
@@ -267,7 +273,7 @@ extern "C" int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtyp
   }
 #undef LNB
   hipLaunchKernelGGL(ln_param_reduce, dim3((D + 63) / 64), dim3(1024), 0, s, (const float*)part, G,
-                     D, dgamma, dbeta);
+                     D, dgamma, dbeta, dxsum);
   VITMI_LAUNCH_CHECK("layernorm_bwd");
   return VITMI_OK;
 }

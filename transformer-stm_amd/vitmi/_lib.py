@@ -37,7 +37,7 @@ SIGNATURES = {
     "vitmi_bias_grad": (I, [I, L, L, P, L, P, P, S, P]),
     "vitmi_bias_grad_workspace_size": (S, [L, L]),
     "vitmi_layernorm_fwd": (I, [L, I, P, L, P, P, F, P, I, L, P, P, P]),
-    "vitmi_layernorm_bwd": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, P, P, S, P]),
+    "vitmi_layernorm_bwd": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, P, P, P, S, P]),
     "vitmi_layernorm_bwd_workspace_size": (S, [L, I]),
     "vitmi_attention_fwd": (I, [I, I, I, I, I, F, P, P, P, P]),
     "vitmi_attention_bwd": (I, [I, I, I, I, I, F, P, P, P, P, P, P, S, P]),

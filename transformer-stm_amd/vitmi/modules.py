@@ -265,12 +265,16 @@ class Block(nn.Module):
 
     def forward(self, x: Tensor, h: Optional[int] = None, w: Optional[int] = None) -> Tensor:
         _check_cuda(x)
-        return _BlockFn.apply(x, self, *self.parameters())
+        return _BlockFn.apply(x, self, None, False, *self.parameters())
 
 
 class _BlockFn(torch.autograd.Function):
+    """Fused block.  ``prev_fc2_bias``: the fc2 bias of the block feeding this one; its grad is
+    colsum(d input), produced for free by this block's LN1 backward.  ``fc2_bias_done``: this
+    block's own fc2 bias grad was already accumulated by its consumer (next block or head)."""
+
     @staticmethod
-    def forward(ctx, x, blk, *params):
+    def forward(ctx, x, blk, prev_fc2_bias, fc2_bias_done, *params):
         T = ops.torch_dtype(blk.dtype)
         B, N, D = x.shape
         M = B * N
@@ -290,6 +294,7 @@ class _BlockFn(torch.autograd.Function):
         out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
         ctx.blk, ctx.shape = blk, (B, N, D)
+        ctx.prev_bias, ctx.bias_done = prev_fc2_bias, fc2_bias_done
         return out.view(B, N, D)
 
     @staticmethod
@@ -306,30 +311,32 @@ class _BlockFn(torch.autograd.Function):
         # MLP branch
         du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u)
         ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
-        ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
-        dh2 = ops.linear_dgrad(du, w1, F32)
+        if not ctx.bias_done:
+            ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
+        dh2 = ops.linear_dgrad(du, w1, T)
         ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
         ops.bias_grad(du, _grad(mlp.fc1.bias))
+        # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
         dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias),
-                                        dres=g2, lp_dtype=lpT)
+                                        dres=g2, lp_dtype=lpT, dxsum=_grad(a_.proj.bias))
         if dx1_lp is None:
             dx1_lp = dx1
         # attention branch
         do = ops.linear_dgrad(dx1_lp, wo, T)
         ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
-        ops.bias_grad(dx1_lp, _grad(a_.proj.bias))
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale)
-        dh1 = ops.linear_dgrad(dqkv, wq, F32)
+        dh1 = ops.linear_dgrad(dqkv, wq, T)
         ops.linear_wgrad(dqkv, h1, _grad(a_.qkv.weight))
         if a_.qkv.bias is not None:
             ops.bias_grad(dqkv, _grad(a_.qkv.bias))
+        prev = ctx.prev_bias
         dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
-                                      dres=dx1, lp_dtype=lpT)
+                                      dres=dx1, lp_dtype=lpT, dxsum=_grad(prev) if prev is not None else None)
         _stash(dx, dx_lp)
         hook = getattr(blk, "_grad_ready_hook", None)
         if hook is not None:
             hook(blk)
-        return (dx.view(B, N, D), None) + (None,) * (len(ctx.needs_input_grad) - 2)
+        return (dx.view(B, N, D), None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
 
 
 # ======================================================================= embedding
@@ -429,8 +436,9 @@ class _HeadFn(torch.autograd.Function):
         dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), _grad(head.weight),
                           _grad(head.bias) if head.bias is not None else None)
         dx = torch.zeros_like(x)
+        last_fc2_bias = model.blocks[-1].mlp.fc2.bias if len(model.blocks) else None
         ops.layernorm_bwd(dy, x[:, 0], mean, rstd, norm.weight, _grad(norm.weight), _grad(norm.bias),
-                          dx=dx[:, 0])
+                          dx=dx[:, 0], dxsum=_grad(last_fc2_bias) if last_fc2_bias is not None else None)
         hook = getattr(model, "_head_ready_hook", None)
         if hook is not None:
             hook()
@@ -601,8 +609,11 @@ class VisionTransformer(nn.Module):
             arena.bind_grads()
         pe = self.patch_embed
         t = _EmbedFn.apply(x, pe, self.cls_token, self.pos_embed, *pe.parameters())
-        for blk in self.blocks:
-            t = _BlockFn.apply(t, blk, *blk.parameters())
+        # bias-grad fusion: block i's LN1 backward produces colsum(d input) = the fc2 bias grad
+        # of block i-1; the head's LN backward does it for the last block.
+        for i, blk in enumerate(self.blocks):
+            prev_bias = self.blocks[i - 1].mlp.fc2.bias if i > 0 else None
+            t = _BlockFn.apply(t, blk, prev_bias, True, *blk.parameters())
         return t
 
     def forward(self, x: Tensor) -> Tensor:

@@ -158,8 +158,10 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.
 
 def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
                   dgamma: Optional[Tensor], dbeta: Optional[Tensor], dres: Optional[Tensor] = None,
-                  dx: Optional[Tensor] = None, lp_dtype: Optional[torch.dtype] = None):
-    """dx = dres + LN'(dy); dgamma/dbeta (fp32) +=.  Returns (dx fp32, dx_lp or None).
+                  dx: Optional[Tensor] = None, lp_dtype: Optional[torch.dtype] = None,
+                  dxsum: Optional[Tensor] = None):
+    """dx = dres + LN'(dy); dgamma/dbeta (fp32) +=; dxsum += column sums of dx.
+    Returns (dx fp32, dx_lp or None).
 
     ``dx`` may be a pre-allocated (possibly row-strided) fp32 destination."""
     M, ldy = _rows(dy)
@@ -175,7 +177,7 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
     ws = _ws(lib().vitmi_layernorm_bwd_workspace_size(M, D), x)
     check(lib().vitmi_layernorm_bwd(M, D, _p(dy), dt(dy.dtype), ldy, _p(x), ldx, _p(mean), _p(rstd), _p(w),
                                     _p(dres), ldres, _p(dx), lddx, _p(dx_lp), D, _p(dgamma), _p(dbeta),
-                                    _p(ws), ws.numel(), _s()), "layernorm_bwd")
+                                    _p(dxsum), _p(ws), ws.numel(), _s()), "layernorm_bwd")
     return dx, dx_lp
 
 
