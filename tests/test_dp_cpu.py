@@ -1,0 +1,89 @@
+"""Data-parallel gradient reduction on CPU with the gloo backend (world_size 2).
+
+Covers vitmi.dp.GradReducer: buckets over the flat gradient buffer are launched only when
+their whole range is inside the finished prefix (backward order), every bucket is reduced
+exactly once, and the result is the mean over ranks — the semantics of the reference's
+MirroredStrategy cross-replica reduction (old_codes/BayConvT(Par)(Muti).py:16-19)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from vitmi import dp
+from vitmi.config import ViTConfig
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        # 1) raw reducer: 10 buckets of 1 KiB (256 floats) over a 2500-element buffer
+        n = 2500
+        flat = torch.arange(n, dtype=torch.float32) * (rank + 1)
+        red = dp.GradReducer(flat, bucket_mb=256 * 4 / (1 << 20))
+        red.start()
+        red.mark_ready(700)              # only buckets ending <= 700 may launch
+        out["early"] = [b for _, b in red.launch_log]
+        red.mark_ready(2500)
+        red.finish()
+        out["flat"] = flat.clone()
+        out["nbuckets"] = len(red.bounds)
+        out["launched"] = sorted(b for _, b in red.launch_log)
+        # 2) attached to a (CPU-resident) model arena, hooks fired in backward order
+        from vitmi.modules import VisionTransformer
+        torch.manual_seed(0)
+        m = VisionTransformer(ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=3, num_heads=2,
+                                        dtype="fp32"))
+        r2 = dp.attach(m, bucket_mb=0.1)
+        arena = m.arena()
+        arena.grad.copy_(torch.full_like(arena.grad, float(rank + 1)))
+        r2.start()
+        m._head_ready_hook()
+        for blk in reversed(m.blocks):
+            blk._grad_ready_hook(blk)
+        m.patch_embed._grad_ready_hook(m.patch_embed)
+        r2.finish()
+        out["arena_mean"] = arena.grad.clone()
+        out["arena_order"] = [b for _, b in r2.launch_log]
+        dp.broadcast_parameters(m)
+        out["param0"] = arena.flat[:8].clone()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_grad_reducer_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    n = 2500
+    expect = torch.arange(n, dtype=torch.float32) * 1.5        # mean of 1x and 2x
+    for r in range(world):
+        o = res[r]
+        assert torch.allclose(o["flat"], expect)
+        # 1 KiB buckets = 256 elements: only buckets [0,256) and [256,512) end <= 700
+        assert o["early"] == [0, 1]
+        assert o["launched"] == list(range(o["nbuckets"]))
+        assert torch.allclose(o["arena_mean"], torch.full_like(o["arena_mean"], 1.5))
+        assert o["arena_order"] == sorted(o["arena_order"])    # front-to-back readiness
+        assert torch.equal(o["param0"], res[0]["param0"])       # broadcast from rank 0
