@@ -36,9 +36,9 @@ enum { VITMI_F32 = 0, VITMI_BF16 = 1 };
 /* GEMM epilogues (all apply `bias` (fp32, may be NULL) first where it applies) */
 enum {
   VITMI_EPI_STORE = 0,     /* C = acc + bias                                        */
-  VITMI_EPI_BIAS_GELU = 1, /* aux = acc + bias (pre-activation), C = gelu(aux)       */
+  VITMI_EPI_BIAS_GELU = 1, /* u = acc + bias: C = gelu(u), aux = gelu'(u) (saved)     */
   VITMI_EPI_RESIDUAL = 2,  /* C(f32) = residual(f32) + acc + bias                    */
-  VITMI_EPI_DGELU = 3,     /* C = acc * gelu'(aux)                                  */
+  VITMI_EPI_DGELU = 3,     /* C = acc * aux   (aux = gelu'(u) from BIAS_GELU)        */
   VITMI_EPI_ACCUM = 4      /* C(f32) += acc                                          */
 };
 
@@ -54,7 +54,7 @@ int vitmi_device_cus(void);
  *   a_kmajor=1: A stored [M][lda] (k contiguous);  0: A stored [K][lda] (m contiguous)
  *   b_kmajor=1: B stored [N][ldb] (k contiguous);  0: B stored [K][ldb] (n contiguous)
  *   dtype: operand type (VITMI_BF16 -> v_mfma_f32_16x16x32_bf16, VITMI_F32 -> v_mfma_f32_16x16x4_f32)
- *   c_dtype: output type; aux (epilogue GELU pre-activation) has the operand dtype.
+ *   c_dtype: output type; aux (the saved GELU derivative gelu'(u)) has the operand dtype.
  *   k-major operands need K % 64 == 0 (bf16) / K % 32 == 0 (f32); ragged M/N and a
  *   ragged reduction over m-major operands are zero-filled by the buffer range check.
  * Replaces the reference's Dense/EinsumDense MatMul and their autodiff transposes
@@ -77,7 +77,7 @@ size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajor, int64_t 
 int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, const void* x, const void* w,
                      const float* bias, void* y, int y_dtype, int epilogue, void* aux,
                      const float* residual, vitmi_stream_t stream);
-/* dx[M,K] = dy[M,N] W[N,K]   (epilogue STORE or DGELU with aux = pre-activation [M,K]) */
+/* dx[M,K] = dy[M,N] W[N,K]   (epilogue STORE or DGELU with aux = gelu'(u) [M,K]) */
 int vitmi_linear_dgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* w,
                        void* dx, int dx_dtype, int epilogue, const void* aux,
                        vitmi_stream_t stream);

@@ -48,13 +48,18 @@ def test_linear_fwd_store(M, N, K, T, policy):
     assert rel(y.float(), ref) < (8e-3 if T == BF else 1e-5)
 
 
+def gelu_grad(u):
+    """d/du of the exact-erf GELU: Phi(u) + u phi(u)."""
+    return 0.5 * (1 + torch.erf(u / 2 ** 0.5)) + u * torch.exp(-0.5 * u * u) / (2 * torch.pi) ** 0.5
+
+
 @pytest.mark.parametrize("T", [BF, torch.float32])
 def test_linear_fwd_gelu_and_residual(T, policy):
     M, N, K = 394, 768, 192
     x, w, b = rnd(M, K, dtype=T, seed=4), rnd(N, K, dtype=T, seed=5, scale=0.05), rnd(N, seed=6)
     u_ref = x.float() @ w.float().t() + b
-    a, u = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), T, ops.EPI_BIAS_GELU)
-    assert rel(u.float(), u_ref) < (8e-3 if T == BF else 1e-5)
+    a, gp = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), T, ops.EPI_BIAS_GELU)
+    assert rel(gp.float(), gelu_grad(u_ref)) < (8e-3 if T == BF else 1e-5)   # saved gelu'(u)
     assert rel(a.float(), F.gelu(u_ref)) < (8e-3 if T == BF else 1e-5)
     r = rnd(M, N, seed=7)
     y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), torch.float32, ops.EPI_RESIDUAL, residual=r.to(DEV))
@@ -68,9 +73,10 @@ def test_linear_dgrad(M, N, K, T, policy):
     ref = dy.float() @ w.float()
     dx = ops.linear_dgrad(dy.to(DEV), w.to(DEV), torch.float32)
     assert rel(dx, ref) < 1e-5
-    u = rnd(M, K, dtype=T, seed=10)
-    dg = ops.linear_dgrad(dy.to(DEV), w.to(DEV), T, ops.EPI_DGELU, aux=u.to(DEV))
-    uu = u.float().requires_grad_(True)
+    u = rnd(M, K, seed=10)
+    gp = gelu_grad(u).to(T)                       # what the BIAS_GELU forward saved
+    dg = ops.linear_dgrad(dy.to(DEV), w.to(DEV), T, ops.EPI_DGELU, aux=gp.to(DEV))
+    uu = u.requires_grad_(True)
     gl = torch.autograd.grad(F.gelu(uu), uu, ref)[0]
     assert rel(dg.float(), gl) < (8e-3 if T == BF else 1e-5)
 
@@ -146,12 +152,24 @@ def attn_ref(qkv, B, N, H, scale):
     return o, lse
 
 
-ATT = [(2, 197, 2), (1, 17, 3), (2, 64, 1), (1, 577, 2), (3, 1, 2), (1, 130, 1)]
+ATT = [(2, 197, 2), (1, 17, 3), (2, 64, 1), (1, 577, 2), (3, 1, 2), (1, 130, 1), (1, 256, 1), (2, 255, 1),
+       (1, 33, 2), (1, 96, 1), (1, 300, 1)]
+
+
+@pytest.fixture(params=["seq", "stream"])
+def attn_path(request, monkeypatch):
+    """bf16 N <= 256 runs the whole-sequence kernels; VITMI_ATTN_STREAM=1 forces the streamed
+    ones (read by the library on every call), so both are checked at the same sizes."""
+    if request.param == "stream":
+        monkeypatch.setenv("VITMI_ATTN_STREAM", "1")
+    return request.param
 
 
 @pytest.mark.parametrize("B,N,H", ATT)
 @pytest.mark.parametrize("T", [BF, torch.float32])
-def test_attention_fwd_bwd(B, N, H, T):
+def test_attention_fwd_bwd(B, N, H, T, attn_path):
+    if attn_path == "stream" and (T != BF or N > 256):
+        pytest.skip("same kernels as the default path")
     D = 64 * H
     scale = 64 ** -0.5
     qkv = rnd(B * N, 3 * D, dtype=T, seed=22)
@@ -171,7 +189,7 @@ def test_attention_fwd_bwd(B, N, H, T):
         assert rel(d[:, i], g[:, i]) < (2e-2 if T == BF else 1e-5), name
 
 
-def test_attention_softmax_spike():
+def test_attention_softmax_spike(attn_path):
     """A key row that dominates one query forces the online-softmax rescale branch."""
     B, N, H = 1, 197, 1
     qkv = rnd(B * N, 192, seed=24) * 0.5

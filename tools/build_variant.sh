@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build libvitmi.so from a modified copy of csrc/ for A/B kernel timing:
+#   tools/build_variant.sh NAME SRC_DIR   -> transformer-stm_amd/build/variants/NAME.so
+# SRC_DIR must sit two levels below a directory holding include/ (mirror of the repo layout).
+set -e
+name=$1; src=$2
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/transformer-stm_amd/build/variants
+mkdir -p $out /tmp/vb_$name
+objs=""
+for f in abi.cpp gemm.hip attention.hip layernorm.hip elementwise.hip; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c $src/$f -o /tmp/vb_$name/$f.o &
+  objs="$objs /tmp/vb_$name/$f.o"
+done
+wait
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/$name.so $objs
+echo built $out/$name.so

@@ -50,11 +50,17 @@ def main():
                                        2 * M * D * D),
         "fc2 dgrad dGELU[M,3072,768]": (lambda: ops.linear_dgrad(x, w2, BF, ops.EPI_DGELU, aux=h), 2 * M * F * D),
         "fc1 dgrad f32  [M,768,3072]": (lambda: ops.linear_dgrad(h, w1, torch.float32), 2 * M * F * D),
+        "fc1 dgrad bf16 [M,768,3072]": (lambda: ops.linear_dgrad(h, w1, BF), 2 * M * F * D),
+        "qkv dgrad bf16 [M,768,2304]": (lambda: ops.linear_dgrad(gq, wq, BF), 2 * M * 3 * D * D),
+        "proj dgrad bf16[M,768,768]": (lambda: ops.linear_dgrad(x, wo, BF), 2 * M * D * D),
         "qkv dgrad f32  [M,768,2304]": (lambda: ops.linear_dgrad(gq, wq, torch.float32), 2 * M * 3 * D * D),
         "fc1 wgrad      [3072,768]/M": (lambda: ops.linear_wgrad(h, x, dw), 2 * M * F * D),
         "torch mm       [M,3072,768]": (lambda: torch.mm(x, w1.t()), 2 * M * F * D),
     }
+    only = os.environ.get("GEMM_BENCH_ONLY")
     for name, (fn, flops) in cases.items():
+        if only and not any(k in name for k in only.split(",")):
+            continue
         ms = t(fn, iters)
         print(f"{name}: {ms * 1e3:8.1f} us  {flops / ms / 1e9:7.1f} TFLOP/s", flush=True)
 

@@ -1,0 +1,43 @@
+"""torch.profiler view of the bench step (ViT-B/16, bs from argv): which host call sites
+launch the non-vitmi kernels (fills, copies).  usage: python tools/torch_prof.py [batch]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "transformer-stm_amd"))
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+from vitmi.config import config_c3  # noqa: E402
+from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    cfg = config_c3()
+    model = VisionTransformer(cfg).cuda()
+    model.reset_parameters(seed=0)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    arena = model.arena()
+    img = torch.rand(B, 3, 224, 224, device="cuda")
+    tgt = torch.randint(0, cfg.num_classes, (B,), device="cuda")
+
+    def step():
+        arena.grad.zero_()
+        loss = cross_entropy(model(img), tgt)
+        loss.backward()
+        opt.step()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=25), flush=True)
+    print(prof.key_averages(group_by_stack_n=6).table(sort_by="count", row_limit=30), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -20,12 +20,19 @@
 //   tiles streamed) + dQ kernel (queries on lanes, key tiles streamed); no atomics.
 // fp32 path: thread-per-row VALU kernels (exact fp32; the parity configuration).
 #include "common.h"
+#include <stdlib.h>
+#include <type_traits>
 
 namespace vitmi {
 
 static constexpr int DH = 64;
 static constexpr float LOG2E = 1.4426950408889634f;
 static constexpr float LN2 = 0.6931471805599453f;
+
+// raw v_exp_f32: exp2f() wraps it in denormal range handling (compare, select, ldexp: 5
+// extra VALU per element); softmax arguments are <= 0 and results below 2^-126 are
+// negligible next to the row sum, so the flush is harmless.  exp2(-inf) = 0.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ int att_swz(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
 
@@ -175,14 +182,14 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(const bf16* __restrict__ qk
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mn = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mn);  // m=-inf on the first tile -> 0
+      const float alpha = fexp2(m - mn);  // m=-inf on the first tile -> 0
       m = mn;
       float rs = 0.f;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(st[u][r] - mn);
+          const float p = fexp2(st[u][r] - mn);
           st[u][r] = p;
           rs += p;
         }
@@ -317,7 +324,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
           const f32x4 dl = *(const f32x4*)(rl + 64 + q4);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = exp2f(sa[4 * g4 + i] * c2 - L2[i]);
+            const float p = fexp2(sa[4 * g4 + i] * c2 - L2[i]);
             sa[4 * g4 + i] = p;
             dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
           }
@@ -427,7 +434,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = t * 64 + 32 * u + acc_row(r, h);
-          const float p = (key < N && qok) ? exp2f(st[r] * c2 - L2) : 0.f;
+          const float p = (key < N && qok) ? fexp2(st[r] * c2 - L2) : 0.f;
           dp[r] = p * (dp[r] - dl);
         }
         // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
@@ -452,6 +459,310 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
       const int d = 32 * d2 + 8 * g4 + 4 * h;
       store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale,
              dqt[d2][4 * g4 + 2] * scale, dqt[d2][4 * g4 + 3] * scale);
+    }
+}
+
+// ====================================================== whole-sequence kernels (bf16)
+// For N <= NPMAX = 256 (ViT: N = 197): ONE workgroup per (batch, head) with NW = ceil(N/32) waves
+// (wave w owns the 32 rows 32w..32w+31 of the lane-side operand).  The streamed operands of
+// the whole sequence are staged into LDS once (one DMA wait, one barrier); afterwards every
+// wave runs its loop with no synchronisation, so MFMA, softmax VALU and LDS reads of the
+// 2 x 7 co-resident waves interleave freely.  Rows are padded to NP = 32*NW only (the
+// streamed kernels above pad to 128 queries x 64 keys: 1.69x the work at N = 197, here 1.29x).
+
+// Stage rows [0, NP) (128 B of one head each) of a token-major matrix into an LDS image.
+__device__ __forceinline__ void stage_seq(char* lds, __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int np,
+                                          int nw, int wave, int lane) {
+  for (int p = wave; p < np / 8; p += nw) {
+    const int r = p * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ att_swz(r);
+    const uint32_t voff = (uint32_t)((int64_t)r * ld_bytes + c * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, lds + p * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// grid B*H, block 64*NW.  Online softmax over key tiles of 64 (a final tile of 32 when NP is
+// an odd multiple of 32); keys >= N exist only in the last tile and are masked there.
+template <int NPMAX>
+__global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __restrict__ qkv,
+                                                               bf16* __restrict__ o, float* __restrict__ lse,
+                                                               int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6, NP = nw * 32;
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  char* kt = smem;
+  char* vt = smem + NP * 128;
+  stage_seq(kt, rk, ldb, NP, nw, wave, lane);
+  stage_seq(vt, rv, ldb, NP, nw, wave, lane);
+  const int q = wave * 32 + (lane & 31);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const float c2 = scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x16 oacc[2] = {zero16(), zero16()};
+  auto tile = [&](auto uc, int k0) {
+    constexpr int U = decltype(uc)::value;
+    f32x16 st[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      st[u] = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st[u] = mfma32(frag_row(kt, k0 + 32 * u, s, lane), qf[s], st[u]);
+    }
+    if (k0 + 32 * U > N) {   // last tile: keys >= N out of the softmax
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (k0 + 32 * u + acc_row(r, h) >= N) st[u][r] = -INFINITY;
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[u][r]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax * c2);
+    const float alpha = fexp2(m - mn);   // 0 on the first tile (m = -inf)
+    const bool first = m == -INFINITY;
+    m = mn;
+    float rs = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fexp2(fmaf(st[u][r], c2, -mn));
+        st[u][r] = p;
+        rs += p;
+      }
+    l = fmaf(l, alpha, rs);
+    // rescale O only when some lane's running max moved (rare after the first tiles)
+    if (!first && __builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8(st[u], s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          oacc[dt] = mfma32(frag_tr(vt, k0 + 32 * u + 16 * s, 32 * dt, lane), pb, oacc[dt]);
+      }
+  };
+  int k0 = 0;
+  for (; k0 + 64 <= NP; k0 += 64) tile(std::integral_constant<int, 2>{}, k0);
+  if (k0 < NP) tile(std::integral_constant<int, 1>{}, k0);
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (q < N) {
+    const float inv = 1.f / lt;
+    bf16* orow = o + ((int64_t)b * N + q) * D + hd * DH;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * h;
+        store4(orow + d, oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv, oacc[dt][4 * g4 + 2] * inv,
+               oacc[dt][4 * g4 + 3] * inv);
+      }
+    if (h == 0) lse[(int64_t)bh * N + q] = (m + log2f(lt)) * LN2;
+  }
+}
+
+// dQ (+ delta = rowsum(dO * O)): grid B*H, block 64*NW, wave w owns queries 32w..+31, K and V
+// of the whole sequence in LDS.  Keys >= N need no mask: their K rows are zero in LDS, so
+// their dS (whatever it is) meets a zero row of K in dQ = dS K.
+template <int NPMAX>
+__global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dq_seq_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
+    float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6, NP = nw * 32;
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  char* kt = smem;
+  char* vt = smem + NP * 128;
+  stage_seq(kt, rk, ldb, NP, nw, wave, lane);
+  stage_seq(vt, rv, ldb, NP, nw, wave, lane);
+
+  const int q = wave * 32 + (lane & 31);
+  const bool qok = q < N;
+  bf16x8 qf[4], df[4];
+  float dl;
+  {
+    bf16x8 of[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t off = (uint32_t)((int64_t)q * ldo + (16 * s + 8 * h) * 2);
+      df[s] = load_row16(rdo, off);
+      of[s] = load_row16(ro, off);
+    }
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)of[s][j] * (float)df[s][j];
+    dl = part + __shfl_xor(part, 32, 64);
+  }
+  if (qok && h == 0) delta[(int64_t)bh * N + q] = dl;
+  asm volatile("" ::: "memory");   // keep the Q loads after the delta reduction (registers)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
+  const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;   // q >= N -> p = 0
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const float c2 = scale * LOG2E;
+  f32x16 dqt[2] = {zero16(), zero16()};
+#pragma unroll 1
+  for (int k0 = 0; k0 < NP; k0 += 32) {
+    f32x16 st = zero16(), dp = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      st = mfma32(frag_row(kt, k0, s, lane), qf[s], st);   // S^T[key][q]
+      dp = mfma32(frag_row(vt, k0, s, lane), df[s], dp);   // dP^T[key][q]
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = fexp2(fmaf(st[r], c2, -L2));
+      dp[r] = p * (dp[r] - dl);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 sb = pack8(dp, s);
+#pragma unroll
+      for (int d2 = 0; d2 < 2; ++d2) dqt[d2] = mfma32(frag_tr(kt, k0 + 16 * s, 32 * d2, lane), sb, dqt[d2]);
+    }
+  }
+  if (!qok) return;
+  bf16* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
+#pragma unroll
+  for (int d2 = 0; d2 < 2; ++d2)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * d2 + 8 * g4 + 4 * h;
+      store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale, dqt[d2][4 * g4 + 2] * scale,
+             dqt[d2][4 * g4 + 3] * scale);
+    }
+}
+
+// dK/dV: grid B*H, block 64*NW, wave w owns keys 32w..+31; Q, dO, lse*log2e and delta of the
+// whole sequence in LDS.  Queries >= N get L2 = +inf -> P = 0, dS = 0.
+template <int NPMAX>
+__global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
+  // one LDS object: [Q | dO] images, then L2[NPMAX], delta[NPMAX]
+  __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128 + 2 * NPMAX * 4];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6, NP = nw * 32;
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  char* qt = smem;
+  char* dt_ = smem + NP * 128;
+  float* l2s = (float*)(smem + 2 * NPMAX * 128);
+  float* dls = l2s + NPMAX;
+  stage_seq(qt, rq, ldb, NP, nw, wave, lane);
+  stage_seq(dt_, rdo, ldo, NP, nw, wave, lane);
+  for (int i = threadIdx.x; i < NP; i += blockDim.x) {
+    const bool ok = i < N;
+    l2s[i] = ok ? lse[(int64_t)bh * N + i] * LOG2E : INFINITY;
+    dls[i] = ok ? delta[(int64_t)bh * N + i] : 0.f;
+  }
+  const int key = wave * 32 + (lane & 31);
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = load_row16(rk, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
+    vf[s] = load_row16(rv, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const float c2 = scale * LOG2E;
+  f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+#pragma unroll 1
+  for (int q0 = 0; q0 < NP; q0 += 32) {
+    f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
+      dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key]
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int q4 = q0 + 8 * g4 + 4 * h;   // rows acc_row(4*g4 + i, h) = q4 + i
+      const f32x4 L2 = *(const f32x4*)(l2s + q4);
+      const f32x4 dl = *(const f32x4*)(dls + q4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = fexp2(fmaf(sa[4 * g4 + i], c2, -L2[i]));
+        sa[4 * g4 + i] = p;
+        dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
+#pragma unroll
+      for (int d2 = 0; d2 < 2; ++d2) {
+        dvt[d2] = mfma32(frag_tr(dt_, q0 + 16 * s, 32 * d2, lane), pb, dvt[d2]);
+        dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
+      }
+    }
+  }
+  if (key >= N) return;
+  bf16* row = dqkv + ((int64_t)b * N + key) * ld;
+#pragma unroll
+  for (int d2 = 0; d2 < 2; ++d2)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 32 * d2 + 8 * g4 + 4 * h;
+      store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
+             dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
+      store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
+             dvt[d2][4 * g4 + 3]);
     }
 }
 
@@ -620,6 +931,14 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_f32(const float* __restrict__
 
 using namespace vitmi;
 
+// whole-sequence kernels for N <= SEQ_MAX (8 waves, 2 workgroups of <= 64 KiB LDS per CU);
+// VITMI_ATTN_STREAM=1 forces the streamed kernels (A/B timing, tests)
+static constexpr int SEQ_MAX = 256;
+static bool seq_path(int N) {
+  const char* e = getenv("VITMI_ATTN_STREAM");
+  return N <= SEQ_MAX && !(e && atoi(e));
+}
+
 static int attn_check(int dtype, int B, int N, int H, int dh) {
   VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "attention: bad dtype %d", dtype);
   VITMI_CHECK_ARG(dh == DH, "attention: head dim must be 64 (got %d)", dh);
@@ -634,7 +953,11 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
   if (int rc = attn_check(dtype, B, N, H, dh)) return rc;
   VITMI_CHECK_ARG(qkv && o && lse, "attention_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VITMI_BF16) {
+  if (dtype == VITMI_BF16 && seq_path(N)) {
+    const dim3 block(64 * ((N + 31) / 32));
+    hipLaunchKernelGGL(attn_fwd_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv, (bf16*)o, lse, N, H,
+                       scale);
+  } else if (dtype == VITMI_BF16) {
     dim3 grid((N + 127) / 128, B * H);
     hipLaunchKernelGGL(attn_fwd_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (bf16*)o, lse, N, H, scale);
   } else {
@@ -661,7 +984,14 @@ extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float
   float* delta = (float*)workspace;
   const int64_t rows = (int64_t)B * N * H;
   const int blocks = (int)((rows + 255) / 256);
-  if (dtype == VITMI_BF16) {
+  if (dtype == VITMI_BF16 && seq_path(N)) {
+    // dQ first: it also writes delta, which the dK/dV kernel consumes
+    const dim3 block(64 * ((N + 31) / 32));
+    hipLaunchKernelGGL(attn_bwd_dq_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv, (const bf16*)o,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dkv_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
+  } else if (dtype == VITMI_BF16) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
     dim3 grid((N + 127) / 128, B * H);
     hipLaunchKernelGGL(attn_bwd_dq_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)o,

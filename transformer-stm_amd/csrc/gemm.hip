@@ -177,13 +177,13 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc + biasv);
   } else if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
     const float u = acc + biasv;
-    ((T*)g.aux)[row * g.ldaux + col] = from_f32<T>(u);
+    ((T*)g.aux)[row * g.ldaux + col] = from_f32<T>(gelu_grad_f(u));
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(gelu_f(u));
   } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
     ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + acc + biasv;
   } else if constexpr (EPI == VITMI_EPI_DGELU) {
-    const float u = to_f32(((const T*)g.aux)[row * g.ldaux + col]);
-    ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc * gelu_grad_f(u));
+    const float gp = to_f32(((const T*)g.aux)[row * g.ldaux + col]);
+    ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc * gp);
   } else if constexpr (EPI == VITMI_EPI_ACCUM) {
     ((float*)g.C)[row * g.ldc + col] += acc;
   }
@@ -368,7 +368,9 @@ __device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf)
 template <bool AK, bool BKM, int EPI, typename TC>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   using namespace g256;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // two DMA stages + the bias of the current and the next tile (fp32, double-buffered)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048];
+  constexpr bool HAS_BIAS = EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -546,7 +548,25 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   }
 
   const int lc4 = 4 * (lane >> 4), lr = lane & 15;
+  const __amdgpu_buffer_rsrc_t rbias = make_rsrc(g.bias, g.bias ? clamp_bytes(g.N * 4) : 0u);
+  int tpar = 0;   // bias buffer of the current tile
   for (;;) {
+    if constexpr (HAS_BIAS) {
+      // bias[n0 + 32*wave .. +32) -> LDS by scalar buffer loads (lgkmcnt, so the vmcnt
+      // accounting of the DMA and of the stores is untouched; the range check zero-fills
+      // columns >= N and a null bias).  Read by the epilogue after many barriers.
+      typedef int i32x16 __attribute__((ext_vector_type(16)));
+      i32x16 s0, s1;
+      const int boff = __builtin_amdgcn_readfirstlane((int)((n0 + 32 * wave) * 4));
+      asm volatile("s_buffer_load_dwordx16 %0, %2, %3\n\ts_buffer_load_dwordx16 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+                   : "=s"(s0), "=s"(s1) : "s"(rbias), "s"(boff), "s"(boff + 64) : "memory");
+      int bvv = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(bvv) : "s"(s0[i]), "i"(i));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(bvv) : "s"(s1[i]), "i"(16 + i));
+      if (lane < 32) *(int*)(smem + 2 * STAGE + tpar * 1024 + (32 * wave + lane) * 4) = bvv;
+    }
     const int next = tile + nbx;
     const bool has_next = next < t_end;
     const int64_t m0n = has_next ? (int64_t)(next / g.tiles_n) * BM : 0;
@@ -611,8 +631,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         const int64_t col = n0 + wn * 64 + ni * 16 + lc4;
         if (col >= g.N) continue;
         f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL)
-          if (g.bias) bv = *(const f32x4*)(g.bias + col);
+        if constexpr (HAS_BIAS)
+          bv = *(const f32x4*)(smem + 2 * STAGE + tpar * 1024 + (wn * 64 + ni * 16 + lc4) * 4);
         // batch the epilogue's global loads for this column group (one wait for all 8)
         f32x4 ld4[8];
         bf16x4 ldu[8];
@@ -635,9 +655,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             bf16x4 u;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              u[e] = (bf16)v[e];
               float cdf, pdf;
               gelu_fast_parts(v[e], cdf, pdf);
+              u[e] = (bf16)(cdf + v[e] * pdf);   // gelu'(x) = Phi(x) + x phi(x), kept for DGELU
               v[e] = v[e] * cdf;
             }
             const uint32_t uoff = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldaux + wn * 64 + lc4) * 2);
@@ -647,12 +667,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
                             "s"(usoff), "i"(ni * 32) : "memory");
           } else if constexpr (EPI == VITMI_EPI_DGELU) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float uf = (float)ldu[mi][e];
-              float cdf, pdf;
-              gelu_fast_parts(uf, cdf, pdf);
-              v[e] *= cdf + uf * pdf;
-            }
+            for (int e = 0; e < 4; ++e) v[e] *= (float)ldu[mi][e];   // aux = gelu'(u) from the forward
           }
           if constexpr (CES == 4) {
             asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
@@ -668,6 +683,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         }
       }
     }
+    tpar ^= 1;
     if (!has_next) break;
     tile = next; m0 = m0n; n0 = n0n; ra = ran; rb = rbn;
   }

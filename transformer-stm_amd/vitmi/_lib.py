@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvitmi.so")
+# VITMI_LIB: load another build of the same ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("VITMI_LIB") or os.path.join(_HERE, "libvitmi.so")
 
 P = ctypes.c_void_p
 I = ctypes.c_int

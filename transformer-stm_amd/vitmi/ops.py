@@ -72,7 +72,7 @@ def _rows(t: Tensor) -> Tuple[int, int]:
 def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dtype,
                epilogue: int = EPI_STORE, residual: Optional[Tensor] = None):
     """y = x W^T + b (+GELU, +residual).  x [M,K], w [N,K] (same dtype).  Returns y
-    (and the pre-activation for EPI_BIAS_GELU)."""
+    (and gelu'(pre-activation), the saved GELU derivative, for EPI_BIAS_GELU)."""
     assert x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N = w.shape[0]
@@ -97,7 +97,7 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
 
 def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = EPI_STORE,
                  aux: Optional[Tensor] = None) -> Tensor:
-    """dx[M,K] = dy[M,N] W[N,K] (optionally * gelu'(aux))."""
+    """dx[M,K] = dy[M,N] W[N,K] (optionally * aux, the gelu' saved by the forward)."""
     assert dy.is_contiguous() and w.is_contiguous() and dy.dtype == w.dtype
     M, N = dy.numel() // dy.shape[-1], dy.shape[-1]
     K = w.shape[1]
