@@ -74,13 +74,19 @@ size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajor, int64_t 
 
 /* Linear layer y = x W^T + b  (keras layers.Dense, models/CvT(Par).py:132-134,142,254,256;
  * torch nn.Linear in old_codes/MS_CvT.py:63-65,116-121).  x [M,K], W [N,K] -> y [M,N]. */
+/* workspace: optional (NULL/0 allowed).  With vitmi_linear_*_workspace_size() bytes the
+ * persistent bf16 GEMM splits the tiles of an under-filled last round over K (fp32 partials
+ * in the workspace, finished by a fix-up kernel): same results up to fp32 summation order. */
 int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, const void* x, const void* w,
                      const float* bias, void* y, int y_dtype, int epilogue, void* aux,
-                     const float* residual, vitmi_stream_t stream);
+                     const float* residual, void* workspace, size_t ws_bytes,
+                     vitmi_stream_t stream);
+size_t vitmi_linear_fwd_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
 /* dx[M,K] = dy[M,N] W[N,K]   (epilogue STORE or DGELU with aux = gelu'(u) [M,K]) */
 int vitmi_linear_dgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* w,
-                       void* dx, int dx_dtype, int epilogue, const void* aux,
-                       vitmi_stream_t stream);
+                       void* dx, int dx_dtype, int epilogue, const void* aux, void* workspace,
+                       size_t ws_bytes, vitmi_stream_t stream);
+size_t vitmi_linear_dgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
 /* dW[N,K] (f32) += dy[M,N]^T x[M,K]; uses split-K over M with fp32 partial slabs */
 int vitmi_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* x,
                        float* dw, void* workspace, size_t ws_bytes, vitmi_stream_t stream);

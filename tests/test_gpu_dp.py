@@ -60,7 +60,9 @@ def _worker(rank, world, port, q):
         early = sum(1 for r, _ in red.launch_log if r < model.arena().numel)
         red.finish()
         torch.cuda.synchronize()
-        grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()}
+        # numpy arrays pickle by value (torch tensors would travel as fds that vanish with
+        # this process)
+        grads = {k: p.grad.detach().cpu().numpy() for k, p in model.named_parameters()}
         q.put((rank, dict(grads=grads, early=early, nb=len(red.bounds))))
     finally:
         dist.destroy_process_group()
@@ -88,6 +90,6 @@ def test_dp_two_ranks_match_full_batch_oracle():
         assert o["nb"] > 2
         assert o["early"] >= 1, "no bucket was launched during the backward (no overlap)"
         for k, ref in g_ref.items():
-            assert vit_ref.rel_err(o["grads"][k], ref) <= 1e-4, (r, k)
+            assert vit_ref.rel_err(torch.from_numpy(o["grads"][k]), ref) <= 1e-4, (r, k)
     for k in g_ref:
-        assert torch.equal(res[0]["grads"][k], res[1]["grads"][k]), k
+        assert (res[0]["grads"][k] == res[1]["grads"][k]).all(), k

@@ -81,6 +81,52 @@ def test_linear_dgrad(M, N, K, T, policy):
     assert rel(dg.float(), gl) < (8e-3 if T == BF else 1e-5)
 
 
+@pytest.mark.parametrize("M,N,K", [(256 * 9, 256, 768), (256 * 8 + 100, 256 + 64, 512), (256 * 17, 256, 256)])
+def test_gemm_tail_split(M, N, K):
+    """Persistent gemm256 on an 8-block grid (policy 3): the tiles of an under-filled last
+    round are split over K into fp32 partials + fix-up kernel.  Every epilogue goes through
+    the fix-up path; the workspace query must size it."""
+    from vitmi._lib import lib
+    lib().vitmi_gemm_set_policy(3)
+    try:
+        assert lib().vitmi_linear_fwd_workspace_size(1, M, N, K) > 0
+        x, w, b = rnd(M, K, dtype=BF, seed=41), rnd(N, K, dtype=BF, seed=42, scale=0.05), rnd(N, seed=43)
+        u_ref = x.float() @ w.float().t() + b
+        y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), BF)
+        assert rel(y.float(), u_ref) < 8e-3
+        a, gp = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), BF, ops.EPI_BIAS_GELU)
+        assert rel(a.float(), F.gelu(u_ref)) < 8e-3
+        assert rel(gp.float(), gelu_grad(u_ref)) < 8e-3
+        r = rnd(M, N, seed=44)
+        y2 = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), torch.float32, ops.EPI_RESIDUAL, residual=r.to(DEV))
+        assert rel(y2, u_ref + r) < 1e-5
+        # dgrad: dx[M,K'] = dy[M,N'] W[N',K'] with the output [M, N] -> reduction K
+        dy, w2 = rnd(M, K, dtype=BF, seed=45), rnd(K, N, dtype=BF, seed=46, scale=0.05)
+        ref = dy.float() @ w2.float()
+        gpv = gelu_grad(rnd(M, N, seed=47)).to(BF)
+        dx = ops.linear_dgrad(dy.to(DEV), w2.to(DEV), BF, ops.EPI_DGELU, aux=gpv.to(DEV))
+        assert rel(dx.float(), ref * gpv.float()) < 8e-3
+    finally:
+        lib().vitmi_gemm_set_policy(0)
+
+
+def test_gemm_tail_split_vit_shape():
+    """The ViT-B/16 bs=256 N=768 shape on the real grid (591 tiles over the device's CUs),
+    against torch's own GEMM on the GPU (the CPU reference would take minutes)."""
+    M, N, K = 256 * 197, 768, 3072
+    g = torch.Generator(device=DEV).manual_seed(5)
+    h = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(BF)
+    w2 = ((torch.rand(N, K, device=DEV, generator=g) * 2 - 1) * 0.05).to(BF)
+    b2 = torch.rand(N, device=DEV, generator=g)
+    res = torch.rand(M, N, device=DEV, generator=g)
+    y = ops.linear_fwd(h, w2, b2, torch.float32, ops.EPI_RESIDUAL, residual=res)
+    ref = res + h.float() @ w2.float().t() + b2
+    assert ((y - ref).norm() / ref.norm()).item() < 1e-5
+    dx = ops.linear_dgrad(h, w2.t().contiguous(), BF)          # [M,K] x [K,N] -> [M,N]
+    ref2 = h.float() @ w2.float().t()
+    assert ((dx.float() - ref2).norm() / ref2.norm()).item() < 8e-3
+
+
 @pytest.mark.parametrize("M,N,K", [(197 * 2, 384, 192), (4000, 384, 768), (50, 64, 64), (20000, 192, 576)])
 @pytest.mark.parametrize("T", [BF, torch.float32])
 def test_linear_wgrad_accumulates(M, N, K, T, policy):

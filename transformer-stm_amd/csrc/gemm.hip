@@ -37,6 +37,14 @@ struct GemmArgs {
   int64_t k_per_split;   // reduction range of one blockIdx.z (multiple of BK)
   int64_t split_stride;  // elements between split partial slabs (EPI_PARTIAL)
   int tiles_n;           // number of BN tiles along N
+  // gemm256 tail split (stream-K-like): units [0, t_full) are whole tiles; the remaining
+  // tiles are split into nsplit K-ranges of ksplit K-steps each, written as fp32 partials
+  // to tail_ws ([unit - t_full][256][256]) and finished by gemm_tail_fixup_kernel.
+  int t_full;
+  int nsplit;
+  int ksplit;
+  float* tail_ws;
+  size_t tail_ws_bytes;
 };
 
 enum { EPI_PARTIAL = 100 };
@@ -380,27 +388,53 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   const int xcd = blockIdx.x & 7, jx = blockIdx.x >> 3;
   const int gq = G >> 3, gr = G & 7;
   const int nbx = gq + (xcd < gr ? 1 : 0);              // blocks in this group
-  const int q = nwg >> 3, r = nwg & 7;
-  const int t_begin = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int t_end = t_begin + q + (xcd < r ? 1 : 0);
+  // Each XCD group owns a contiguous range of the whole tiles AND an equal share of the
+  // tail-split units (work-balanced; consecutive whole tiles share A panels in the XCD's
+  // L2).  Sequence index i of a block runs jx, jx + nbx, ... over [0, nf + ns).
+  const int ns_all = nwg - g.t_full;
+  const int q1 = g.t_full >> 3, r1 = g.t_full & 7;
+  const int f_b = xcd < r1 ? xcd * (q1 + 1) : r1 * (q1 + 1) + (xcd - r1) * q1;
+  const int nf = q1 + (xcd < r1 ? 1 : 0);
+  const int q2 = ns_all >> 3, r2 = ns_all & 7;
+  const int s_b = xcd < r2 ? xcd * (q2 + 1) : r2 * (q2 + 1) + (xcd - r2) * q2;
+  const int nseq = nf + q2 + (xcd < r2 ? 1 : 0);
+  auto unit_at = [&](int i) { return i < nf ? f_b + i : g.t_full + s_b + (i - nf); };
 
   const int64_t kb = (int64_t)blockIdx.z * g.k_per_split;
   const int64_t ke = min(g.K, kb + g.k_per_split);
   const int nk = (int)((ke - kb + BK - 1) / BK);
   if (nk <= 0) return;
 
-  auto rsrc_a = [&](int64_t m0) {
-    return AK ? make_rsrc((const char*)g.A + m0 * g.lda * 2, clamp_bytes((g.M - m0) * g.lda * 2))
-              : make_rsrc((const char*)g.A + (kb * g.lda + m0) * 2, clamp_bytes(((g.K - kb) * g.lda - m0) * 2));
+  // Operand descriptors with the unit's first k (kb + ks0 K-steps) baked into the base, so
+  // the DMA issue only needs the unit-relative K-step.
+  auto rsrc_a = [&](int64_t m0, int ks0) {
+    const int64_t k = kb + (int64_t)ks0 * BK;
+    return AK ? make_rsrc((const char*)g.A + (m0 * g.lda + k) * 2, clamp_bytes((g.M - m0) * g.lda * 2 - k * 2))
+              : make_rsrc((const char*)g.A + (k * g.lda + m0) * 2, clamp_bytes(((g.K - k) * g.lda - m0) * 2));
   };
-  auto rsrc_b = [&](int64_t n0) {
-    return BKM ? make_rsrc((const char*)g.B + n0 * g.ldb * 2, clamp_bytes((g.N - n0) * g.ldb * 2))
-               : make_rsrc((const char*)g.B + (kb * g.ldb + n0) * 2, clamp_bytes(((g.K - kb) * g.ldb - n0) * 2));
+  auto rsrc_b = [&](int64_t n0, int ks0) {
+    const int64_t k = kb + (int64_t)ks0 * BK;
+    return BKM ? make_rsrc((const char*)g.B + (n0 * g.ldb + k) * 2, clamp_bytes((g.N - n0) * g.ldb * 2 - k * 2))
+               : make_rsrc((const char*)g.B + (k * g.ldb + n0) * 2, clamp_bytes(((g.K - k) * g.ldb - n0) * 2));
+  };
+  // unit u -> tile origin, first K-step and K-step count
+  auto unit_of = [&](int u, int64_t& m0_, int64_t& n0_, int& ks0_, int& nk_) {
+    int tl = u;
+    ks0_ = 0;
+    nk_ = nk;
+    if (u >= g.t_full) {
+      const int v = u - g.t_full;
+      tl = g.t_full + v / g.nsplit;
+      ks0_ = (v % g.nsplit) * g.ksplit;
+      nk_ = min(g.ksplit, nk - ks0_);
+    }
+    m0_ = (int64_t)(tl / g.tiles_n) * BM;
+    n0_ = (int64_t)(tl % g.tiles_n) * BN;
   };
   auto sub = [&](int buf, int which) -> char* { return smem + buf * STAGE + which * HALF; };
   // issue half `which` (0=A0 1=B0 2=A1 3=B1) of K-step t into buffer buf
   auto issue = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int t, int buf, int which) {
-    const int64_t k0 = kb + (int64_t)t * BK;
+    const int64_t k0 = (int64_t)t * BK;   // relative to the descriptor's k
     const int krow0 = t * BK;
     if (which == 0) stage_half<true, AK>(sub(buf, 0), ra, g.lda, k0, krow0, 0, wave, lane);
     if (which == 1) stage_half<false, BKM>(sub(buf, 2), rb, g.ldb, k0, krow0, 0, wave, lane);
@@ -497,7 +531,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     } else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
     barrier();                                                                                  \
     if (has2) { issue(s2a, s2b, s2t, buf, 3); issue(s2a, s2b, s2t, buf, 2); }                   \
-    if (has1) { RD_A(ax, buf ^ 1, 0); RD_B(BQ, buf ^ 1, 0); }                                   \
+    if (rd1) { RD_A(ax, buf ^ 1, 0); RD_B(BQ, buf ^ 1, 0); }                                    \
     MMA4(1, 0, ay, BP);                                                                         \
   } while (0)
 
@@ -520,17 +554,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       issue(s1a, s1b, s1t, buf ^ 1, 3);                                                         \
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                          \
       barrier();                                                                                \
-      RD_A(ax, buf ^ 1, 0);                                                                     \
-      RD_B(BQ, buf ^ 1, 0);                                                                     \
+      if (rd1) { RD_A(ax, buf ^ 1, 0); RD_B(BQ, buf ^ 1, 0); }                                  \
     }                                                                                           \
     MMA4(1, 0, ay, BP);                                                                         \
   } while (0)
   constexpr bool DEEP = AK && BKM;
 
-  int tile = t_begin + jx;
-  if (tile >= t_end) return;
-  int64_t m0 = (int64_t)(tile / g.tiles_n) * BM, n0 = (int64_t)(tile % g.tiles_n) * BN;
-  __amdgpu_buffer_rsrc_t ra = rsrc_a(m0), rb = rsrc_b(n0);
+  int it = jx;
+  if (it >= nseq) return;
+  int tile = unit_at(it);   // work unit (a whole tile, or a K-range of a tail tile)
+  int64_t m0, n0;
+  int ks0, nku;
+  unit_of(tile, m0, n0, ks0, nku);
+  __amdgpu_buffer_rsrc_t ra = rsrc_a(m0, ks0), rb = rsrc_b(n0, ks0);
   int buf = 0;
   {
     // prologue: steps 0 and 1 of the first tile (nk >= 2 is a launch precondition)
@@ -567,11 +603,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       for (int i = 0; i < 16; ++i) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(bvv) : "s"(s1[i]), "i"(16 + i));
       if (lane < 32) *(int*)(smem + 2 * STAGE + tpar * 1024 + (32 * wave + lane) * 4) = bvv;
     }
-    const int next = tile + nbx;
-    const bool has_next = next < t_end;
-    const int64_t m0n = has_next ? (int64_t)(next / g.tiles_n) * BM : 0;
-    const int64_t n0n = has_next ? (int64_t)(next % g.tiles_n) * BN : 0;
-    const __amdgpu_buffer_rsrc_t ran = rsrc_a(m0n), rbn = rsrc_b(n0n);
+    const int itn = it + nbx;
+    const bool has_next = itn < nseq;
+    const int next = has_next ? unit_at(itn) : 0;
+    int64_t m0n = 0, n0n = 0;
+    int ks0n = 0, nkn = 0;
+    if (has_next) unit_of(next, m0n, n0n, ks0n, nkn);
+    const __amdgpu_buffer_rsrc_t ran = rsrc_a(m0n, ks0n), rbn = rsrc_b(n0n, ks0n);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -579,39 +617,43 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 
     // K-loop unrolled by 2 so the B register sets alternate statically
 #define STEP_SETUP(T)                                                                           \
-    const bool has1 = ((T) + 1 < nk) || has_next;                                               \
-    const bool has2 = ((T) + 2 < nk) || has_next;                                               \
-    const __amdgpu_buffer_rsrc_t s2a = ((T) + 2 < nk) ? ra : ran;                               \
-    const __amdgpu_buffer_rsrc_t s2b = ((T) + 2 < nk) ? rb : rbn;                               \
-    const int s2t = ((T) + 2 < nk) ? (T) + 2 : (T) + 2 - nk;                                    \
-    const __amdgpu_buffer_rsrc_t s1a = ((T) + 1 < nk) ? ra : ran;                               \
-    const __amdgpu_buffer_rsrc_t s1b = ((T) + 1 < nk) ? rb : rbn;                               \
-    const int s1t = ((T) + 1 < nk) ? (T) + 1 : 0;
-    for (int t = 0; t < nk; t += 2) {
+    const bool has1 = ((T) + 1 < nku) || has_next;                                              \
+    const bool has2 = ((T) + 2 < nku) || has_next;                                              \
+    const __amdgpu_buffer_rsrc_t s2a = ((T) + 2 < nku) ? ra : ran;                              \
+    const __amdgpu_buffer_rsrc_t s2b = ((T) + 2 < nku) ? rb : rbn;                              \
+    const int s2t = ((T) + 2 < nku) ? (T) + 2 : (T) + 2 - nku;                                  \
+    const __amdgpu_buffer_rsrc_t s1a = ((T) + 1 < nku) ? ra : ran;                              \
+    const __amdgpu_buffer_rsrc_t s1b = ((T) + 1 < nku) ? rb : rbn;                              \
+    const int s1t = ((T) + 1 < nku) ? (T) + 1 : 0;                                              \
+    const bool rd1 = (T) + 1 < nku;  /* next tile's step-0 fragments: read after the epilogue */
+    for (int t = 0; t < nku; t += 2) {
       {
         STEP_SETUP(t)
         if constexpr (DEEP) KSTEP(b0, b1); else KSTEP1(b0, b1);
         buf ^= 1;
       }
-      if (t + 1 < nk) {
+      if (t + 1 < nku) {
         STEP_SETUP(t + 1)
         if constexpr (DEEP) KSTEP(b1, b0); else KSTEP1(b1, b0);
         buf ^= 1;
-      } else {
-        // odd step count: the next tile's B0 was preloaded into b1
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) b0[nt][ks] = b1[nt][ks];
       }
     }
 #undef STEP_SETUP
 #undef KSTEP
 #undef KSTEP1
 #undef MMA4
-#undef RD_A
-#undef RD_B
 
+    if (tile >= g.t_full) {
+      // K-range of a tail tile: raw fp32 partial into its [256][256] slab
+      const __amdgpu_buffer_rsrc_t rw = make_rsrc(g.tail_ws + (int64_t)(tile - g.t_full) * BM * BN, BM * BN * 4);
+      const uint32_t wbase = (uint32_t)(((wm * 128 + lr) * BN + wn * 64 + lc4) * 4);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                       :: "v"(acc[mi][ni]), "v"(wbase), "s"(rw), "s"(mi * 16 * BN * 4), "i"(ni * 64) : "memory");
+    } else
     // ---- epilogue straight from registers: acc[mi][ni] = C^T tile; lane owns row
     // m0 + wm*128 + mi*16 + lr, columns n0 + wn*64 + ni*16 + lc4 .. +3.
     // Stores are inline-asm buffer stores: hipcc would otherwise put `s_waitcnt vmcnt(0)`
@@ -626,67 +668,98 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, clamp_bytes(((g.M - m0) * g.ldc - n0) * CES));
       const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
       const uint32_t vbase = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldc + wn * 64 + lc4) * CES);
+      // Branch-free ragged N (straight-line epilogue code schedules far better): lanes past
+      // N load from a clamped column and store to a voffset beyond the buffer range, so the
+      // store is dropped (N % 8 == 0 is a gemm256 precondition).
+      bool cok[4];
+      uint32_t vb[4];
+      int64_t colc[4];
+      f32x4 bv[4];
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const int64_t col = n0 + wn * 64 + ni * 16 + lc4;
-        if (col >= g.N) continue;
-        f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+        cok[ni] = col < g.N;
+        colc[ni] = cok[ni] ? col : g.N - 4;
+        vb[ni] = cok[ni] ? vbase : 0x80000000u;
+        bv[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (HAS_BIAS)
-          bv = *(const f32x4*)(smem + 2 * STAGE + tpar * 1024 + (wn * 64 + ni * 16 + lc4) * 4);
-        // batch the epilogue's global loads for this column group (one wait for all 8)
-        f32x4 ld4[8];
-        bf16x4 ldu[8];
+          bv[ni] = *(const f32x4*)(smem + 2 * STAGE + tpar * 1024 + (wn * 64 + ni * 16 + lc4) * 4);
+      }
+      [[maybe_unused]] __amdgpu_buffer_rsrc_t ru = rc;
+      if constexpr (EPI == VITMI_EPI_BIAS_GELU)
+        ru = make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
+      // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand
+      auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) {
+        f32x4 v = acc[mi][ni] + bv[ni];
+        const int soff = mi * rstride;
+        if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM) v += ldv;
+        if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
+          bf16x4 u;
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          const int64_t row = min(m0 + wm * 128 + mi * 16 + lr, g.M - 1);
-          if constexpr (EPI == VITMI_EPI_RESIDUAL) ld4[mi] = *(const f32x4*)(g.residual + row * g.ldr + col);
-          if constexpr (EPI == VITMI_EPI_ACCUM) ld4[mi] = *(const f32x4*)((const float*)g.C + row * g.ldc + col);
-          if constexpr (EPI == VITMI_EPI_DGELU) ldu[mi] = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + col);
-        }
-        __amdgpu_buffer_rsrc_t ru = rc;
-        if constexpr (EPI == VITMI_EPI_BIAS_GELU)
-          ru = make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          f32x4 v = acc[mi][ni] + bv;
-          const int soff = mi * rstride;
-          if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM) v += ld4[mi];
-          if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
-            bf16x4 u;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float cdf, pdf;
-              gelu_fast_parts(v[e], cdf, pdf);
-              u[e] = (bf16)(cdf + v[e] * pdf);   // gelu'(x) = Phi(x) + x phi(x), kept for DGELU
-              v[e] = v[e] * cdf;
-            }
-            const uint32_t uoff = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldaux + wn * 64 + lc4) * 2);
-            const int usoff = (int)(mi * 16 * g.ldaux * 2);
-            asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
-                         :: "v"(__builtin_bit_cast(unsigned long long, u)), "v"(uoff), "s"(ru),
-                            "s"(usoff), "i"(ni * 32) : "memory");
-          } else if constexpr (EPI == VITMI_EPI_DGELU) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] *= (float)ldu[mi][e];   // aux = gelu'(u) from the forward
+          for (int e = 0; e < 4; ++e) {
+            float cdf, pdf;
+            gelu_fast_parts(v[e], cdf, pdf);
+            u[e] = (bf16)(cdf + v[e] * pdf);   // gelu'(x) = Phi(x) + x phi(x), kept for DGELU
+            v[e] = v[e] * cdf;
           }
-          if constexpr (CES == 4) {
-            asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
-                         :: "v"(v), "v"(vbase), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
-          } else {
-            bf16x4 o;
+          const uint32_t uoff = cok[ni] ? (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldaux + wn * 64 + lc4) * 2)
+                                        : 0x80000000u;
+          const int usoff = (int)(mi * 16 * g.ldaux * 2);
+          asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                       :: "v"(__builtin_bit_cast(unsigned long long, u)), "v"(uoff), "s"(ru),
+                          "s"(usoff), "i"(ni * 32) : "memory");
+        } else if constexpr (EPI == VITMI_EPI_DGELU) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-            asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
-                         :: "v"(__builtin_bit_cast(unsigned long long, o)), "v"(vbase), "s"(rc),
-                            "s"(soff), "i"(ni * 32) : "memory");
-          }
+          for (int e = 0; e < 4; ++e) v[e] *= (float)ldb[e];   // aux = gelu'(u) from the forward
         }
+        if constexpr (CES == 4) {
+          asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                       :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
+        } else {
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+          asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                       :: "v"(__builtin_bit_cast(unsigned long long, o)), "v"(vb[ni]), "s"(rc),
+                          "s"(soff), "i"(ni * 32) : "memory");
+        }
+      };
+      if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM || EPI == VITMI_EPI_DGELU) {
+        // epilogues that load: per column group, batch its 8 loads (one wait for all)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          f32x4 ld4[8];
+          bf16x4 ldu[8];
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) {
+            const int64_t row = min(m0 + wm * 128 + mi * 16 + lr, g.M - 1);
+            if constexpr (EPI == VITMI_EPI_RESIDUAL) ld4[mi] = *(const f32x4*)(g.residual + row * g.ldr + colc[ni]);
+            if constexpr (EPI == VITMI_EPI_ACCUM) ld4[mi] = *(const f32x4*)((const float*)g.C + row * g.ldc + colc[ni]);
+            if constexpr (EPI == VITMI_EPI_DGELU) ldu[mi] = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + colc[ni]);
+          }
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) emit(mi, ni, ld4[mi], ldu[mi]);
+        }
+      } else {
+        // store-only epilogues go row by row: the 4 column groups of a row (one 128-B line
+        // for bf16) leave back to back, so the L2 sees whole lines
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) emit(mi, ni, f32x4{0.f, 0.f, 0.f, 0.f}, bf16x4{});
       }
     }
     tpar ^= 1;
     if (!has_next) break;
-    tile = next; m0 = m0n; n0 = n0n; ra = ran; rb = rbn;
+    it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; ra = ran; rb = rbn;
+    // step-0 fragments of the next tile (its DMA landed before the last p3 barrier; nobody
+    // refills those halves before the next p0 barrier).  Read here rather than in the last
+    // K-step so the epilogue has the fragment registers to itself.
+    RD_A(ax, buf, 0);
+    RD_B(b0, buf, 0);
   }
+#undef RD_A
+#undef RD_B
 #undef G256_MMA
 }
 
@@ -706,6 +779,32 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
         for (int z = 0; z < splits; ++z) s += ws[z * stride + e];
         dst[e] = s;
       }
+    }
+  }
+}
+
+// Finish the tail tiles of a split gemm256 launch: sum the nsplit fp32 partials of each
+// element and apply the epilogue (the elementwise epi_store of the 128x128 kernel).
+template <typename T, typename TC, int EPI>
+__global__ __launch_bounds__(256) void gemm_tail_fixup_kernel(GemmArgs g, int ntail) {
+  const int64_t groups = (int64_t)ntail * (256 * 256 / 4);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < groups; i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i / (256 * 64));
+    const int e = (int)(i % (256 * 64)) * 4;
+    const int rl = e >> 8, cl = e & 255;
+    const int tile = g.t_full + t;
+    const int64_t row = (int64_t)(tile / g.tiles_n) * 256 + rl;
+    const int64_t col = (int64_t)(tile % g.tiles_n) * 256 + cl;
+    if (row >= g.M || col >= g.N) continue;
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < g.nsplit; ++z)
+      a += *(const f32x4*)(g.tail_ws + ((int64_t)(t * g.nsplit + z) * 256 + rl) * 256 + cl);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (col + j >= g.N) break;
+      const float bv = (g.bias && (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL))
+                           ? g.bias[col + j] : 0.f;
+      epi_store<T, TC, EPI>(g, row, col + j, a[j], bv);
     }
   }
 }
@@ -737,20 +836,70 @@ static bool use256(int dtype, int64_t M, int64_t N) {
   return tiles >= 16;
 }
 
+// persistent grid of the gemm256 launch for nwg tiles and `splits` K-slabs
+static int grid256(int nwg, int splits) {
+  int gx = g_cus / splits;
+  if (gx < 8 || g_policy == 3) gx = 8;   // policy 3: force many tiles per block (tests)
+  if (g_grid_override < 0) gx = nwg;
+  else if (g_grid_override > 0) gx = g_grid_override;
+  return gx > nwg ? nwg : gx;
+}
+
+// Tail split: when the last round of a persistent launch would leave more than half of the
+// blocks idle (ViT N=768 GEMMs: 591 tiles on 256 CUs), its tiles are split into S K-ranges
+// (S <= 4, >= 2 K-steps each) so that round takes ~1/S of the time.
+static bool tail_plan(int nwg, int gx, int nk, int& S, int& ks, int& ntail) {
+  ntail = nwg % gx;
+  if (nwg < gx || ntail == 0 || 2 * ntail > gx || nk < 4) return false;
+  S = gx / ntail;
+  if (S > 4) S = 4;
+  if (S < 2) return false;
+  ks = (nk + S - 1) / S;
+  if (ks < 2) ks = 2;
+  S = (nk + ks - 1) / ks;
+  while (S > 1 && nk - (S - 1) * ks < 2) { ++ks; S = (nk + ks - 1) / ks; }
+  return S > 1;
+}
+
+static size_t tail_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  init_cus();
+  const int nwg = (int)(((M + 255) / 256) * ((N + 255) / 256));
+  int S, ks, ntail;
+  if (nwg <= 0 || !tail_plan(nwg, grid256(nwg, 1), (int)((K + 63) / 64), S, ks, ntail)) return 0;
+  // (sized for any epilogue; launch_t may still decide not to split, see tail_ok)
+  return (size_t)ntail * S * 256 * 256 * sizeof(float);
+}
+
 template <typename T, bool AK, bool BKM, int EPI, typename TC>
 static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (big) {
       g.tiles_n = (int)((g.N + 255) / 256);
       const int nwg = (int)((g.M + 255) / 256) * g.tiles_n;
-      // persistent: about one block per CU over all splits
-      int gx = g_cus / splits;
-      if (gx < 8 || g_policy == 3) gx = 8;   // policy 3: force many tiles per block (tests)
-      if (g_grid_override < 0) gx = nwg;
-      else if (g_grid_override > 0) gx = g_grid_override;
-      if (gx > nwg) gx = nwg;
-      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, nwg);
+      const int gx = grid256(nwg, splits);
+      int units = nwg, S = 1, ks = 0, ntail = 0;
+      g.t_full = nwg;
+      g.nsplit = 1;
+      g.ksplit = 0;
+      const char* tenv = getenv("VITMI_GEMM_TAIL");   // 0: no tail split (A/B timing)
+      // measured: pays off for long reductions (>= 16 K-steps) and for the DGELU epilogue
+      // (whose partial units skip its aux loads); a wash or a loss for K = 768 otherwise
+      const bool tail_ok = g.k_per_split / 64 >= 16 || EPI == VITMI_EPI_DGELU;
+      if (splits == 1 && tail_ok && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM && g.tail_ws && !(tenv && atoi(tenv) == 0) &&
+          tail_plan(nwg, gx, (int)(g.k_per_split / 64), S, ks, ntail) &&
+          g.tail_ws_bytes >= (size_t)ntail * S * 256 * 256 * sizeof(float)) {
+        g.t_full = nwg - ntail;
+        g.nsplit = S;
+        g.ksplit = ks;
+        units = g.t_full + ntail * S;
+      }
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
+      if (units != nwg) {
+        const int blocks = (ntail * 256 * 64 + 255) / 256;
+        hipLaunchKernelGGL((gemm_tail_fixup_kernel<T, TC, EPI>), dim3(blocks), dim3(256), 0, s, g, ntail);
+        VITMI_LAUNCH_CHECK("gemm_tail_fixup_kernel");
+      }
       return VITMI_OK;
     }
   }
@@ -878,6 +1027,8 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   const bool big_ok = big2;
   if (splits == 1) {
     g.k_per_split = (K > 0 ? ktiles : 1) * BK;
+    g.tail_ws = (float*)ws;   // tail split of the persistent gemm256 launch (if it fits)
+    g.tail_ws_bytes = ws ? ws_bytes : 0;
     if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
     return dispatch<float>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
   }
@@ -920,29 +1071,39 @@ extern "C" int vitmi_gemm(int dtype, int a_kmajor, int b_kmajor, int64_t M, int6
 extern "C" size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajor, int64_t M,
                                             int64_t N, int64_t K, int epilogue) {
   (void)a_kmajor; (void)b_kmajor;
-  if (epilogue != VITMI_EPI_ACCUM) return 0;
+  if (epilogue != VITMI_EPI_ACCUM) return use256(dtype, M, N) ? tail_ws_bytes(M, N, K) : 0;
   const int splits = choose_splits(dtype, M, N, K);
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
+extern "C" size_t vitmi_linear_fwd_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
+  return use256(dtype, M, N) ? tail_ws_bytes(M, N, K) : 0;
+}
+
 extern "C" int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, const void* x,
                                 const void* w, const float* bias, void* y, int y_dtype,
-                                int epilogue, void* aux, const float* residual,
-                                vitmi_stream_t stream) {
+                                int epilogue, void* aux, const float* residual, void* workspace,
+                                size_t ws_bytes, vitmi_stream_t stream) {
   VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_BIAS_GELU ||
                       epilogue == VITMI_EPI_RESIDUAL, "linear_fwd: bad epilogue %d", epilogue);
   return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, N, y_dtype, epilogue, bias, aux, N,
-                   residual, N, nullptr, 0, (hipStream_t)stream, false);
+                   residual, N, workspace, ws_bytes, (hipStream_t)stream, false);
+}
+
+extern "C" size_t vitmi_linear_dgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
+  // GEMM rows M, cols K, reduction N
+  return use256(dtype, M, K) ? tail_ws_bytes(M, K, N) : 0;
 }
 
 extern "C" int vitmi_linear_dgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy,
                                   const void* w, void* dx, int dx_dtype, int epilogue,
-                                  const void* aux, vitmi_stream_t stream) {
+                                  const void* aux, void* workspace, size_t ws_bytes,
+                                  vitmi_stream_t stream) {
   VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_DGELU,
                   "linear_dgrad: bad epilogue %d", epilogue);
   // dx[M,K] = dy[M,N] . W[N,K]: reduction over N; A = dy (k-major), B = W as [N][K] (n-major)
   return gemm_impl(dtype, 1, 0, M, K, N, dy, N, w, K, dx, K, dx_dtype, epilogue, nullptr,
-                   const_cast<void*>(aux), K, nullptr, 0, nullptr, 0, (hipStream_t)stream, false);
+                   const_cast<void*>(aux), K, nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, false);
 }
 
 extern "C" size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {

@@ -31,8 +31,10 @@ SIGNATURES = {
     "vitmi_gemm": (I, [I, I, I, L, L, L, P, L, P, L, P, L, I, I, P, P, L, P, L, P, S, P]),
     "vitmi_gemm_workspace_size": (S, [I, I, I, L, L, L, I]),
     "vitmi_gemm_set_policy": (I, [I]),
-    "vitmi_linear_fwd": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P]),
-    "vitmi_linear_dgrad": (I, [I, L, L, L, P, P, P, I, I, P, P]),
+    "vitmi_linear_fwd": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P, S, P]),
+    "vitmi_linear_fwd_workspace_size": (S, [I, L, L, L]),
+    "vitmi_linear_dgrad": (I, [I, L, L, L, P, P, P, I, I, P, P, S, P]),
+    "vitmi_linear_dgrad_workspace_size": (S, [I, L, L, L]),
     "vitmi_linear_wgrad": (I, [I, L, L, L, P, P, P, P, S, P]),
     "vitmi_linear_wgrad_workspace_size": (S, [I, L, L, L]),
     "vitmi_bias_grad": (I, [I, L, L, P, L, P, P, S, P]),

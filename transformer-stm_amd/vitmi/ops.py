@@ -87,8 +87,10 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
     if probe:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
+    nws = lib().vitmi_linear_fwd_workspace_size(dt(x.dtype), M, N, K)
+    ws = _ws(nws, x) if nws else None
     check(lib().vitmi_linear_fwd(dt(x.dtype), M, N, K, _p(x), _p(w), _p(bias), _p(y), dt(out_dtype),
-                                 epilogue, _p(aux), _p(residual), _s()), "linear_fwd")
+                                 epilogue, _p(aux), _p(residual), _p(ws), nws, _s()), "linear_fwd")
     if probe:
         e1.record()
         _PROBE["events"].append((e0, e1))
@@ -102,8 +104,10 @@ def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = 
     M, N = dy.numel() // dy.shape[-1], dy.shape[-1]
     K = w.shape[1]
     dx = torch.empty(*dy.shape[:-1], K, dtype=out_dtype, device=dy.device)
+    nws = lib().vitmi_linear_dgrad_workspace_size(dt(dy.dtype), M, N, K)
+    ws = _ws(nws, dy) if nws else None
     check(lib().vitmi_linear_dgrad(dt(dy.dtype), M, N, K, _p(dy), _p(w), _p(dx), dt(out_dtype),
-                                   epilogue, _p(aux), _s()), "linear_dgrad")
+                                   epilogue, _p(aux), _p(ws), nws, _s()), "linear_dgrad")
     return dx
 
 
