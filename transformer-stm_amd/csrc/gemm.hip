@@ -725,20 +725,26 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         }
       };
       if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM || EPI == VITMI_EPI_DGELU) {
-        // epilogues that load: per column group, batch its 8 loads (one wait for all)
+        // epilogues that load: two row groups at a time, all 4 column groups each (8 loads
+        // per wait), stored row by row like the store-only epilogues below
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          f32x4 ld4[8];
-          bf16x4 ldu[8];
+        for (int mp = 0; mp < 4; ++mp) {
+          f32x4 ld4[2][4];
+          bf16x4 ldu[2][4];
 #pragma unroll
-          for (int mi = 0; mi < 8; ++mi) {
-            const int64_t row = min(m0 + wm * 128 + mi * 16 + lr, g.M - 1);
-            if constexpr (EPI == VITMI_EPI_RESIDUAL) ld4[mi] = *(const f32x4*)(g.residual + row * g.ldr + colc[ni]);
-            if constexpr (EPI == VITMI_EPI_ACCUM) ld4[mi] = *(const f32x4*)((const float*)g.C + row * g.ldc + colc[ni]);
-            if constexpr (EPI == VITMI_EPI_DGELU) ldu[mi] = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + colc[ni]);
+          for (int h = 0; h < 2; ++h) {
+            const int64_t row = min(m0 + wm * 128 + (2 * mp + h) * 16 + lr, g.M - 1);
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+              if constexpr (EPI == VITMI_EPI_RESIDUAL) ld4[h][ni] = *(const f32x4*)(g.residual + row * g.ldr + colc[ni]);
+              if constexpr (EPI == VITMI_EPI_ACCUM) ld4[h][ni] = *(const f32x4*)((const float*)g.C + row * g.ldc + colc[ni]);
+              if constexpr (EPI == VITMI_EPI_DGELU) ldu[h][ni] = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + colc[ni]);
+            }
           }
 #pragma unroll
-          for (int mi = 0; mi < 8; ++mi) emit(mi, ni, ld4[mi], ldu[mi]);
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) emit(2 * mp + h, ni, ld4[h][ni], ldu[h][ni]);
         }
       } else {
         // store-only epilogues go row by row: the 4 column groups of a row (one 128-B line
