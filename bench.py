@@ -66,8 +66,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=8)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=16)
+    ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-optimizer", action="store_true", help="diagnostic only: skip Adam")
     args = ap.parse_args()
 
