@@ -313,6 +313,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
 // "Pipelining across barriers", 8-phase template T3/T4/T5).
 // Block ids are remapped so consecutive tiles of one XCD share an A row panel.
 // =============================================================================
+#ifndef VITMI_STAG_BAL
+#define VITMI_STAG_BAL 0
+#endif
+#ifndef VITMI_STAG_PRIO
+#define VITMI_STAG_PRIO 0
+#endif
 namespace g256 {
 // raw s_barrier that the compiler may not move memory operations across; DMA (vmcnt)
 // stays in flight (a __syncthreads() would drain it).
@@ -373,7 +379,26 @@ __device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf)
 // epilogue.  MFMA operands are swapped (B first): the 16x16 accumulator then holds C^T,
 // i.e. every lane owns 4 consecutive output COLUMNS of one row -> 8/16-byte vector stores
 // straight from registers.
-template <bool AK, bool BKM, int EPI, typename TC>
+//
+// STAG = the staggered ("ping-pong") schedule.  A workgroup's waves w and w+4 share a SIMD.
+// Waves 4..7 run one barrier behind waves 0..3, and every phase is
+//     load section:  ds_read this phase's fragments, issue one half-tile LDS-DMA of the
+//                    next K-step, counted vmcnt;
+//     s_barrier;  compute section: lgkmcnt(0), 16 MFMAs;  s_barrier
+// so in every barrier interval one wave of each SIMD is in its MFMA section while its
+// partner is in its load section: the matrix pipe stays busy and the LDS reads of one
+// wave hide under the partner's MFMAs (cdna_hip_programming.md §5, "The 256² 8-phase
+// template"; MI355X_MICROARCH.md "Two waves per SIMD").
+// Step s (buffer b = s&1) reads A0,B0 @P0, B1 @P1, A1 @P2, nothing @P3 (B0 stays in
+// registers).  Each half is refilled two phases after its last read (the WAR rule once the
+// reads were retired by an lgkmcnt before the reading phase's compute section): P0 DMAs
+// B1(s+1), P1 A1(s+1) into b^1, P2 A0(s+2), P3 B0(s+2) into b, so four half-tiles (8
+// LDS-DMA instructions per wave) are always in flight and each lands ~5 phases before it
+// is read.  The stream of steps runs across tile boundaries (the next tile's steps 0/1).
+// Waits: vmcnt(8) at P0 retires B1(s), at P1 A1(s), at P3 A0(s+1),B0(s+1); each sits
+// before a barrier that the later reader passes, with one barrier of slack for the
+// staggered group.
+template <bool AK, bool BKM, int EPI, typename TC, bool STAG>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   using namespace g256;
   // two DMA stages + the bias of the current and the next tile (fp32, double-buffered)
@@ -446,6 +471,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   // phase's MFMAs: A sets X/Y (A0 halves in X, A1 in Y); B sets 0/1 alternate per K-step
   // (B0 of a K-step is read once, used by p0 AND p3; B1 lives in the other set).
   Frag<bf16> ax[4][2], ay[4][2], b0[2][2], b1[2][2];
+#if VITMI_STAG_BAL
+  Frag<bf16> b2[2][2];   // the other B0 set of the read-balanced staggered schedule
+#endif
   f32x4 acc[8][4];
   // Lane-constant LDS offsets (the swizzles depend only on the lane, not on the fragment):
   //  k-major image [128][64]: frag (tile j, ks) at line w*TW + 16j + l15, chunk (4ks+g)^s,
@@ -495,12 +523,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   } while (0)
 #define MMA4(MH, NH, AS, BS)                                                                    \
   do {                                                                                          \
-    __builtin_amdgcn_s_setprio(1);                                                              \
+    if (!STAG || VITMI_STAG_PRIO == 0) __builtin_amdgcn_s_setprio(1);                          \
     _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
     _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                            \
       acc[MH * 4 + mt][NH * 2 + nt] = mma(BS[nt][ks], AS[mt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
-    __builtin_amdgcn_s_setprio(0);                                                              \
+    if (!STAG || VITMI_STAG_PRIO == 0) __builtin_amdgcn_s_setprio(0);                          \
   } while (0)
   // One K-step s (buffer buf = s & 1).  Entry: A0(s) in ax, B0(s) in BP (preloaded).
   // Each half of buffer buf is refilled for step s+2 right after its last ds_read, so every
@@ -568,7 +596,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   unit_of(tile, m0, n0, ks0, nku);
   __amdgpu_buffer_rsrc_t ra = rsrc_a(m0, ks0), rb = rsrc_b(n0, ks0);
   int buf = 0;
-  {
+  if constexpr (STAG) {
+    // steps 0 and 1 of the first unit in the loop's issue order (nk >= 2 is a precondition)
+    issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 3); issue(ra, rb, 0, 0, 2);
+    issue(ra, rb, 1, 1, 0); issue(ra, rb, 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");      // A0(0), B0(0) landed
+    barrier();
+#if VITMI_STAG_BAL
+    RD_B(b0, 0, 0);                                        // B0(0): read at "P3" of step -1
+#endif
+    if (wm) barrier();                                     // waves 4..7 one barrier behind
+    // VITMI_STAG_PRIO 1: static priority for the staggered half (MI355X_MICROARCH.md "Two
+    // waves per SIMD" item 4) instead of per-MFMA-section priority flips
+    if (VITMI_STAG_PRIO == 1 && wm) __builtin_amdgcn_s_setprio(1);
+  } else {
     // prologue: steps 0 and 1 of the first tile (nk >= 2 is a launch precondition)
     if constexpr (DEEP) {
       issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 3); issue(ra, rb, 0, 0, 2);
@@ -586,6 +627,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   const int lc4 = 4 * (lane >> 4), lr = lane & 15;
   const __amdgpu_buffer_rsrc_t rbias = make_rsrc(g.bias, g.bias ? clamp_bytes(g.N * 4) : 0u);
   int tpar = 0;   // bias buffer of the current tile
+  [[maybe_unused]] bool ep_pending = false;   // an epilogue's stores are still in the vmcnt queue
   for (;;) {
     if constexpr (HAS_BIAS) {
       // bias[n0 + 32*wave .. +32) -> LDS by scalar buffer loads (lgkmcnt, so the vmcnt
@@ -626,6 +668,103 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     const __amdgpu_buffer_rsrc_t s1b = ((T) + 1 < nku) ? rb : rbn;                              \
     const int s1t = ((T) + 1 < nku) ? (T) + 1 : 0;                                              \
     const bool rd1 = (T) + 1 < nku;  /* next tile's step-0 fragments: read after the epilogue */
+    if constexpr (STAG) {
+      // vmcnt counts of the first step after an epilogue: that epilogue issued >= 32 vector
+      // memory ops per wave, all younger than the half-tiles this step waits for
+      constexpr int EPW = 40;
+#define WAITV(N) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory")
+#define COMPUTE(MH, NH, AS, BS)                                                                 \
+      do {                                                                                      \
+        barrier();                                                                              \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                      \
+        MMA4(MH, NH, AS, BS);                                                                   \
+        barrier();                                                                              \
+      } while (0)
+#if VITMI_STAG_BAL
+      // Read-balanced form: B0(t+1) is read at P3(t) into the other B0 register set (8/4/8/4
+      // ds_read_b128 per phase instead of 12/4/8/0), so A0(t+1),B0(t+1) are retired at P2.
+#define SSTEP(T, BC, BN)                                                                        \
+      do {                                                                                      \
+        const bool in1 = (T) + 1 < nku, in2 = (T) + 2 < nku;                                    \
+        const bool h1 = in1 || has_next, h2 = in2 || has_next;                                  \
+        const __amdgpu_buffer_rsrc_t a1 = in1 ? ra : ran, b1r = in1 ? rb : rbn;                 \
+        const __amdgpu_buffer_rsrc_t a2 = in2 ? ra : ran, b2r = in2 ? rb : rbn;                 \
+        const int t1 = in1 ? (T) + 1 : 0, t2 = in2 ? (T) + 2 : (T) + 2 - nku;                   \
+        const bool fst = (T) == 0 && ep_pending;                                                \
+        RD_A(ax, buf, 0);                                   /* P0 (A0,B0) */                    \
+        if (h1) { issue(a1, b1r, t1, buf ^ 1, 3); if (fst) WAITV(EPW); else WAITV(8); }         \
+        else WAITV(0);                                                                          \
+        COMPUTE(0, 0, ax, BC);                                                                  \
+        RD_B(b1, buf, 1);                                   /* P1 (A0,B1) */                    \
+        if (h1) { issue(a1, b1r, t1, buf ^ 1, 2); if (fst) WAITV(EPW); else WAITV(8); }         \
+        else WAITV(0);                                                                          \
+        COMPUTE(0, 1, ax, b1);                                                                  \
+        RD_A(ay, buf, 1);                                   /* P2 (A1,B1) */                    \
+        if (h2) { issue(a2, b2r, t2, buf, 0); if (fst) WAITV(EPW - 2); else WAITV(6); }         \
+        else WAITV(0);                                                                          \
+        COMPUTE(1, 1, ay, b1);                                                                  \
+        if (h1) RD_B(BN, buf ^ 1, 0);                       /* P3 (A1,B0) */                    \
+        if (h2) issue(a2, b2r, t2, buf, 1);                                                     \
+        COMPUTE(1, 0, ay, BC);                                                                  \
+        buf ^= 1;                                                                               \
+      } while (0)
+      for (int t = 0; t < nku; t += 2) {
+        SSTEP(t, b0, b2);
+        if (t + 1 < nku) SSTEP(t + 1, b2, b0);
+      }
+      if (nku & 1) {   // the next unit's first step expects its B0 in b0
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) b0[i][j] = b2[i][j];
+      }
+#undef SSTEP
+#else
+      for (int t = 0; t < nku; ++t) {
+        // step t+1 (B1, A1 still to issue, buffer buf^1) and step t+2 (A0, B0, buffer buf)
+        const bool in1 = t + 1 < nku, in2 = t + 2 < nku;
+        const bool h1 = in1 || has_next, h2 = in2 || has_next;
+        const __amdgpu_buffer_rsrc_t a1 = in1 ? ra : ran, b1r = in1 ? rb : rbn;
+        const __amdgpu_buffer_rsrc_t a2 = in2 ? ra : ran, b2r = in2 ? rb : rbn;
+        const int t1 = in1 ? t + 1 : 0, t2 = in2 ? t + 2 : t + 2 - nku;
+        const bool fst = t == 0 && ep_pending;
+        // P0 (A0,B0): DMA B1(t+1); retire B1(t)
+        RD_A(ax, buf, 0);
+        RD_B(b0, buf, 0);
+        if (h1) {
+          issue(a1, b1r, t1, buf ^ 1, 3);
+          if (fst) WAITV(EPW); else WAITV(8);
+        } else {
+          WAITV(0);
+        }
+        COMPUTE(0, 0, ax, b0);
+        // P1 (A0,B1): DMA A1(t+1); retire A1(t)
+        RD_B(b1, buf, 1);
+        if (h1) {
+          issue(a1, b1r, t1, buf ^ 1, 2);
+          if (fst) WAITV(EPW); else WAITV(8);
+        } else {
+          WAITV(0);
+        }
+        COMPUTE(0, 1, ax, b1);
+        // P2 (A1,B1): DMA A0(t+2) into the half read at P0
+        RD_A(ay, buf, 1);
+        if (h2) issue(a2, b2r, t2, buf, 0);
+        COMPUTE(1, 1, ay, b1);
+        // P3 (A1,B0): DMA B0(t+2); retire A0(t+1), B0(t+1)
+        if (h2) {
+          issue(a2, b2r, t2, buf, 1);
+          if (fst) WAITV(EPW); else WAITV(8);
+        } else {
+          WAITV(0);
+        }
+        COMPUTE(1, 0, ay, b0);
+        buf ^= 1;
+      }
+#endif
+#undef COMPUTE
+#undef WAITV
+    } else {
     for (int t = 0; t < nku; t += 2) {
       {
         STEP_SETUP(t)
@@ -637,6 +776,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         if constexpr (DEEP) KSTEP(b1, b0); else KSTEP1(b1, b0);
         buf ^= 1;
       }
+    }
     }
 #undef STEP_SETUP
 #undef KSTEP
@@ -758,11 +898,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     tpar ^= 1;
     if (!has_next) break;
     it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; ra = ran; rb = rbn;
-    // step-0 fragments of the next tile (its DMA landed before the last p3 barrier; nobody
-    // refills those halves before the next p0 barrier).  Read here rather than in the last
-    // K-step so the epilogue has the fragment registers to itself.
-    RD_A(ax, buf, 0);
-    RD_B(b0, buf, 0);
+    if constexpr (STAG) {
+      ep_pending = true;
+    } else {
+      // step-0 fragments of the next tile (its DMA landed before the last p3 barrier; nobody
+      // refills those halves before the next p0 barrier).  Read here rather than in the last
+      // K-step so the epilogue has the fragment registers to itself.
+      RD_A(ax, buf, 0);
+      RD_B(b0, buf, 0);
+    }
+  }
+  // the leading group owes the staggered group its extra barrier: equal counts per wave
+  if constexpr (STAG) {
+    if (!wm) barrier();
   }
 #undef RD_A
 #undef RD_B
@@ -822,11 +970,13 @@ static int g_policy = 0;
 static int g_cus = 256;   // compute units of the current device (set on first use)
 
 static int g_grid_override = 0;   // VITMI_GEMM_GRID: 0 = persistent (one block per CU), -1 = one block per tile
+static int g_sched = 1;           // VITMI_GEMM_SCHED: 1 = staggered ping-pong K-loop, 0 = lockstep (A/B timing)
 
 static void init_cus() {
   static bool done = false;
   if (done) return;
   if (const char* e = getenv("VITMI_GEMM_GRID")) g_grid_override = atoi(e);
+  if (const char* e = getenv("VITMI_GEMM_SCHED")) g_sched = atoi(e);
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
@@ -899,7 +1049,10 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
         g.ksplit = ks;
         units = g.t_full + ntail * S;
       }
-      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
+      if (g_sched)
+        hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC, true>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
+      else
+        hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC, false>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
       if (units != nwg) {
         const int blocks = (ntail * 256 * 64 + 255) / 256;
