@@ -138,6 +138,18 @@ def test_linear_wgrad_accumulates(M, N, K, T, policy):
     assert rel(dw, ref) < 2e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(197 * 64, 768, 768), (197 * 32 + 5, 2304, 768), (9000, 768, 3072)])
+def test_linear_wgrad_split_units(M, N, K):
+    """Default policy at ViT shapes: gemm256 split-K folded into the persistent unit space
+    (unit = slab * tiles + tile), with ragged reduction length."""
+    dy, x = rnd(M, N, dtype=BF, seed=21), rnd(M, K, dtype=BF, seed=22)
+    prev = rnd(N, K, seed=23)
+    ref = prev + dy.float().t() @ x.float()
+    dw = prev.clone().to(DEV)
+    ops.linear_wgrad(dy.to(DEV), x.to(DEV), dw)
+    assert rel(dw, ref) < 2e-5
+
+
 @pytest.mark.parametrize("T", [BF, torch.float32])
 def test_bias_grad(T):
     dy = rnd(197 * 3 + 1, 2304, dtype=T, seed=14)

@@ -45,6 +45,13 @@ struct GemmArgs {
   int ksplit;
   float* tail_ws;
   size_t tail_ws_bytes;
+  // gemm256 split-K folded into the persistent unit space (EPI_PARTIAL): unit = z*ntiles +
+  // tile, slab z covers K-steps [z*kz_steps, (z+1)*kz_steps).  Consecutive units share one
+  // K-range, so the contiguous unit range of an XCD re-reads its A/B panels from that
+  // XCD's L2 (a gridDim.z split scatters them over all XCDs).
+  int kz;          // 1 = no folded split
+  int kz_steps;
+  int ntiles;
 };
 
 enum { EPI_PARTIAL = 100 };
@@ -443,11 +450,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
                : make_rsrc((const char*)g.B + (k * g.ldb + n0) * 2, clamp_bytes(((g.K - k) * g.ldb - n0) * 2));
   };
   // unit u -> tile origin, first K-step and K-step count
-  auto unit_of = [&](int u, int64_t& m0_, int64_t& n0_, int& ks0_, int& nk_) {
+  auto unit_of = [&](int u, int64_t& m0_, int64_t& n0_, int& ks0_, int& nk_, int& z_) {
     int tl = u;
     ks0_ = 0;
     nk_ = nk;
-    if (u >= g.t_full) {
+    z_ = 0;
+    if (EPI == EPI_PARTIAL && g.kz > 1) {
+      z_ = u / g.ntiles;
+      tl = u - z_ * g.ntiles;
+      ks0_ = z_ * g.kz_steps;
+      nk_ = min(g.kz_steps, nk - ks0_);
+    } else if (u >= g.t_full) {
       const int v = u - g.t_full;
       tl = g.t_full + v / g.nsplit;
       ks0_ = (v % g.nsplit) * g.ksplit;
@@ -592,8 +605,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   if (it >= nseq) return;
   int tile = unit_at(it);   // work unit (a whole tile, or a K-range of a tail tile)
   int64_t m0, n0;
-  int ks0, nku;
-  unit_of(tile, m0, n0, ks0, nku);
+  int ks0, nku, zs;
+  unit_of(tile, m0, n0, ks0, nku, zs);
   __amdgpu_buffer_rsrc_t ra = rsrc_a(m0, ks0), rb = rsrc_b(n0, ks0);
   int buf = 0;
   if constexpr (STAG) {
@@ -630,27 +643,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   [[maybe_unused]] bool ep_pending = false;   // an epilogue's stores are still in the vmcnt queue
   for (;;) {
     if constexpr (HAS_BIAS) {
-      // bias[n0 + 32*wave .. +32) -> LDS by scalar buffer loads (lgkmcnt, so the vmcnt
-      // accounting of the DMA and of the stores is untouched; the range check zero-fills
-      // columns >= N and a null bias).  Read by the epilogue after many barriers.
-      typedef int i32x16 __attribute__((ext_vector_type(16)));
-      i32x16 s0, s1;
-      const int boff = __builtin_amdgcn_readfirstlane((int)((n0 + 32 * wave) * 4));
-      asm volatile("s_buffer_load_dwordx16 %0, %2, %3\n\ts_buffer_load_dwordx16 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
-                   : "=s"(s0), "=s"(s1) : "s"(rbias), "s"(boff), "s"(boff + 64) : "memory");
-      int bvv = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(bvv) : "s"(s0[i]), "i"(i));
-#pragma unroll
-      for (int i = 0; i < 16; ++i) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(bvv) : "s"(s1[i]), "i"(16 + i));
-      if (lane < 32) *(int*)(smem + 2 * STAGE + tpar * 1024 + (32 * wave + lane) * 4) = bvv;
+      // bias[n0 .. n0+256) -> LDS by ONE LDS-DMA instruction of wave 0 (64 lanes x 16 B; the
+      // range check zero-fills columns >= N and a null bias).  It is older than every DMA the
+      // K-loop waits for, so it only makes those counted waits stricter; the epilogue reads it
+      // many barriers later.
+      if (wave == 0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rbias, LDS_PTR(void, smem + 2 * STAGE + tpar * 1024), 16,
+                                                 (uint32_t)(n0 * 4 + lane * 16), 0, 0, 0);
     }
     const int itn = it + nbx;
     const bool has_next = itn < nseq;
     const int next = has_next ? unit_at(itn) : 0;
     int64_t m0n = 0, n0n = 0;
-    int ks0n = 0, nkn = 0;
-    if (has_next) unit_of(next, m0n, n0n, ks0n, nkn);
+    int ks0n = 0, nkn = 0, zsn = 0;
+    if (has_next) unit_of(next, m0n, n0n, ks0n, nkn, zsn);
     const __amdgpu_buffer_rsrc_t ran = rsrc_a(m0n, ks0n), rbn = rsrc_b(n0n, ks0n);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -783,7 +789,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #undef KSTEP1
 #undef MMA4
 
-    if (tile >= g.t_full) {
+    if ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) {
       // K-range of a tail tile: raw fp32 partial into its [256][256] slab
       const __amdgpu_buffer_rsrc_t rw = make_rsrc(g.tail_ws + (int64_t)(tile - g.t_full) * BM * BN, BM * BN * 4);
       const uint32_t wbase = (uint32_t)(((wm * 128 + lr) * BN + wn * 64 + lc4) * 4);
@@ -803,7 +809,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     {
       constexpr int CES = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM &&
                                   EPI != VITMI_EPI_RESIDUAL ? 2 : 4;
-      const int64_t zoff = EPI == EPI_PARTIAL ? (int64_t)blockIdx.z * g.split_stride : 0;
+      int64_t zoff = 0;
+      if constexpr (EPI == EPI_PARTIAL) zoff = (int64_t)(blockIdx.z + zs) * g.split_stride;
       char* cbase = (char*)g.C + (zoff + m0 * g.ldc + n0) * CES;
       const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, clamp_bytes(((g.M - m0) * g.ldc - n0) * CES));
       const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
@@ -897,7 +904,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     }
     tpar ^= 1;
     if (!has_next) break;
-    it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; ra = ran; rb = rbn;
+    it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
     if constexpr (STAG) {
       ep_pending = true;
     } else {
@@ -971,12 +978,16 @@ static int g_cus = 256;   // compute units of the current device (set on first u
 
 static int g_grid_override = 0;   // VITMI_GEMM_GRID: 0 = persistent (one block per CU), -1 = one block per tile
 static int g_sched = 1;           // VITMI_GEMM_SCHED: 1 = staggered ping-pong K-loop, 0 = lockstep (A/B timing)
+static int g_fold = 1;            // VITMI_GEMM_FOLD: 1 = split-K folded into persistent units, 0 = gridDim.z
+static int g_split256 = 1;        // VITMI_GEMM_SPLIT256: 1 = few-tile split-K GEMMs on gemm256
 
 static void init_cus() {
   static bool done = false;
   if (done) return;
   if (const char* e = getenv("VITMI_GEMM_GRID")) g_grid_override = atoi(e);
   if (const char* e = getenv("VITMI_GEMM_SCHED")) g_sched = atoi(e);
+  if (const char* e = getenv("VITMI_GEMM_FOLD")) g_fold = atoi(e);
+  if (const char* e = getenv("VITMI_GEMM_SPLIT256")) g_split256 = atoi(e);
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
@@ -984,12 +995,24 @@ static void init_cus() {
   done = true;
 }
 
-static bool use256(int dtype, int64_t M, int64_t N) {
+static int64_t splits_for(int64_t tiles, int64_t ktiles, int64_t target) {
+  int64_t want = target / tiles;
+  const int64_t maxs = ktiles / 4;
+  if (want > maxs) want = maxs;
+  if (want > 64) want = 64;
+  return want < 1 ? 1 : want;
+}
+
+// gemm256 for this shape?  `split`: the caller may split K (wgrad), which fills the chip
+// with units even when there are few output tiles.
+static bool use256(int dtype, int64_t M, int64_t N, int64_t K = 0, bool split = false) {
   if (dtype != VITMI_BF16 || (N % 8) != 0) return false;
   if (g_policy == 1) return false;
   if (g_policy >= 2) return true;
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  return tiles >= 16;
+  if (tiles >= 16) return true;
+  init_cus();
+  return split && g_split256 && tiles * splits_for(tiles, (K + 63) / 64, 256) >= 128;
 }
 
 // persistent grid of the gemm256 launch for nwg tiles and `splits` K-slabs
@@ -1031,7 +1054,17 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (big) {
       g.tiles_n = (int)((g.N + 255) / 256);
-      const int nwg = (int)((g.M + 255) / 256) * g.tiles_n;
+      int nwg = (int)((g.M + 255) / 256) * g.tiles_n;
+      g.kz = 1;
+      g.ntiles = nwg;
+      if (splits > 1 && g_fold) {
+        // fold the K-slabs into the persistent unit space (see GemmArgs::kz)
+        g.kz = splits;
+        g.kz_steps = (int)(g.k_per_split / 64);
+        g.k_per_split = ((g.K + 63) / 64) * 64;
+        nwg *= splits;
+        splits = 1;
+      }
       const int gx = grid256(nwg, splits);
       int units = nwg, S = 1, ks = 0, ntail = 0;
       g.t_full = nwg;
@@ -1107,16 +1140,11 @@ static int bk_of(int dtype) { return dtype == VITMI_BF16 ? 64 : 32; }
 // split count for a reduction-heavy GEMM (wgrad): about one full round of blocks
 // (1 block/CU for gemm256, ~2 for the 128 kernel), at least 4 k-tiles per split.
 static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K) {
-  const bool big = use256(dtype, M, N);
+  const bool big = use256(dtype, M, N, K, true);
   const int64_t t = big ? 256 : 128;
   const int64_t tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
   const int64_t ktiles = (K + bk_of(dtype) - 1) / bk_of(dtype);
-  const int64_t target = big ? 256 : 512;
-  int64_t want = target / tiles;
-  int64_t maxs = ktiles / 4;
-  if (want > maxs) want = maxs;
-  if (want > 64) want = 64;
-  return want < 1 ? 1 : (int)want;
+  return (int)splits_for(tiles, ktiles, big ? 256 : 512);
 }
 
 static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K, const void* A,
@@ -1144,7 +1172,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   // 32-bit buffer offsets: one block's panel must stay under 2 GiB
   VITMI_CHECK_ARG((ak ? 128 * lda : K * lda) * es < 0x7fffffffLL, "gemm: A panel exceeds 2 GiB");
 
-  const bool big = use256(dtype, M, N);
+  const bool big = use256(dtype, M, N, K, allow_split && epi == VITMI_EPI_ACCUM);
   if (big) {
     init_cus();
     VITMI_CHECK_ARG(ldc % 8 == 0 && (ldr % 4) == 0 && (ldaux % 8) == 0 && ((uintptr_t)C % 16) == 0,
