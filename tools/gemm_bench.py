@@ -37,9 +37,12 @@ def main():
     gq = r(M, 3 * D)
     dw = torch.zeros(F, D, device="cuda")
     a8, b8 = r(8192, 8192), r(8192, 8192)
+    c8 = torch.empty(8192, 8192, device="cuda", dtype=BF)
     cases = {
         "square bf16    [8192^3]": (lambda: ops.linear_fwd(a8, b8, None, BF), 2 * 8192 ** 3),
         "torch square   [8192^3]": (lambda: torch.mm(a8, b8.t()), 2 * 8192 ** 3),
+        "square NN      [8192^3]": (lambda: ops.gemm(a8, b8, True, False, 8192, 8192, 8192, c8), 2 * 8192 ** 3),
+        "square TN      [8192^3]": (lambda: ops.gemm(a8, b8, False, False, 8192, 8192, 8192, c8), 2 * 8192 ** 3),
         "fc1 fwd store  [M,3072,768]": (lambda: ops.linear_fwd(x, w1, b1, BF), 2 * M * F * D),
         "fc1 fwd f32out [M,3072,768]": (lambda: ops.linear_fwd(x, w1, b1, torch.float32), 2 * M * F * D),
         "fc1 fwd +GELU  [M,3072,768]": (lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU), 2 * M * F * D),

@@ -320,6 +320,13 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
 // "Pipelining across barriers", 8-phase template T3/T4/T5).
 // Block ids are remapped so consecutive tiles of one XCD share an A row panel.
 // =============================================================================
+// row groups per load batch of the loading epilogues (bf16 gelu' / fp32 residual+accum)
+#ifndef VITMI_EPI_RB_BF16
+#define VITMI_EPI_RB_BF16 8
+#endif
+#ifndef VITMI_EPI_RB_F32
+#define VITMI_EPI_RB_F32 4
+#endif
 #ifndef VITMI_STAG_BAL
 #define VITMI_STAG_BAL 0
 #endif
@@ -872,15 +879,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         }
       };
       if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM || EPI == VITMI_EPI_DGELU) {
-        // epilogues that load: two row groups at a time, all 4 column groups each (8 loads
-        // per wait), stored row by row like the store-only epilogues below
+        // epilogues that load: RB row groups at a time (all 4 column groups each; 64 VGPRs of
+        // loaded operand per wait -- the fragment registers are free here), stored row by row
+        // like the store-only epilogues below
+        constexpr int RB = EPI == VITMI_EPI_DGELU ? VITMI_EPI_RB_BF16 : VITMI_EPI_RB_F32;
 #pragma unroll
-        for (int mp = 0; mp < 4; ++mp) {
-          f32x4 ld4[2][4];
-          bf16x4 ldu[2][4];
+        for (int mp = 0; mp < 8 / RB; ++mp) {
+          f32x4 ld4[RB][4];
+          bf16x4 ldu[RB][4];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int64_t row = min(m0 + wm * 128 + (2 * mp + h) * 16 + lr, g.M - 1);
+          for (int h = 0; h < RB; ++h) {
+            const int64_t row = min(m0 + wm * 128 + (RB * mp + h) * 16 + lr, g.M - 1);
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
               if constexpr (EPI == VITMI_EPI_RESIDUAL) ld4[h][ni] = *(const f32x4*)(g.residual + row * g.ldr + colc[ni]);
@@ -889,9 +898,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             }
           }
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
+          for (int h = 0; h < RB; ++h)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) emit(2 * mp + h, ni, ld4[h][ni], ldu[h][ni]);
+            for (int ni = 0; ni < 4; ++ni) emit(RB * mp + h, ni, ld4[h][ni], ldu[h][ni]);
         }
       } else {
         // store-only epilogues go row by row: the 4 column groups of a row (one 128-B line
