@@ -1,0 +1,21 @@
+"""Run the bf16 attention forward + backward at the ViT-B/16 bs=256 shape a few times (the
+target of a rocprofv3 --pmc pass).  usage: python tools/attn_one.py [iters]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "transformer-stm_amd"))
+import torch  # noqa: E402
+
+from vitmi import ops  # noqa: E402
+
+B, N, H = 256, 197, 12
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+g = torch.Generator(device="cuda").manual_seed(0)
+qkv = (torch.randn(B * N, 3 * 64 * H, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+do = torch.randn(B * N, 64 * H, device="cuda", generator=g).to(torch.bfloat16)
+for _ in range(iters):
+    o, lse = ops.attention_fwd(qkv, B, N, H, 0.125)
+    ops.attention_bwd(qkv, o, do, lse, B, N, H, 0.125)
+torch.cuda.synchronize()
+print("done", iters)
