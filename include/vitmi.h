@@ -155,6 +155,29 @@ int vitmi_head_bwd(int B, int D, int C, const float* dlogits, const float* y, in
 int vitmi_loss_fwd_bwd(int kind, int B, int C, const float* logits, const void* target,
                        float* loss, float* dlogits, vitmi_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Dropout (layers.Dropout, models/CvT(Par).py:189 after the out-projection, :255 after the
+ * GELU, :257 after fc2; Keras rate 0.1, active in training only).  Element (row, col) of
+ * dropout site `site` is kept iff vitmi_dropout_hash(seed, site, row, col) >= thresh, with
+ * thresh = round(p * 2^32), and kept values are scaled by `scale` = 1/(1-p).  The mask is a
+ * pure function of its coordinates: it is regenerated in the backward, never stored.
+ */
+uint32_t vitmi_dropout_hash(uint32_t seed, uint32_t site, uint32_t row, uint32_t col);
+/* vitmi_linear_fwd with the dropout fused into the epilogue:
+ *   BIAS_GELU: y = gelu(u) * keep * scale, aux = gelu'(u) * keep * scale (so the DGELU
+ *              backward of the dropped activation needs no mask);
+ *   RESIDUAL:  y = residual + (acc + bias) * keep * scale.   (x, W k-major as in linear_fwd) */
+int vitmi_linear_fwd_dropout(int dtype, int64_t M, int64_t N, int64_t K, const void* x,
+                             const void* w, const float* bias, void* y, int y_dtype, int epilogue,
+                             void* aux, const float* residual, void* workspace, size_t ws_bytes,
+                             uint32_t seed, uint32_t site, uint32_t thresh, float scale,
+                             vitmi_stream_t stream);
+/* y[M][ldy] (f32 or bf16) = x[M][ldx] (f32) * keep * scale   (N % 4 == 0): the masked
+ * gradient of a dropped branch in the backward */
+int vitmi_dropout_apply(int64_t M, int64_t N, const float* x, int64_t ldx, void* y, int y_dtype,
+                        int64_t ldy, uint32_t seed, uint32_t site, uint32_t thresh, float scale,
+                        vitmi_stream_t stream);
+
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
 

@@ -36,8 +36,9 @@ both.  The TF/Keras boundary itself is unpinned (TensorFlow is not installed).
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional, Tuple
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -105,12 +106,55 @@ def init_params(cfg, seed: int = 0, randomize_all: bool = True) -> Dict[str, Ten
     return out
 
 
+# ---------------------------------------------------------------- dropout
+# layers.Dropout at models/CvT(Par).py:189 (after the out-projection), :255 (after the GELU)
+# and :257 (after fc2); Keras' rate 0.1, active in training only.  Keras draws its mask from
+# TF's stateful RNG (unreproducible here, and TF is absent); the build defines the mask as a
+# counter hash of (seed, site, row, col) -- restated here bit for bit from the C ABI's
+# vitmi_dropout_hash (include/vitmi.h) -- so the oracle and the device path drop the SAME
+# elements.  Sites: block i -> 3i (proj), 3i+1 (GELU), 3i+2 (fc2); rows = b*N + token.
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _fmix32(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x85EBCA6B)) & _M32
+    x ^= x >> np.uint64(13)
+    x = (x * np.uint64(0xC2B2AE35)) & _M32
+    x ^= x >> np.uint64(16)
+    return x
+
+
+def dropout_hash(seed: int, site: int, rows: np.ndarray, cols: np.ndarray) -> np.ndarray:
+    """uint32 hash of every (row, col) pair of the broadcast of rows[:, None], cols[None, :]."""
+    rows = np.asarray(rows, dtype=np.uint64)
+    cols = np.asarray(cols, dtype=np.uint64)
+    base = np.uint64(seed & 0xFFFFFFFF) ^ ((np.uint64(site) * np.uint64(0x9E3779B1)) & _M32)
+    rk = _fmix32(base ^ _fmix32((rows + np.uint64(0x7F4A7C15)) & _M32))
+    return _fmix32(rk[:, None] ^ ((cols[None, :] * np.uint64(0x85EBCA77)) & _M32))
+
+
+def dropout_params(p: float) -> Tuple[int, float]:
+    """(thresh, scale): keep iff hash >= thresh = round(p * 2^32); kept values * 1/(1-p)."""
+    return min(int(round(p * 2.0 ** 32)), 0xFFFFFFFF), 1.0 / (1.0 - p)
+
+
+def dropout(x: Tensor, seed: int, site: int, p: float) -> Tensor:
+    """x [..., C] with rows = the flattened leading dims (token-major, like the device GEMMs)."""
+    shape = x.shape
+    x2 = x.reshape(-1, shape[-1])
+    thresh, scale = dropout_params(p)
+    keep = dropout_hash(seed, site, np.arange(x2.shape[0]), np.arange(x2.shape[1])) >= thresh
+    return (x2 * torch.from_numpy(keep.astype(np.float32)) * scale).reshape(shape)
+
+
 def layer_norm(x: Tensor, w: Tensor, b: Tensor, eps: float) -> Tensor:
     # models/CvT(Par).py:248 (LayerNormalization over the channel axis)
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
 
 
-def attention(x: Tensor, p: Dict[str, Tensor], pre: str, cfg) -> Tensor:
+def attention(x: Tensor, p: Dict[str, Tensor], pre: str, cfg, drop=None) -> Tensor:
     """ConvAttention.call with identity projections (models/CvT(Par).py:144-191)."""
     B, N, D = x.shape
     H = cfg.num_heads
@@ -124,22 +168,36 @@ def attention(x: Tensor, p: Dict[str, Tensor], pre: str, cfg) -> Tensor:
     s = torch.matmul(q, k.transpose(-1, -2)) * scale           # old_codes/MS_CvT.py:202
     a = torch.softmax(s, dim=-1)                                # :203
     o = torch.matmul(a, v).transpose(1, 2).reshape(B, N, D)     # :206-207
-    return F.linear(o, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"])  # :209
+    out = F.linear(o, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"])  # :209
+    if drop is not None:                                        # proj_dropout, CvT(Par).py:189
+        out = dropout(out, drop[0], drop[1], drop[2])
+    return out
 
 
-def mlp(x: Tensor, p: Dict[str, Tensor], pre: str) -> Tensor:
-    """Mlp: Dense(4D, gelu) -> Dense(D) (models/CvT(Par).py:253-258)."""
+def mlp(x: Tensor, p: Dict[str, Tensor], pre: str, drop=None) -> Tensor:
+    """Mlp: Dense(4D, gelu) -> Dropout -> Dense(D) -> Dropout (models/CvT(Par).py:253-258).
+    ``drop`` = (seed, first site, rate) or None (inference / rate 0)."""
     h = F.linear(x, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])
     h = F.gelu(h)  # exact erf GELU (tf.nn.gelu default approximate=False)
-    return F.linear(h, p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+    if drop is not None:
+        h = dropout(h, drop[0], drop[1], drop[2])
+    y = F.linear(h, p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+    if drop is not None:
+        y = dropout(y, drop[0], drop[1] + 1, drop[2])
+    return y
 
 
-def block(x: Tensor, p: Dict[str, Tensor], i: int, cfg) -> Tensor:
-    """ConvTransformerBlock.call (models/CvT(Par).py:261-289)."""
+def block(x: Tensor, p: Dict[str, Tensor], i: int, cfg, drop_seed: Optional[int] = None) -> Tensor:
+    """ConvTransformerBlock.call (models/CvT(Par).py:261-289).  ``drop_seed``: training-mode
+    dropout at ``cfg.drop_rate`` (sites 3i, 3i+1, 3i+2)."""
     pre = f"blocks.{i}."
     n2 = "norm1" if cfg.tie_norms else "norm2"
-    x = x + attention(layer_norm(x, p[pre + "norm1.weight"], p[pre + "norm1.bias"], cfg.ln_eps), p, pre, cfg)
-    x = x + mlp(layer_norm(x, p[pre + n2 + ".weight"], p[pre + n2 + ".bias"], cfg.ln_eps), p, pre)
+    rate = getattr(cfg, "drop_rate", 0.0)
+    on = drop_seed is not None and rate > 0
+    da = (drop_seed, 3 * i, rate) if on else None
+    dm = (drop_seed, 3 * i + 1, rate) if on else None
+    x = x + attention(layer_norm(x, p[pre + "norm1.weight"], p[pre + "norm1.bias"], cfg.ln_eps), p, pre, cfg, da)
+    x = x + mlp(layer_norm(x, p[pre + n2 + ".weight"], p[pre + n2 + ".bias"], cfg.ln_eps), p, pre, dm)
     return x
 
 
@@ -158,16 +216,16 @@ def embed(img: Tensor, p: Dict[str, Tensor], cfg) -> Tensor:
     return x
 
 
-def forward_features(img: Tensor, p: Dict[str, Tensor], cfg) -> Tensor:
+def forward_features(img: Tensor, p: Dict[str, Tensor], cfg, drop_seed: Optional[int] = None) -> Tensor:
     x = embed(img, p, cfg)
     for i in range(cfg.depth):
-        x = block(x, p, i, cfg)
+        x = block(x, p, i, cfg, drop_seed)
     return x
 
 
-def forward(img: Tensor, p: Dict[str, Tensor], cfg) -> Tensor:
+def forward(img: Tensor, p: Dict[str, Tensor], cfg, drop_seed: Optional[int] = None) -> Tensor:
     """Logits [B, num_classes] (head: models/CvT(Par).py:326-329,350)."""
-    x = forward_features(img, p, cfg)
+    x = forward_features(img, p, cfg, drop_seed)
     cls = x[:, 0] if cfg.with_cls_token else x.mean(dim=1)
     cls = layer_norm(cls, p["norm.weight"], p["norm.bias"], cfg.ln_eps)
     return F.linear(cls, p["head.weight"], p["head.bias"])
@@ -180,10 +238,10 @@ def loss_fn(logits: Tensor, target: Tensor, num_classes: int) -> Tensor:
     return F.cross_entropy(logits, target.long())
 
 
-def forward_backward(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg):
+def forward_backward(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg, drop_seed: Optional[int] = None):
     """One fwd+bwd step on the CPU: returns (logits, loss, {name: grad})."""
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    logits = forward(img, leaves, cfg)
+    logits = forward(img, leaves, cfg, drop_seed)
     loss = loss_fn(logits, target, cfg.num_classes)
     loss.backward()
     grads = {k: v.grad.detach() for k, v in leaves.items()}
@@ -211,5 +269,6 @@ def rel_err(a: Tensor, b: Tensor) -> float:
 __all__ = [
     "param_shapes", "init_params", "forward", "forward_features", "forward_backward",
     "loss_fn", "synthetic_batch", "rel_err", "layer_norm", "attention", "mlp", "block", "embed",
+    "dropout", "dropout_hash", "dropout_params",
 ]
 

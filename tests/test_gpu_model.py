@@ -158,3 +158,67 @@ def test_adam_training_tracks_oracle():
     got16 = _train(cfg.replace(dtype="bf16"), params, img, tgt, 8, 3e-4, on_gpu=True)
     assert max(abs(a - b) for a, b in zip(ref, got16)) < 2e-2, (ref, got16)
     assert ref[-1] < ref[0]
+
+
+# ------------------------------------------------------------------ dropout (row a12)
+def _drop_step(cfg, params, img, tgt, seed, train=True):
+    model = VisionTransformer(cfg).cuda()
+    model.load_param_dict(params)
+    model.drop_seed = seed
+    model.train(train)
+    logits = model(img.cuda())
+    loss = cross_entropy(logits, tgt.cuda())
+    loss.backward()
+    grads = {k: p.grad.detach().cpu() for k, p in model.named_parameters()}
+    return logits.detach().cpu(), loss.detach().cpu(), grads
+
+
+@pytest.mark.parametrize("dtype,ltol,gtol", [("fp32", 1e-4, 1e-4), ("bf16", 5e-2, 2e-2)])
+def test_dropout_training_matches_oracle(dtype, ltol, gtol):
+    """Keras' training-mode Dropout (models/CvT(Par).py:189,255,257) at rate 0.1: the device
+    epilogues and masked backward copies drop exactly the oracle's elements (same hash)."""
+    cfg = ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2, num_classes=2,
+                    dtype=dtype, drop_rate=0.1)
+    params = vit_ref.init_params(cfg, seed=0)
+    img, tgt = vit_ref.synthetic_batch(cfg, 4)
+    l_ref, loss_ref, g_ref = vit_ref.forward_backward(img, tgt, params, cfg, drop_seed=4242)
+    l_nodrop, _, _ = vit_ref.forward_backward(img, tgt, params, cfg)
+    assert (l_ref - l_nodrop).abs().max().item() > 1e-3      # the masks do act
+    l, loss, g = _drop_step(cfg, params, img, tgt, 4242)
+    assert (l - l_ref).abs().max().item() <= ltol
+    worst = max((vit_ref.rel_err(g[k], g_ref[k]), k) for k in g_ref)
+    assert worst[0] <= gtol, f"grad {worst[1]} rel {worst[0]:.3e}"
+
+
+def test_dropout_eval_mode_is_identity():
+    cfg = ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=2, num_heads=2, num_classes=2,
+                    dtype="fp32", drop_rate=0.1)
+    params = vit_ref.init_params(cfg, seed=0)
+    img, tgt = vit_ref.synthetic_batch(cfg, 4)
+    l_ref, _, g_ref = vit_ref.forward_backward(img, tgt, params, cfg)
+    l, _, g = _drop_step(cfg, params, img, tgt, 4242, train=False)
+    assert (l - l_ref).abs().max().item() <= 1e-4
+    assert max(vit_ref.rel_err(g[k], g_ref[k]) for k in g_ref) <= 1e-4
+
+
+def test_dropout_vit_shape_rate_and_scale():
+    """ViT-B rows x 3072 GELU activations: the fused epilogue keeps ~90% and scales by 1/0.9."""
+    from vitmi import ops
+    g = torch.Generator(device="cuda").manual_seed(0)
+    M, D, F = 197 * 16, 768, 3072
+    x = (torch.rand(M, D, device="cuda", generator=g) - 0.5).to(torch.bfloat16)
+    w = ((torch.rand(F, D, device="cuda", generator=g) - 0.5) * 0.1).to(torch.bfloat16)
+    b = torch.zeros(F, device="cuda")
+    a0, u0 = ops.linear_fwd(x, w, b, torch.bfloat16, ops.EPI_BIAS_GELU)
+    a1, u1 = ops.linear_fwd(x, w, b, torch.bfloat16, ops.EPI_BIAS_GELU, dropout=(7, 1, 0.1))
+    keep = vit_ref.dropout_hash(7, 1, np.arange(M), np.arange(F)) >= vit_ref.dropout_params(0.1)[0]
+    keep_t = torch.from_numpy(keep).cuda()
+    assert abs(keep.mean() - 0.9) < 0.005
+    assert torch.all(a1[~keep_t] == 0) and torch.all(u1[~keep_t] == 0)
+    ref = (a0.float() / 0.9)[keep_t]
+    assert ((a1.float()[keep_t] - ref).abs() <= 1e-2 * ref.abs() + 1e-3).all()
+    # the backward copy uses the same mask
+    gsrc = torch.randn(M, F, device="cuda", generator=g)
+    gm = ops.dropout_apply(gsrc, 7, 1, 0.1, torch.float32)
+    assert torch.equal(gm[~keep_t], torch.zeros_like(gm[~keep_t]))
+    assert torch.allclose(gm[keep_t], gsrc[keep_t] / 0.9, rtol=1e-6, atol=0)

@@ -52,6 +52,27 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return cdf + x * pdf;
 }
 
+// ---------------------------------------------------------------- dropout mask
+// Keep-mask of dropout (layers.Dropout, models/CvT(Par).py:189,255,257; Keras rate 0.1 in
+// training): a counter hash of (seed, site, row, col) built from murmur3's 32-bit finaliser,
+// keep iff hash >= thresh with thresh = round(p * 2^32).  Kept elements are scaled by
+// 1/(1-p).  The mask is regenerated wherever it is needed (forward epilogue, backward copy)
+// and never stored; oracle/vit_ref.py restates the same function bit for bit.
+__host__ __device__ inline uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+__host__ __device__ inline uint32_t drop_row_key(uint32_t seed, uint32_t site, uint32_t row) {
+  return fmix32(seed ^ (site * 0x9E3779B1u) ^ fmix32(row + 0x7F4A7C15u));
+}
+__host__ __device__ inline uint32_t drop_hash(uint32_t row_key, uint32_t col) {
+  return fmix32(row_key ^ (col * 0x85EBCA77u));
+}
+
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -263,6 +263,33 @@ __global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16* __re
   if (t < n) dst[t] = (bf16)src[t];
 }
 
+// y[r][c] = x[r][c] * keep(seed, site, r, c) / (1 - p): the dropout mask applied to a
+// gradient in the backward (the forward fuses it into the GEMM epilogues).  4 columns per
+// thread; N % 4 == 0.
+template <typename TO>
+__global__ void dropout_apply_kernel(int64_t M, int64_t N, const float* __restrict__ x, int64_t ldx,
+                                     TO* __restrict__ y, int64_t ldy, uint32_t seed, uint32_t site,
+                                     uint32_t thresh, float scale) {
+  const int64_t n4 = N / 4, total = M * n4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / n4, c = (i - r * n4) * 4;
+    const uint32_t rk = drop_row_key(seed, site, (uint32_t)r);
+    const f32x4 v = *(const f32x4*)(x + r * ldx + c);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = drop_hash(rk, (uint32_t)(c + e)) >= thresh ? v[e] * scale : 0.f;
+    if constexpr (sizeof(TO) == 4) {
+      *(f32x4*)(y + r * ldy + c) = o;
+    } else {
+      bf16x4 b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b[e] = (bf16)o[e];
+      *(bf16x4*)(y + r * ldy + c) = b;
+    }
+  }
+}
+
 static unsigned grid_for(int64_t work, int per_block = 256) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g > 8192) g = 8192;
@@ -393,4 +420,28 @@ extern "C" int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi
                      (bf16*)dst);
   VITMI_LAUNCH_CHECK("cast");
   return VITMI_OK;
+}
+
+extern "C" int vitmi_dropout_apply(int64_t M, int64_t N, const float* x, int64_t ldx, void* y,
+                                   int y_dtype, int64_t ldy, uint32_t seed, uint32_t site,
+                                   uint32_t thresh, float scale, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(x && y, "dropout_apply: null pointer");
+  VITMI_CHECK_ARG(y_dtype == VITMI_F32 || y_dtype == VITMI_BF16, "dropout_apply: bad dtype %d", y_dtype);
+  VITMI_CHECK_ARG(N % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ldx >= N && ldy >= N,
+                  "dropout_apply: N and leading dims must be multiples of 4");
+  VITMI_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 8) == 0, "dropout_apply: alignment");
+  if (M == 0 || N == 0) return VITMI_OK;
+  const unsigned grid = grid_for(M * N / 4);
+  if (y_dtype == VITMI_F32)
+    hipLaunchKernelGGL(dropout_apply_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, N, x, ldx,
+                       (float*)y, ldy, seed, site, thresh, scale);
+  else
+    hipLaunchKernelGGL(dropout_apply_kernel<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, M, N, x, ldx,
+                       (bf16*)y, ldy, seed, site, thresh, scale);
+  VITMI_LAUNCH_CHECK("dropout_apply");
+  return VITMI_OK;
+}
+
+extern "C" uint32_t vitmi_dropout_hash(uint32_t seed, uint32_t site, uint32_t row, uint32_t col) {
+  return drop_hash(drop_row_key(seed, site, row), col);
 }

@@ -52,9 +52,27 @@ struct GemmArgs {
   int kz;          // 1 = no folded split
   int kz_steps;
   int ntiles;
+  // dropout of the *_DROP epilogues (see drop_hash in common.h)
+  uint32_t drop_seed, drop_site, drop_thresh;
+  float drop_scale;
 };
 
-enum { EPI_PARTIAL = 100 };
+// internal epilogues: split-K partial slab, and GELU / residual with a fused dropout
+enum { EPI_PARTIAL = 100, EPI_GELU_DROP = 101, EPI_RESIDUAL_DROP = 102 };
+// the public epilogue an internal one extends, and whether it drops
+template <int EPI> struct EpiOf {
+  static constexpr int base = EPI == EPI_GELU_DROP ? VITMI_EPI_BIAS_GELU
+                              : EPI == EPI_RESIDUAL_DROP ? VITMI_EPI_RESIDUAL : EPI;
+  static constexpr bool drop = EPI == EPI_GELU_DROP || EPI == EPI_RESIDUAL_DROP;
+};
+static inline int epi_base(int epi) {
+  return epi == EPI_GELU_DROP ? VITMI_EPI_BIAS_GELU : epi == EPI_RESIDUAL_DROP ? VITMI_EPI_RESIDUAL : epi;
+}
+// dropout factor (0 or 1/(1-p)) of output element (row, col)
+__device__ __forceinline__ float drop_factor(const GemmArgs& g, int64_t row, int64_t col) {
+  return drop_hash(drop_row_key(g.drop_seed, g.drop_site, (uint32_t)row), (uint32_t)col) >= g.drop_thresh
+             ? g.drop_scale : 0.f;
+}
 
 __device__ __forceinline__ int swz_k(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int swz_mn(int k) { return 2 * (k & 3) + 8 * ((k >> 3) & 1); }
@@ -186,7 +204,13 @@ __device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b,
 template <typename T, typename TC, int EPI>
 __device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_t col, float acc,
                                           float biasv) {
-  if constexpr (EPI == EPI_PARTIAL) {
+  if constexpr (EPI == EPI_GELU_DROP) {
+    const float u = acc + biasv, f = drop_factor(g, row, col);
+    ((T*)g.aux)[row * g.ldaux + col] = from_f32<T>(gelu_grad_f(u) * f);
+    ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(gelu_f(u) * f);
+  } else if constexpr (EPI == EPI_RESIDUAL_DROP) {
+    ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + (acc + biasv) * drop_factor(g, row, col);
+  } else if constexpr (EPI == EPI_PARTIAL) {
     ((float*)g.C)[blockIdx.z * g.split_stride + row * g.ldc + col] = acc;
   } else if constexpr (EPI == VITMI_EPI_STORE) {
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc + biasv);
@@ -292,7 +316,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
     const int64_t col = n0 + wn * (BN / WN) + j * 16 + cl;
     if (col >= g.N) continue;
     const float bv = (g.bias && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM &&
-                      EPI != VITMI_EPI_DGELU) ? g.bias[col] : 0.f;
+                      EPI != VITMI_EPI_DGELU) ? g.bias[col] : 0.f;   // (the *_DROP ones have bias)
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -326,12 +350,6 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
 #endif
 #ifndef VITMI_EPI_RB_F32
 #define VITMI_EPI_RB_F32 4
-#endif
-#ifndef VITMI_STAG_BAL
-#define VITMI_STAG_BAL 0
-#endif
-#ifndef VITMI_STAG_PRIO
-#define VITMI_STAG_PRIO 0
 #endif
 namespace g256 {
 // raw s_barrier that the compiler may not move memory operations across; DMA (vmcnt)
@@ -394,7 +412,7 @@ __device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf)
 // i.e. every lane owns 4 consecutive output COLUMNS of one row -> 8/16-byte vector stores
 // straight from registers.
 //
-// STAG = the staggered ("ping-pong") schedule.  A workgroup's waves w and w+4 share a SIMD.
+// The staggered ("ping-pong") K-loop.  A workgroup's waves w and w+4 share a SIMD.
 // Waves 4..7 run one barrier behind waves 0..3, and every phase is
 //     load section:  ds_read this phase's fragments, issue one half-tile LDS-DMA of the
 //                    next K-step, counted vmcnt;
@@ -412,12 +430,14 @@ __device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf)
 // Waits: vmcnt(8) at P0 retires B1(s), at P1 A1(s), at P3 A0(s+1),B0(s+1); each sits
 // before a barrier that the later reader passes, with one barrier of slack for the
 // staggered group.
-template <bool AK, bool BKM, int EPI, typename TC, bool STAG>
+template <bool AK, bool BKM, int EPI, typename TC>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   using namespace g256;
   // two DMA stages + the bias of the current and the next tile (fp32, double-buffered)
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048];
-  constexpr bool HAS_BIAS = EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL;
+  constexpr int EB = EpiOf<EPI>::base;         // public epilogue (the *_DROP ones extend one)
+  constexpr bool DROP = EpiOf<EPI>::drop;
+  constexpr bool HAS_BIAS = EB == VITMI_EPI_STORE || EB == VITMI_EPI_BIAS_GELU || EB == VITMI_EPI_RESIDUAL;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -491,9 +511,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   // phase's MFMAs: A sets X/Y (A0 halves in X, A1 in Y); B sets 0/1 alternate per K-step
   // (B0 of a K-step is read once, used by p0 AND p3; B1 lives in the other set).
   Frag<bf16> ax[4][2], ay[4][2], b0[2][2], b1[2][2];
-#if VITMI_STAG_BAL
-  Frag<bf16> b2[2][2];   // the other B0 set of the read-balanced staggered schedule
-#endif
   f32x4 acc[8][4];
   // Lane-constant LDS offsets (the swizzles depend only on the lane, not on the fragment):
   //  k-major image [128][64]: frag (tile j, ks) at line w*TW + 16j + l15, chunk (4ks+g)^s,
@@ -543,70 +560,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   } while (0)
 #define MMA4(MH, NH, AS, BS)                                                                    \
   do {                                                                                          \
-    if (!STAG || VITMI_STAG_PRIO == 0) __builtin_amdgcn_s_setprio(1);                          \
+    __builtin_amdgcn_s_setprio(1);                                                              \
     _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
     _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                            \
       acc[MH * 4 + mt][NH * 2 + nt] = mma(BS[nt][ks], AS[mt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
-    if (!STAG || VITMI_STAG_PRIO == 0) __builtin_amdgcn_s_setprio(0);                          \
+    __builtin_amdgcn_s_setprio(0);                                                              \
   } while (0)
-  // One K-step s (buffer buf = s & 1).  Entry: A0(s) in ax, B0(s) in BP (preloaded).
-  // Each half of buffer buf is refilled for step s+2 right after its last ds_read, so every
-  // DMA has ~2 K-steps to land:  p0 refills A0,B0 (read at p3 of s-1);  p3 refills B1,A1
-  // (read at p0/p1 of s).  Issue order per step: [A0,B0]@p0 [B1,A1]@p3, 2 instr per half.
-  // Waits: p0 needs B1(s),A1(s) -> leave the 8 younger instr of step s+1 in flight;
-  //        p3 needs A0(s+1),B0(s+1) -> leave B1,A1(s+1) [+ A0,B0(s+2)] in flight.
-  // lgkmcnt(0) before each barrier retires this wave's reads of the halves about to be
-  // refilled (WAR).  Leaves A0(s+1) in ax, B0(s+1) in BQ.
-#define KSTEP(BP, BQ)                                                                           \
-  do {                                                                                          \
-    /* p0 (A0,B0) */                                                                            \
-    if (has1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");                       \
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                            \
-    barrier();                                                                                  \
-    if (has2) { issue(s2a, s2b, s2t, buf, 0); issue(s2a, s2b, s2t, buf, 1); }                   \
-    RD_B(BQ, buf, 1);                                                                           \
-    MMA4(0, 0, ax, BP);                                                                         \
-    /* p1 (A0,B1) */                                                                            \
-    RD_A(ay, buf, 1);                                                                           \
-    MMA4(0, 1, ax, BQ);                                                                         \
-    /* p2 (A1,B1) */                                                                            \
-    MMA4(1, 1, ay, BQ);                                                                         \
-    /* p3 (A1,B0): refill B1/A1 for s+2, preload A0/B0 of s+1 from the other buffer */          \
-    if (has1) {                                                                                 \
-      if (has2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");                     \
-      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");                          \
-    } else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
-    barrier();                                                                                  \
-    if (has2) { issue(s2a, s2b, s2t, buf, 3); issue(s2a, s2b, s2t, buf, 2); }                   \
-    if (rd1) { RD_A(ax, buf ^ 1, 0); RD_B(BQ, buf ^ 1, 0); }                                    \
-    MMA4(1, 0, ay, BP);                                                                         \
-  } while (0)
-
-  // Shallow variant (1 K-step ahead): each phase stages one half of step s+1 into the
-  // other buffer (A0@p0 B0@p1 A1@p2 B1@p3); waits vmcnt(2) at p0, vmcnt(4) at p3.  Measured
-  // faster than KSTEP for layouts with m/n-major operands (transposed LDS reads).
-#define KSTEP1(BP, BQ)                                                                          \
-  do {                                                                                          \
-    if (has1) { issue(s1a, s1b, s1t, buf ^ 1, 0); asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); } \
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                       \
-    barrier();                                                                                  \
-    RD_B(BQ, buf, 1);                                                                           \
-    MMA4(0, 0, ax, BP);                                                                         \
-    if (has1) issue(s1a, s1b, s1t, buf ^ 1, 1);                                                 \
-    RD_A(ay, buf, 1);                                                                           \
-    MMA4(0, 1, ax, BQ);                                                                         \
-    if (has1) issue(s1a, s1b, s1t, buf ^ 1, 2);                                                 \
-    MMA4(1, 1, ay, BQ);                                                                         \
-    if (has1) {                                                                                 \
-      issue(s1a, s1b, s1t, buf ^ 1, 3);                                                         \
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                                          \
-      barrier();                                                                                \
-      if (rd1) { RD_A(ax, buf ^ 1, 0); RD_B(BQ, buf ^ 1, 0); }                                  \
-    }                                                                                           \
-    MMA4(1, 0, ay, BP);                                                                         \
-  } while (0)
-  constexpr bool DEEP = AK && BKM;
 
   int it = jx;
   if (it >= nseq) return;
@@ -616,38 +576,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   unit_of(tile, m0, n0, ks0, nku, zs);
   __amdgpu_buffer_rsrc_t ra = rsrc_a(m0, ks0), rb = rsrc_b(n0, ks0);
   int buf = 0;
-  if constexpr (STAG) {
-    // steps 0 and 1 of the first unit in the loop's issue order (nk >= 2 is a precondition)
-    issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 3); issue(ra, rb, 0, 0, 2);
-    issue(ra, rb, 1, 1, 0); issue(ra, rb, 1, 1, 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");      // A0(0), B0(0) landed
-    barrier();
-#if VITMI_STAG_BAL
-    RD_B(b0, 0, 0);                                        // B0(0): read at "P3" of step -1
-#endif
-    if (wm) barrier();                                     // waves 4..7 one barrier behind
-    // VITMI_STAG_PRIO 1: static priority for the staggered half (MI355X_MICROARCH.md "Two
-    // waves per SIMD" item 4) instead of per-MFMA-section priority flips
-    if (VITMI_STAG_PRIO == 1 && wm) __builtin_amdgcn_s_setprio(1);
-  } else {
-    // prologue: steps 0 and 1 of the first tile (nk >= 2 is a launch precondition)
-    if constexpr (DEEP) {
-      issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 3); issue(ra, rb, 0, 0, 2);
-      issue(ra, rb, 1, 1, 0); issue(ra, rb, 1, 1, 1); issue(ra, rb, 1, 1, 3); issue(ra, rb, 1, 1, 2);
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // A0(0), B0(0) landed
-    } else {
-      issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 2); issue(ra, rb, 0, 0, 3);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");    // A0(0), B0(0) landed
-    }
-    barrier();
-    RD_A(ax, 0, 0);
-    RD_B(b0, 0, 0);
-  }
+  // steps 0 and 1 of the first unit in the loop's issue order (nk >= 2 is a precondition)
+  issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 3); issue(ra, rb, 0, 0, 2);
+  issue(ra, rb, 1, 1, 0); issue(ra, rb, 1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");      // A0(0), B0(0) landed
+  barrier();
+  if (wm) barrier();                                     // waves 4..7 one barrier behind
 
   const int lc4 = 4 * (lane >> 4), lr = lane & 15;
   const __amdgpu_buffer_rsrc_t rbias = make_rsrc(g.bias, g.bias ? clamp_bytes(g.N * 4) : 0u);
   int tpar = 0;   // bias buffer of the current tile
-  [[maybe_unused]] bool ep_pending = false;   // an epilogue's stores are still in the vmcnt queue
+  bool ep_pending = false;   // an epilogue's stores are still in the vmcnt queue
   for (;;) {
     if constexpr (HAS_BIAS) {
       // bias[n0 .. n0+256) -> LDS by ONE LDS-DMA instruction of wave 0 (64 lanes x 16 B; the
@@ -670,18 +609,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // K-loop unrolled by 2 so the B register sets alternate statically
-#define STEP_SETUP(T)                                                                           \
-    const bool has1 = ((T) + 1 < nku) || has_next;                                              \
-    const bool has2 = ((T) + 2 < nku) || has_next;                                              \
-    const __amdgpu_buffer_rsrc_t s2a = ((T) + 2 < nku) ? ra : ran;                              \
-    const __amdgpu_buffer_rsrc_t s2b = ((T) + 2 < nku) ? rb : rbn;                              \
-    const int s2t = ((T) + 2 < nku) ? (T) + 2 : (T) + 2 - nku;                                  \
-    const __amdgpu_buffer_rsrc_t s1a = ((T) + 1 < nku) ? ra : ran;                              \
-    const __amdgpu_buffer_rsrc_t s1b = ((T) + 1 < nku) ? rb : rbn;                              \
-    const int s1t = ((T) + 1 < nku) ? (T) + 1 : 0;                                              \
-    const bool rd1 = (T) + 1 < nku;  /* next tile's step-0 fragments: read after the epilogue */
-    if constexpr (STAG) {
       // vmcnt counts of the first step after an epilogue: that epilogue issued >= 32 vector
       // memory ops per wave, all younger than the half-tiles this step waits for
       constexpr int EPW = 40;
@@ -693,46 +620,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         MMA4(MH, NH, AS, BS);                                                                   \
         barrier();                                                                              \
       } while (0)
-#if VITMI_STAG_BAL
-      // Read-balanced form: B0(t+1) is read at P3(t) into the other B0 register set (8/4/8/4
-      // ds_read_b128 per phase instead of 12/4/8/0), so A0(t+1),B0(t+1) are retired at P2.
-#define SSTEP(T, BC, BN)                                                                        \
-      do {                                                                                      \
-        const bool in1 = (T) + 1 < nku, in2 = (T) + 2 < nku;                                    \
-        const bool h1 = in1 || has_next, h2 = in2 || has_next;                                  \
-        const __amdgpu_buffer_rsrc_t a1 = in1 ? ra : ran, b1r = in1 ? rb : rbn;                 \
-        const __amdgpu_buffer_rsrc_t a2 = in2 ? ra : ran, b2r = in2 ? rb : rbn;                 \
-        const int t1 = in1 ? (T) + 1 : 0, t2 = in2 ? (T) + 2 : (T) + 2 - nku;                   \
-        const bool fst = (T) == 0 && ep_pending;                                                \
-        RD_A(ax, buf, 0);                                   /* P0 (A0,B0) */                    \
-        if (h1) { issue(a1, b1r, t1, buf ^ 1, 3); if (fst) WAITV(EPW); else WAITV(8); }         \
-        else WAITV(0);                                                                          \
-        COMPUTE(0, 0, ax, BC);                                                                  \
-        RD_B(b1, buf, 1);                                   /* P1 (A0,B1) */                    \
-        if (h1) { issue(a1, b1r, t1, buf ^ 1, 2); if (fst) WAITV(EPW); else WAITV(8); }         \
-        else WAITV(0);                                                                          \
-        COMPUTE(0, 1, ax, b1);                                                                  \
-        RD_A(ay, buf, 1);                                   /* P2 (A1,B1) */                    \
-        if (h2) { issue(a2, b2r, t2, buf, 0); if (fst) WAITV(EPW - 2); else WAITV(6); }         \
-        else WAITV(0);                                                                          \
-        COMPUTE(1, 1, ay, b1);                                                                  \
-        if (h1) RD_B(BN, buf ^ 1, 0);                       /* P3 (A1,B0) */                    \
-        if (h2) issue(a2, b2r, t2, buf, 1);                                                     \
-        COMPUTE(1, 0, ay, BC);                                                                  \
-        buf ^= 1;                                                                               \
-      } while (0)
-      for (int t = 0; t < nku; t += 2) {
-        SSTEP(t, b0, b2);
-        if (t + 1 < nku) SSTEP(t + 1, b2, b0);
-      }
-      if (nku & 1) {   // the next unit's first step expects its B0 in b0
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) b0[i][j] = b2[i][j];
-      }
-#undef SSTEP
-#else
       for (int t = 0; t < nku; ++t) {
         // step t+1 (B1, A1 still to issue, buffer buf^1) and step t+2 (A0, B0, buffer buf)
         const bool in1 = t + 1 < nku, in2 = t + 2 < nku;
@@ -774,26 +661,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         COMPUTE(1, 0, ay, b0);
         buf ^= 1;
       }
-#endif
 #undef COMPUTE
 #undef WAITV
-    } else {
-    for (int t = 0; t < nku; t += 2) {
-      {
-        STEP_SETUP(t)
-        if constexpr (DEEP) KSTEP(b0, b1); else KSTEP1(b0, b1);
-        buf ^= 1;
-      }
-      if (t + 1 < nku) {
-        STEP_SETUP(t + 1)
-        if constexpr (DEEP) KSTEP(b1, b0); else KSTEP1(b1, b0);
-        buf ^= 1;
-      }
-    }
-    }
-#undef STEP_SETUP
-#undef KSTEP
-#undef KSTEP1
 #undef MMA4
 
     if ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) {
@@ -814,8 +683,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     // serialising the epilogue.  C never aliases A/B here (host contract).  The range
     // check drops rows >= M; the row offset is a scalar per mi, the column an immediate.
     {
-      constexpr int CES = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM &&
-                                  EPI != VITMI_EPI_RESIDUAL ? 2 : 4;
+      constexpr int CES = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EB != VITMI_EPI_ACCUM &&
+                                  EB != VITMI_EPI_RESIDUAL ? 2 : 4;
       int64_t zoff = 0;
       if constexpr (EPI == EPI_PARTIAL) zoff = (int64_t)(blockIdx.z + zs) * g.split_stride;
       char* cbase = (char*)g.C + (zoff + m0 * g.ldc + n0) * CES;
@@ -840,21 +709,34 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           bv[ni] = *(const f32x4*)(smem + 2 * STAGE + tpar * 1024 + (wn * 64 + ni * 16 + lc4) * 4);
       }
       [[maybe_unused]] __amdgpu_buffer_rsrc_t ru = rc;
-      if constexpr (EPI == VITMI_EPI_BIAS_GELU)
+      if constexpr (EB == VITMI_EPI_BIAS_GELU)
         ru = make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand
       auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) {
         f32x4 v = acc[mi][ni] + bv[ni];
         const int soff = mi * rstride;
+        [[maybe_unused]] f32x4 df;   // dropout factors of the 4 columns
+        if constexpr (DROP) {
+          const uint32_t rk = drop_row_key(g.drop_seed, g.drop_site, (uint32_t)(m0 + wm * 128 + mi * 16 + lr));
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            df[e] = drop_hash(rk, (uint32_t)(colc[ni] + e)) >= g.drop_thresh ? g.drop_scale : 0.f;
+        }
+        if constexpr (EPI == EPI_RESIDUAL_DROP) v = v * df + ldv;
         if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM) v += ldv;
-        if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
+        if constexpr (EB == VITMI_EPI_BIAS_GELU) {
           bf16x4 u;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float cdf, pdf;
             gelu_fast_parts(v[e], cdf, pdf);
-            u[e] = (bf16)(cdf + v[e] * pdf);   // gelu'(x) = Phi(x) + x phi(x), kept for DGELU
+            float gp = cdf + v[e] * pdf;       // gelu'(x) = Phi(x) + x phi(x), kept for DGELU
             v[e] = v[e] * cdf;
+            if constexpr (DROP) {              // dropped: a = gelu(u) m/(1-p), aux = gelu'(u) m/(1-p)
+              gp *= df[e];
+              v[e] *= df[e];
+            }
+            u[e] = (bf16)gp;
           }
           const uint32_t uoff = cok[ni] ? (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldaux + wn * 64 + lc4) * 2)
                                         : 0x80000000u;
@@ -878,7 +760,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
                           "s"(soff), "i"(ni * 32) : "memory");
         }
       };
-      if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM || EPI == VITMI_EPI_DGELU) {
+      if constexpr (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM || EPI == VITMI_EPI_DGELU) {
         // epilogues that load: RB row groups at a time (all 4 column groups each; 64 VGPRs of
         // loaded operand per wait -- the fragment registers are free here), stored row by row
         // like the store-only epilogues below
@@ -892,7 +774,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             const int64_t row = min(m0 + wm * 128 + (RB * mp + h) * 16 + lr, g.M - 1);
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
-              if constexpr (EPI == VITMI_EPI_RESIDUAL) ld4[h][ni] = *(const f32x4*)(g.residual + row * g.ldr + colc[ni]);
+              if constexpr (EB == VITMI_EPI_RESIDUAL) ld4[h][ni] = *(const f32x4*)(g.residual + row * g.ldr + colc[ni]);
               if constexpr (EPI == VITMI_EPI_ACCUM) ld4[h][ni] = *(const f32x4*)((const float*)g.C + row * g.ldc + colc[ni]);
               if constexpr (EPI == VITMI_EPI_DGELU) ldu[h][ni] = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + colc[ni]);
             }
@@ -914,20 +796,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     tpar ^= 1;
     if (!has_next) break;
     it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
-    if constexpr (STAG) {
-      ep_pending = true;
-    } else {
-      // step-0 fragments of the next tile (its DMA landed before the last p3 barrier; nobody
-      // refills those halves before the next p0 barrier).  Read here rather than in the last
-      // K-step so the epilogue has the fragment registers to itself.
-      RD_A(ax, buf, 0);
-      RD_B(b0, buf, 0);
-    }
+    ep_pending = true;
   }
   // the leading group owes the staggered group its extra barrier: equal counts per wave
-  if constexpr (STAG) {
-    if (!wm) barrier();
-  }
+  if (!wm) barrier();
 #undef RD_A
 #undef RD_B
 #undef G256_MMA
@@ -972,7 +844,8 @@ __global__ __launch_bounds__(256) void gemm_tail_fixup_kernel(GemmArgs g, int nt
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (col + j >= g.N) break;
-      const float bv = (g.bias && (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_RESIDUAL))
+      constexpr int EB = EpiOf<EPI>::base;
+      const float bv = (g.bias && (EB == VITMI_EPI_STORE || EB == VITMI_EPI_BIAS_GELU || EB == VITMI_EPI_RESIDUAL))
                            ? g.bias[col + j] : 0.f;
       epi_store<T, TC, EPI>(g, row, col + j, a[j], bv);
     }
@@ -986,7 +859,6 @@ static int g_policy = 0;
 static int g_cus = 256;   // compute units of the current device (set on first use)
 
 static int g_grid_override = 0;   // VITMI_GEMM_GRID: 0 = persistent (one block per CU), -1 = one block per tile
-static int g_sched = 1;           // VITMI_GEMM_SCHED: 1 = staggered ping-pong K-loop, 0 = lockstep (A/B timing)
 static int g_fold = 1;            // VITMI_GEMM_FOLD: 1 = split-K folded into persistent units, 0 = gridDim.z
 static int g_split256 = 1;        // VITMI_GEMM_SPLIT256: 1 = few-tile split-K GEMMs on gemm256
 
@@ -994,7 +866,6 @@ static void init_cus() {
   static bool done = false;
   if (done) return;
   if (const char* e = getenv("VITMI_GEMM_GRID")) g_grid_override = atoi(e);
-  if (const char* e = getenv("VITMI_GEMM_SCHED")) g_sched = atoi(e);
   if (const char* e = getenv("VITMI_GEMM_FOLD")) g_fold = atoi(e);
   if (const char* e = getenv("VITMI_GEMM_SPLIT256")) g_split256 = atoi(e);
   int dev = 0;
@@ -1091,10 +962,7 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
         g.ksplit = ks;
         units = g.t_full + ntail * S;
       }
-      if (g_sched)
-        hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC, true>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
-      else
-        hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC, false>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
       if (units != nwg) {
         const int blocks = (ntail * 256 * 64 + 255) / 256;
@@ -1140,6 +1008,13 @@ static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits
       return launch_layout<T, VITMI_EPI_ACCUM, float>(ak, bk, g, splits, big, s);
     case EPI_PARTIAL:
       return launch_layout<T, EPI_PARTIAL, float>(ak, bk, g, splits, big, s);
+    case EPI_GELU_DROP:   // forward linear layers only: x and W both k-major
+      if (!(ak && bk)) break;
+      return cbf ? launch_t<T, true, true, EPI_GELU_DROP, bf16>(g, splits, big, s)
+                 : launch_t<T, true, true, EPI_GELU_DROP, float>(g, splits, big, s);
+    case EPI_RESIDUAL_DROP:
+      if (!(ak && bk)) break;
+      return launch_t<T, true, true, EPI_RESIDUAL_DROP, float>(g, splits, big, s);
   }
   return fail(VITMI_ERR_INVALID, "gemm: unknown epilogue %d", epi);
 }
@@ -1159,7 +1034,8 @@ static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K) {
 static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K, const void* A,
                      int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
                      int epi, const float* bias, void* aux, int64_t ldaux, const float* residual,
-                     int64_t ldr, void* ws, size_t ws_bytes, hipStream_t s, bool allow_split) {
+                     int64_t ldr, void* ws, size_t ws_bytes, hipStream_t s, bool allow_split,
+                     const GemmArgs* drop = nullptr) {
   VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "gemm: bad dtype %d", dtype);
   VITMI_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return VITMI_OK;
@@ -1173,10 +1049,11 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   VITMI_CHECK_ARG(ak ? lda >= K : lda >= M, "gemm: lda too small");
   VITMI_CHECK_ARG(bk ? ldb >= K : ldb >= N, "gemm: ldb too small");
   VITMI_CHECK_ARG(ldc >= N, "gemm: ldc too small");
-  if (epi == VITMI_EPI_BIAS_GELU || epi == VITMI_EPI_DGELU)
+  const int eb = epi_base(epi);
+  if (eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_DGELU)
     VITMI_CHECK_ARG(aux != nullptr && ldaux >= N, "gemm: epilogue needs aux");
-  if (epi == VITMI_EPI_RESIDUAL) VITMI_CHECK_ARG(residual != nullptr && ldr >= N, "gemm: residual missing");
-  if (epi == VITMI_EPI_RESIDUAL || epi == VITMI_EPI_ACCUM)
+  if (eb == VITMI_EPI_RESIDUAL) VITMI_CHECK_ARG(residual != nullptr && ldr >= N, "gemm: residual missing");
+  if (eb == VITMI_EPI_RESIDUAL || eb == VITMI_EPI_ACCUM)
     VITMI_CHECK_ARG(c_dtype == VITMI_F32, "gemm: residual/accum epilogues write fp32");
   // 32-bit buffer offsets: one block's panel must stay under 2 GiB
   VITMI_CHECK_ARG((ak ? 128 * lda : K * lda) * es < 0x7fffffffLL, "gemm: A panel exceeds 2 GiB");
@@ -1193,6 +1070,10 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.bias = bias; g.aux = aux; g.ldaux = ldaux;
   g.residual = residual; g.ldr = ldr;
+  if (drop) {
+    g.drop_seed = drop->drop_seed; g.drop_site = drop->drop_site;
+    g.drop_thresh = drop->drop_thresh; g.drop_scale = drop->drop_scale;
+  }
   int splits = 1;
   if (allow_split && epi == VITMI_EPI_ACCUM) splits = choose_splits(dtype, M, N, K);
   const int64_t ktiles = (K + BK - 1) / BK;
@@ -1284,6 +1165,21 @@ extern "C" int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, cons
                       epilogue == VITMI_EPI_RESIDUAL, "linear_fwd: bad epilogue %d", epilogue);
   return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, N, y_dtype, epilogue, bias, aux, N,
                    residual, N, workspace, ws_bytes, (hipStream_t)stream, false);
+}
+
+extern "C" int vitmi_linear_fwd_dropout(int dtype, int64_t M, int64_t N, int64_t K, const void* x,
+                                        const void* w, const float* bias, void* y, int y_dtype,
+                                        int epilogue, void* aux, const float* residual,
+                                        void* workspace, size_t ws_bytes, uint32_t seed,
+                                        uint32_t site, uint32_t thresh, float scale,
+                                        vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(epilogue == VITMI_EPI_BIAS_GELU || epilogue == VITMI_EPI_RESIDUAL,
+                  "linear_fwd_dropout: epilogue must be BIAS_GELU or RESIDUAL (got %d)", epilogue);
+  GemmArgs d{};
+  d.drop_seed = seed; d.drop_site = site; d.drop_thresh = thresh; d.drop_scale = scale;
+  const int epi = epilogue == VITMI_EPI_BIAS_GELU ? EPI_GELU_DROP : EPI_RESIDUAL_DROP;
+  return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, N, y_dtype, epi, bias, aux, N, residual, N,
+                   workspace, ws_bytes, (hipStream_t)stream, false, &d);
 }
 
 extern "C" size_t vitmi_linear_dgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {

@@ -22,6 +22,7 @@ I = ctypes.c_int
 L = ctypes.c_int64
 F = ctypes.c_float
 S = ctypes.c_size_t
+U = ctypes.c_uint32
 
 # name -> (restype, argtypes); mirrors include/vitmi.h one to one
 SIGNATURES = {
@@ -52,6 +53,9 @@ SIGNATURES = {
     "vitmi_head_bwd": (I, [I, I, I, P, P, L, P, P, P, P, P]),
     "vitmi_loss_fwd_bwd": (I, [I, I, I, P, P, P, P, P]),
     "vitmi_cast_f32_bf16": (I, [L, P, P, P]),
+    "vitmi_dropout_hash": (U, [U, U, U, U]),
+    "vitmi_linear_fwd_dropout": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P, S, U, U, U, F, P]),
+    "vitmi_dropout_apply": (I, [L, L, P, L, P, I, L, U, U, U, F, P]),
 }
 
 _lib = None

@@ -43,6 +43,9 @@ class ViTConfig:
     pos_embed: bool = True
     tie_norms: bool = False
     with_cls_token: bool = True
+    # dropout after the out-projection and in the MLP (models/CvT(Par).py:141,189,255,257;
+    # Keras default 0.1, training mode only).  0 = the parity / benchmark configuration.
+    drop_rate: float = 0.0
     # compute dtype of the device path: 'bf16' (MFMA bf16, fp32 accumulate and
     # fp32 residual stream) or 'fp32' (f32-input MFMA, exact fp32 products)
     dtype: str = "bf16"

@@ -112,6 +112,18 @@ def _join_side(dev: torch.device) -> None:
         torch.cuda.current_stream(side.device).wait_stream(side)
 
 
+def _drop_args(mod: nn.Module, rate: float, site0: int):
+    """(seed, rate, site0) for a training-mode forward with dropout, else None.  The seed is
+    ``mod.drop_seed`` when set (parity tests), otherwise drawn from torch's default CPU
+    generator, so ``torch.manual_seed`` makes the masks reproducible."""
+    if not mod.training or rate <= 0.0 or not torch.is_grad_enabled():
+        return None
+    seed = getattr(mod, "drop_seed", None)
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+    return (int(seed), float(rate), site0)
+
+
 def _grad(p: nn.Parameter) -> Tensor:
     if p.grad is None:
         p.grad = torch.zeros_like(p)
@@ -330,6 +342,8 @@ class Block(nn.Module):
         self.mlp = Mlp(dim, int(dim * mlp_ratio), dtype)
         self.dtype = dtype
         self.eps = eps
+        self.drop_rate = 0.0     # set by VisionTransformer / the caller (Keras default 0.1)
+        self.drop_seed: Optional[int] = None   # fixed seed (tests); None = drawn per forward
 
     @property
     def _norm2(self) -> LayerNorm:
@@ -337,16 +351,19 @@ class Block(nn.Module):
 
     def forward(self, x: Tensor, h: Optional[int] = None, w: Optional[int] = None) -> Tensor:
         _check_cuda(x)
-        return _BlockFn.apply(x, self, None, False, *self.parameters())
+        return _BlockFn.apply(x, self, None, False, _drop_args(self, self.drop_rate, 0), *self.parameters())
 
 
 class _BlockFn(torch.autograd.Function):
     """Fused block.  ``prev_fc2_bias``: the fc2 bias of the block feeding this one; its grad is
     colsum(d input), produced for free by this block's LN1 backward.  ``fc2_bias_done``: this
-    block's own fc2 bias grad was already accumulated by its consumer (next block or head)."""
+    block's own fc2 bias grad was already accumulated by its consumer (next block or head).
+    ``drop``: (seed, rate, site0) -> training-mode dropout (models/CvT(Par).py:189,255,257) at
+    sites site0 (out-projection), site0+1 (GELU output), site0+2 (fc2), fused into the GEMM
+    epilogues; the backward regenerates the masks (vitmi_dropout_apply)."""
 
     @staticmethod
-    def forward(ctx, x, blk, prev_fc2_bias, fc2_bias_done, *params):
+    def forward(ctx, x, blk, prev_fc2_bias, fc2_bias_done, drop, *params):
         T = ops.torch_dtype(blk.dtype)
         B, N, D = x.shape
         M = B * N
@@ -360,13 +377,17 @@ class _BlockFn(torch.autograd.Function):
         h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
         qkv = ops.linear_fwd(h1, wq, a_.qkv.bias, T)
         o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
-        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2)
+        dr = [None, None, None]
+        if drop is not None:
+            seed, rate, site0 = drop
+            dr = [(seed, site0 + j, rate) for j in range(3)]
+        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
         h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
-        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU)
-        out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
+        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1])
+        out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
         ctx.blk, ctx.shape = blk, (B, N, D)
-        ctx.prev_bias, ctx.bias_done = prev_fc2_bias, fc2_bias_done
+        ctx.prev_bias, ctx.bias_done, ctx.drop = prev_fc2_bias, fc2_bias_done, drop
         return out.view(B, N, D)
 
     @staticmethod
@@ -379,7 +400,14 @@ class _BlockFn(torch.autograd.Function):
         n1, n2 = blk.norm1, blk._norm2
         a_, mlp = blk.attn, blk.mlp
         g2 = dout.contiguous().view(M, D)
-        g2_lp = _take_lp(g2, T)
+        drop = ctx.drop
+        if drop is None:
+            g2_lp = _take_lp(g2, T)
+        else:
+            # the fc2 branch was dropped: its dgrad/wgrad/bias see g2 * mask / (1 - p)
+            _LP_STASH.pop(g2.data_ptr(), None)
+            seed, rate, site0 = drop
+            g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
         # MLP branch
         dev = g2.device
         du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u)
@@ -391,10 +419,16 @@ class _BlockFn(torch.autograd.Function):
             ops.bias_grad(du, _grad(mlp.fc1.bias))
         dh2 = ops.linear_dgrad(du, w1, T)
         # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
-        dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias),
-                                        dres=g2, lp_dtype=lpT, dxsum=_grad(a_.proj.bias))
-        if dx1_lp is None:
-            dx1_lp = dx1
+        if drop is None:
+            dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias),
+                                            dres=g2, lp_dtype=lpT, dxsum=_grad(a_.proj.bias))
+            if dx1_lp is None:
+                dx1_lp = dx1
+        else:
+            dx1, _ = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias),
+                                       dres=g2, lp_dtype=None)
+            dx1_lp = ops.dropout_apply(dx1, seed, site0, rate, T)
+            ops.bias_grad(dx1_lp, _grad(a_.proj.bias))
         # attention branch
         do = ops.linear_dgrad(dx1_lp, wo, T)
         with _OnSide(dev, dx1_lp, o):
@@ -407,7 +441,8 @@ class _BlockFn(torch.autograd.Function):
         dh1 = ops.linear_dgrad(dqkv, wq, T)
         prev = ctx.prev_bias
         dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
-                                      dres=dx1, lp_dtype=lpT, dxsum=_grad(prev) if prev is not None else None)
+                                      dres=dx1, lp_dtype=lpT if drop is None else None,
+                                      dxsum=_grad(prev) if prev is not None else None)
         _stash(dx, dx_lp)
         hook = getattr(blk, "_grad_ready_hook", None)
         if hook is not None:
@@ -516,7 +551,7 @@ class _HeadFn(torch.autograd.Function):
         dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), _grad(head.weight),
                           _grad(head.bias) if head.bias is not None else None)
         dx = torch.zeros_like(x)
-        last_fc2_bias = model.blocks[-1].mlp.fc2.bias if len(model.blocks) else None
+        last_fc2_bias = model.blocks[-1].mlp.fc2.bias if len(model.blocks) and model._fc2_bias_fused else None
         ops.layernorm_bwd(dy, x[:, 0], mean, rstd, norm.weight, _grad(norm.weight), _grad(norm.bias),
                           dx=dx[:, 0], dxsum=_grad(last_fc2_bias) if last_fc2_bias is not None else None)
         hook = getattr(model, "_head_ready_hook", None)
@@ -632,6 +667,8 @@ class VisionTransformer(nn.Module):
         self.norm = LayerNorm(D, cfg.ln_eps)
         self.head = Linear(D, cfg.num_classes)
         self._arena: Optional[ParamArena] = None
+        self.drop_seed: Optional[int] = None   # fixed dropout seed (tests); None = drawn per forward
+        self._fc2_bias_fused = True
         self.reset_parameters()
 
     # -- init: trunc_normal(.02) weights, zero biases, LN (1, 0)  (old_codes/MS_CvT.py:437-454)
@@ -691,9 +728,13 @@ class VisionTransformer(nn.Module):
         t = _EmbedFn.apply(x, pe, self.cls_token, self.pos_embed, *pe.parameters())
         # bias-grad fusion: block i's LN1 backward produces colsum(d input) = the fc2 bias grad
         # of block i-1; the head's LN backward does it for the last block.
+        drop = _drop_args(self, self.cfg.drop_rate, 0)
+        # with dropout the fc2/proj bias grads are column sums of MASKED gradients: no fusion
+        self._fc2_bias_fused = drop is None
         for i, blk in enumerate(self.blocks):
-            prev_bias = self.blocks[i - 1].mlp.fc2.bias if i > 0 else None
-            t = _BlockFn.apply(t, blk, prev_bias, True, *blk.parameters())
+            prev_bias = self.blocks[i - 1].mlp.fc2.bias if i > 0 and drop is None else None
+            d = None if drop is None else (drop[0], drop[1], 3 * i)
+            t = _BlockFn.apply(t, blk, prev_bias, drop is None, d, *blk.parameters())
         return t
 
     def forward(self, x: Tensor) -> Tensor:

@@ -69,10 +69,17 @@ def _rows(t: Tensor) -> Tuple[int, int]:
 
 
 # ---------------------------------------------------------------- GEMM
+def dropout_params(p: float):
+    """(thresh, scale) of rate p: keep iff vitmi_dropout_hash >= thresh (include/vitmi.h)."""
+    return min(int(round(p * 2.0 ** 32)), 0xFFFFFFFF), 1.0 / (1.0 - p)
+
+
 def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dtype,
-               epilogue: int = EPI_STORE, residual: Optional[Tensor] = None):
+               epilogue: int = EPI_STORE, residual: Optional[Tensor] = None, dropout=None):
     """y = x W^T + b (+GELU, +residual).  x [M,K], w [N,K] (same dtype).  Returns y
-    (and gelu'(pre-activation), the saved GELU derivative, for EPI_BIAS_GELU)."""
+    (and gelu'(pre-activation), the saved GELU derivative, for EPI_BIAS_GELU).
+    ``dropout`` = (seed, site, rate) fuses the dropout of the GELU output / of the branch
+    before the residual add into the epilogue (vitmi_linear_fwd_dropout)."""
     assert x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N = w.shape[0]
@@ -89,12 +96,31 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
         e0.record()
     nws = lib().vitmi_linear_fwd_workspace_size(dt(x.dtype), M, N, K)
     ws = _ws(nws, x) if nws else None
-    check(lib().vitmi_linear_fwd(dt(x.dtype), M, N, K, _p(x), _p(w), _p(bias), _p(y), dt(out_dtype),
-                                 epilogue, _p(aux), _p(residual), _p(ws), nws, _s()), "linear_fwd")
+    if dropout is not None and dropout[2] > 0:
+        seed, site, rate = dropout
+        thresh, scale = dropout_params(rate)
+        check(lib().vitmi_linear_fwd_dropout(dt(x.dtype), M, N, K, _p(x), _p(w), _p(bias), _p(y),
+                                             dt(out_dtype), epilogue, _p(aux), _p(residual), _p(ws), nws,
+                                             seed & 0xFFFFFFFF, site, thresh, scale, _s()), "linear_fwd_dropout")
+    else:
+        check(lib().vitmi_linear_fwd(dt(x.dtype), M, N, K, _p(x), _p(w), _p(bias), _p(y), dt(out_dtype),
+                                     epilogue, _p(aux), _p(residual), _p(ws), nws, _s()), "linear_fwd")
     if probe:
         e1.record()
         _PROBE["events"].append((e0, e1))
     return (y, aux) if epilogue == EPI_BIAS_GELU else y
+
+
+def dropout_apply(x: Tensor, seed: int, site: int, rate: float, out_dtype: torch.dtype) -> Tensor:
+    """x (fp32, rows x C) * keep(seed, site, row, col) / (1 - rate), in out_dtype: the masked
+    gradient of a dropped branch (the forward applied the same mask in a GEMM epilogue)."""
+    M, ldx = _rows(x)
+    N = x.shape[-1]
+    y = torch.empty(M, N, dtype=out_dtype, device=x.device)
+    thresh, scale = dropout_params(rate)
+    check(lib().vitmi_dropout_apply(M, N, _p(x), ldx, _p(y), dt(out_dtype), N, seed & 0xFFFFFFFF, site,
+                                    thresh, scale, _s()), "dropout_apply")
+    return y
 
 
 def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = EPI_STORE,
