@@ -98,8 +98,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < M; row += (int64_t)gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
-    f32x4 xh[NV], gy[NV];
+    f32x4 xh[NV], gy[NV], rv[NV];
     float s1 = 0.f, s2 = 0.f;
+    // the residual gradient is loaded with x and dy: one memory round trip per row
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 4;
+      rv[i] = (dres && c < D) ? *(const f32x4*)(dres + row * ldres + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 4;
@@ -123,8 +129,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 4;
       if (c < D) {
-        f32x4 o = (gy[i] - c1 - xh[i] * c2) * rs;
-        if (dres) o += *(const f32x4*)(dres + row * ldres + c);
+        const f32x4 o = (gy[i] - c1 - xh[i] * c2) * rs + rv[i];
         ds[i] += o;
         *(f32x4*)(dx + row * lddx + c) = o;
         if (LP) store4<bf16>(dx_lp + row * lddx_lp + c, o);
@@ -180,9 +185,12 @@ __global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict_
   }
 }
 
+#ifndef VITMI_LN_BWD_BLOCKS
+#define VITMI_LN_BWD_BLOCKS 512
+#endif
 static int ln_blocks_bwd(int64_t M) {
   int64_t g = (M + 3) / 4;
-  return (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
+  return (int)(g < VITMI_LN_BWD_BLOCKS ? (g < 1 ? 1 : g) : VITMI_LN_BWD_BLOCKS);
 }
 
 template <int NV>
