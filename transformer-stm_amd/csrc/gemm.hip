@@ -586,7 +586,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   const int lc4 = 4 * (lane >> 4), lr = lane & 15;
   const __amdgpu_buffer_rsrc_t rbias = make_rsrc(g.bias, g.bias ? clamp_bytes(g.N * 4) : 0u);
   int tpar = 0;   // bias buffer of the current tile
-  bool ep_pending = false;   // an epilogue's stores are still in the vmcnt queue
+  // vector-memory ops the previous unit's epilogue issued (0: none yet).  Those are younger
+  // than the half-tiles the first K-step waits for, so its counts may grow by that many.
+  int ep_ops = 0;
   for (;;) {
     if constexpr (HAS_BIAS) {
       // bias[n0 .. n0+256) -> LDS by ONE LDS-DMA instruction of wave 0 (64 lanes x 16 B; the
@@ -609,9 +611,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-      // vmcnt counts of the first step after an epilogue: that epilogue issued >= 32 vector
-      // memory ops per wave, all younger than the half-tiles this step waits for
-      constexpr int EPW = 40;
+      // vmcnt counts of the first step after an epilogue that issued S vector-memory ops:
+      // 8 + S (capped at the counter's 63): S = 32 for store-only and split-partial epilogues,
+      // 64 for GELU (two stores per fragment) and the loading epilogues (loads + stores)
 #define WAITV(N) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory")
 #define COMPUTE(MH, NH, AS, BS)                                                                 \
       do {                                                                                      \
@@ -627,13 +629,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         const __amdgpu_buffer_rsrc_t a1 = in1 ? ra : ran, b1r = in1 ? rb : rbn;
         const __amdgpu_buffer_rsrc_t a2 = in2 ? ra : ran, b2r = in2 ? rb : rbn;
         const int t1 = in1 ? t + 1 : 0, t2 = in2 ? t + 2 : t + 2 - nku;
-        const bool fst = t == 0 && ep_pending;
+        const int fst = t == 0 ? ep_ops : 0;
         // P0 (A0,B0): DMA B1(t+1); retire B1(t)
         RD_A(ax, buf, 0);
         RD_B(b0, buf, 0);
         if (h1) {
           issue(a1, b1r, t1, buf ^ 1, 3);
-          if (fst) WAITV(EPW); else WAITV(8);
+          if (fst >= 64) WAITV(63); else if (fst) WAITV(40); else WAITV(8);
         } else {
           WAITV(0);
         }
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         RD_B(b1, buf, 1);
         if (h1) {
           issue(a1, b1r, t1, buf ^ 1, 2);
-          if (fst) WAITV(EPW); else WAITV(8);
+          if (fst >= 64) WAITV(63); else if (fst) WAITV(40); else WAITV(8);
         } else {
           WAITV(0);
         }
@@ -654,7 +656,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         // P3 (A1,B0): DMA B0(t+2); retire A0(t+1), B0(t+1)
         if (h2) {
           issue(a2, b2r, t2, buf, 1);
-          if (fst) WAITV(EPW); else WAITV(8);
+          if (fst >= 64) WAITV(63); else if (fst) WAITV(40); else WAITV(8);
         } else {
           WAITV(0);
         }
@@ -794,9 +796,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       }
     }
     tpar ^= 1;
+    // the epilogue just issued: 32 stores (store-only, split partials) or 64 ops
+    ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32
+             : (EB == VITMI_EPI_BIAS_GELU || EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ||
+                EPI == VITMI_EPI_DGELU) ? 64 : 32;
     if (!has_next) break;
     it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
-    ep_pending = true;
   }
   // the leading group owes the staggered group its extra barrier: equal counts per wave
   if (!wm) barrier();
