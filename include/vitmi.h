@@ -178,6 +178,46 @@ int vitmi_dropout_apply(int64_t M, int64_t N, const float* x, int64_t ldx, void*
                         int64_t ldy, uint32_t seed, uint32_t site, uint32_t thresh, float scale,
                         vitmi_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * CvT stages (the reference's actual SLS model, models/CvT(Par).py:66-72).
+ *
+ * ConvEmbed = layers.Conv2D(D, kernel=k, strides=s, padding='same') (:203-212) as a GEMM over
+ * patches.  TF 'same': Ho = ceil(H/s), pad_total = max((Ho-1)s + k - H, 0), pad_before =
+ * pad_total/2 (vitmi_conv_same_geometry).  Input rows are NHWC tokens: image b, pixel (h, w)
+ * is row b*img_stride + row_off + h*W + w of x [..][ldx] (fp32).  Patch rows [B*Ho*Wo][Kp]
+ * (dtype) in column order (kh, kw, c) -- the Keras kernel [kh][kw][Cin][Cout] flattened --
+ * zero-padded to Kp (a multiple of the GEMM's K step).
+ */
+int vitmi_conv_same_geometry(int H, int W, int kh, int kw, int s, int* Ho, int* Wo, int* pad_top, int* pad_left);
+/* explicit geometry (pad_top/pad_left/Ho/Wo): TF 'same' from vitmi_conv_same_geometry, or the
+ * symmetric padding of torch Conv2d (old_codes/MS_CvT.py PATCH_PADDING) */
+int vitmi_conv_im2col(int dtype, int B, int H, int W, int C, int kh, int kw, int s, int pad_top, int pad_left,
+                      int Ho, int Wo, const float* x, int64_t ldx, int64_t img_stride, int64_t row_off,
+                      void* patches, int Kp, vitmi_stream_t stream);
+/* adjoint of im2col: dx (f32, rows as x) (+)= the sum over every window reading a pixel (C % 4 == 0) */
+int vitmi_conv_col2im(int dtype, int B, int H, int W, int C, int kh, int kw, int s, int pad_top, int pad_left,
+                      int Ho, int Wo, const void* dpatches, int Kp, float* dx, int64_t ldx, int64_t img_stride,
+                      int64_t row_off, int accumulate, vitmi_stream_t stream);
+/* Projection(method='dw_bn') (:83-112): z = DepthwiseConv2D(3, 'same', no bias)(x) [3][3][C],
+ * y = BatchNormalization: training != 0 -> batch statistics over B*H*W (biased variance) and the
+ * moving statistics m <- momentum m + (1-momentum) stat (NULL to skip); training == 0 -> the
+ * moving statistics normalise (Keras inference).  x/dx rows as above (cls row skipped via
+ * x_off), y rows b*y_img + y_off + hw of y [..][ldy] (y_dtype).  z [B*H*W][C], mean/rstd [C]
+ * are saved for the backward.  C % 4 == 0 and 1024 % C == 0. */
+size_t vitmi_dwconv_bn_workspace_size(int B, int H, int W, int C);
+int vitmi_dwconv_bn_fwd(int B, int H, int W, int C, const float* x, int64_t ldx, int64_t x_img, int64_t x_off,
+                        const float* w, const float* gamma, const float* beta, float eps, float momentum,
+                        int training, float* run_mean, float* run_var, float* z, float* mean, float* rstd, void* y,
+                        int y_dtype,
+                        int64_t ldy, int64_t y_img, int64_t y_off, void* workspace, size_t ws_bytes,
+                        vitmi_stream_t stream);
+/* dx += d/dx, dw/dgamma/dbeta += (f32) from dy (rows as y, dy_dtype) */
+int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, int dy_dtype, int64_t lddy, int64_t dy_img,
+                        int64_t dy_off, const float* x, int64_t ldx, int64_t x_img, int64_t x_off, const float* w,
+                        const float* gamma, const float* z, const float* mean, const float* rstd, float* dx,
+                        float* dw, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
+                        vitmi_stream_t stream);
+
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
 

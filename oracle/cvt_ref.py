@@ -1,0 +1,251 @@
+"""ORACLE — CPU restatement of the reference's CvT stages (TEST INFRASTRUCTURE ONLY).
+
+Only ``tests/`` use this module; the product package never imports it.
+
+SURVEY §8f row 1: the convolutional model the reference actually trains on its SLS images,
+``create_cvt_model`` (``models/CvT(Par).py:292-354``) with the stage spec ``:66-72``:
+
+=======  ==========================================  =============================
+stage    ConvEmbed (Conv2D 'same', ``:194-217``)      ConvTransformerBlock (``:231-289``)
+=======  ==========================================  =============================
+1        D=64,  k7 s4                                 1 head,  dw_bn q/k/v, no cls
+2        D=128, k3 s2                                 2 heads, dw_bn, no cls
+3        D=256, k3 s2                                 4 heads, dw_bn, cls token
+=======  ==========================================  =============================
+
+* ConvEmbed: ``layers.Conv2D(D, k, s, padding='same')`` (TF asymmetric 'same' padding); the
+  LayerNorm it means to apply is never built (``norm_layer == "LayerNormalization"`` compares
+  a class to a string, ``:209``) -> ``embed_norm`` knob, True for MS_CvT (``old_codes/MS_CvT.py:358``).
+* ``Projection('dw_bn')`` (``:83-112``): DepthwiseConv2D(3, stride 1, 'same', no bias) +
+  BatchNormalization (training: batch statistics; Keras eps 1e-3), applied to the spatial
+  tokens of q, k and v; the cls token bypasses it (``:146-150,164-176``).
+* ``ConvAttention.call`` (``:144-191``): q/k/v Dense(D) then MultiHeadAttention(q, v, k) whose
+  own query/key/value EinsumDense projections compose with them into one linear each (the
+  build holds the composition ``proj_{q,k,v}``), softmax(QK^T / sqrt(D/H)) V, output Dense
+  composed with ``self.proj`` into ``proj``.
+* block: ``x += Attn(LN1(x)); x += MLP(LN1(x))`` with the SAME norm1 used twice (``:248,272,278``).
+* head: LN(cls) (eps 1e-6, ``:328``) -> Dense(num_classes).  The reference concatenates a
+  process-parameter MLP before its Dense(1) (``:343-350``, SURVEY §8f row 2, not built yet).
+
+Knobs (``CvTConfig``) cover MS_CvT's semantics too (``old_codes/MS_CvT.py``: symmetric conv
+padding, embed LayerNorm, attention scale 1/sqrt(D) ``:100``, no q/k/v bias ``:82``, BN eps 1e-5,
+separate norm1/norm2), which is how ``tests/golden/mscvt_cvt_dwbn.npz`` -- generated from the
+reference's own module -- pins this restatement.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+Tensor = torch.Tensor
+
+
+@dataclass
+class CvTStage:
+    embed_dim: int
+    patch_size: int
+    stride: int
+    num_heads: int
+    with_cls_token: bool = False
+    depth: int = 1
+    padding: Optional[int] = None    # None: TF 'same'; an int: symmetric (MS_CvT PATCH_PADDING)
+
+
+def keras_spec() -> List[CvTStage]:
+    """models/CvT(Par).py:66-72 (cls_token_switch = True, :28)."""
+    return [CvTStage(64, 7, 4, 1), CvTStage(128, 3, 2, 2), CvTStage(256, 3, 2, 4, with_cls_token=True)]
+
+
+@dataclass
+class CvTConfig:
+    img_size: int = 128               # SLS images resized to 128x128 grayscale (:413-423)
+    in_chans: int = 1
+    num_classes: int = 1              # the reference regresses one value (MSE, :464-466)
+    stages: List[CvTStage] = field(default_factory=keras_spec)
+    mlp_ratio: float = 4.0
+    attn_scale: str = "head"          # 'head' 1/sqrt(D/H) Keras; 'dim' 1/sqrt(D) MS_CvT
+    ln_eps: float = 1e-6
+    bn_eps: float = 1e-3              # Keras BatchNormalization default; torch 1e-5
+    bn_momentum: float = 0.99         # Keras convention (running <- m running + (1-m) batch)
+    qkv_bias: bool = True
+    tie_norms: bool = True
+    embed_norm: bool = False
+    dtype: str = "bf16"
+
+    def replace(self, **kw) -> "CvTConfig":
+        return dataclasses.replace(self, **kw)
+
+
+def conv_geometry(H: int, k: int, s: int, padding: Optional[int]) -> Tuple[int, int, int]:
+    """(Ho, pad_before, pad_after): TF 'same' when padding is None, else symmetric."""
+    if padding is None:
+        Ho = -(-H // s)
+        tot = max((Ho - 1) * s + k - H, 0)
+        return Ho, tot // 2, tot - tot // 2
+    Ho = (H + 2 * padding - k) // s + 1
+    return Ho, padding, padding
+
+
+def param_shapes(cfg: CvTConfig) -> Dict[str, tuple]:
+    s = {}
+    cin = cfg.in_chans
+    for i, st in enumerate(cfg.stages):
+        D, k = st.embed_dim, st.patch_size
+        p = f"stage{i}."
+        s[p + "embed.weight"] = (D, cin, k, k)        # torch conv layout
+        s[p + "embed.bias"] = (D,)
+        if cfg.embed_norm:
+            s[p + "embed.norm.weight"] = (D,)
+            s[p + "embed.norm.bias"] = (D,)
+        if st.with_cls_token:
+            s[p + "cls_token"] = (1, 1, D)
+        for j in range(st.depth):
+            b = f"{p}blocks.{j}."
+            s[b + "norm1.weight"] = (D,)
+            s[b + "norm1.bias"] = (D,)
+            for c in "qkv":
+                s[b + f"attn.conv_proj_{c}.weight"] = (D, 1, 3, 3)
+                s[b + f"attn.conv_proj_{c}.bn.weight"] = (D,)
+                s[b + f"attn.conv_proj_{c}.bn.bias"] = (D,)
+                s[b + f"attn.proj_{c}.weight"] = (D, D)
+                if cfg.qkv_bias:
+                    s[b + f"attn.proj_{c}.bias"] = (D,)
+            s[b + "attn.proj.weight"] = (D, D)
+            s[b + "attn.proj.bias"] = (D,)
+            if not cfg.tie_norms:
+                s[b + "norm2.weight"] = (D,)
+                s[b + "norm2.bias"] = (D,)
+            Fh = int(D * cfg.mlp_ratio)
+            s[b + "mlp.fc1.weight"] = (Fh, D)
+            s[b + "mlp.fc1.bias"] = (Fh,)
+            s[b + "mlp.fc2.weight"] = (D, Fh)
+            s[b + "mlp.fc2.bias"] = (D,)
+        cin = D
+    D = cfg.stages[-1].embed_dim
+    s["norm.weight"] = (D,)
+    s["norm.bias"] = (D,)
+    s["head.weight"] = (cfg.num_classes, D)
+    s["head.bias"] = (cfg.num_classes,)
+    return s
+
+
+def init_params(cfg: CvTConfig, seed: int = 0) -> Dict[str, Tensor]:
+    """Random parameters for parity runs (every gamma/beta/bias random)."""
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    for name, shape in param_shapes(cfg).items():
+        leaf = name.rsplit(".", 1)[-1]
+        parent = name.split(".")[-2]
+        if parent in ("norm1", "norm2", "norm", "bn"):
+            t = (1.0 + 0.1 * torch.randn(shape, generator=g)) if leaf == "weight" else 0.1 * torch.randn(shape, generator=g)
+        elif leaf == "bias":
+            t = 0.02 * torch.randn(shape, generator=g)
+        elif "conv_proj" in name:
+            t = 0.2 * torch.randn(shape, generator=g)
+        elif leaf == "cls_token":
+            t = 0.02 * torch.randn(shape, generator=g)
+        else:
+            fan_in = shape[1] * (shape[2] * shape[3] if len(shape) == 4 else 1)
+            t = torch.randn(shape, generator=g) * (1.0 / fan_in) ** 0.5
+        out[name] = t.float().contiguous()
+    return out
+
+
+def conv_embed(x: Tensor, w: Tensor, b: Tensor, st: CvTStage) -> Tensor:
+    """layers.Conv2D(D, k, s, padding='same') (models/CvT(Par).py:203-212). x NCHW -> NCHW."""
+    k, s = st.patch_size, st.stride
+    _, pt, pb = conv_geometry(x.shape[2], k, s, st.padding)
+    _, pl, pr = conv_geometry(x.shape[3], k, s, st.padding)
+    return F.conv2d(F.pad(x, (pl, pr, pt, pb)), w, b, stride=s)
+
+
+def dw_bn(x: Tensor, w: Tensor, gamma: Tensor, beta: Tensor, eps: float) -> Tensor:
+    """Projection('dw_bn') (models/CvT(Par).py:92-94,104-106): x NCHW, training-mode BN."""
+    z = F.conv2d(x, w, None, stride=1, padding=1, groups=x.shape[1])
+    return F.batch_norm(z, None, None, gamma, beta, training=True, eps=eps)
+
+
+def block(x: Tensor, hw: Tuple[int, int], p: Dict[str, Tensor], pre: str, cfg: CvTConfig, st: CvTStage) -> Tensor:
+    """ConvTransformerBlock.call (models/CvT(Par).py:261-289) on tokens [B, N, D]."""
+    B, N, D = x.shape
+    H, W = hw
+    Hh = st.num_heads
+    dh = D // Hh
+    n1w, n1b = p[pre + "norm1.weight"], p[pre + "norm1.bias"]
+    n2w, n2b = (n1w, n1b) if cfg.tie_norms else (p[pre + "norm2.weight"], p[pre + "norm2.bias"])
+    h = F.layer_norm(x, (D,), n1w, n1b, cfg.ln_eps)
+    cls, sp = (h[:, :1], h[:, 1:]) if st.with_cls_token else (None, h)
+    img = sp.transpose(1, 2).reshape(B, D, H, W)
+    proj = []
+    for c in "qkv":
+        a = pre + f"attn.conv_proj_{c}."
+        t = dw_bn(img, p[a + "weight"], p[a + "bn.weight"], p[a + "bn.bias"], cfg.bn_eps)
+        t = t.flatten(2).transpose(1, 2)
+        if cls is not None:
+            t = torch.cat([cls, t], dim=1)
+        proj.append(F.linear(t, p[pre + f"attn.proj_{c}.weight"], p.get(pre + f"attn.proj_{c}.bias")))
+    q, k, v = (t.reshape(B, N, Hh, dh).transpose(1, 2) for t in proj)
+    scale = dh ** -0.5 if cfg.attn_scale == "head" else D ** -0.5
+    a = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * scale, dim=-1)
+    o = torch.matmul(a, v).transpose(1, 2).reshape(B, N, D)
+    x = x + F.linear(o, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"])
+    y = F.layer_norm(x, (D,), n2w, n2b, cfg.ln_eps)
+    y = F.linear(F.gelu(F.linear(y, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])),
+                 p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+    return x + y
+
+
+def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig) -> Tensor:
+    """Stages 1..S; returns LN(final cls token) [B, D] (the token mean without cls, :337-340)."""
+    x = img
+    tok = None
+    t = None
+    for i, st in enumerate(cfg.stages):
+        pre = f"stage{i}."
+        x = conv_embed(x, p[pre + "embed.weight"], p[pre + "embed.bias"], st)
+        B, D, H, W = x.shape
+        t = x.flatten(2).transpose(1, 2)
+        if cfg.embed_norm:
+            t = F.layer_norm(t, (D,), p[pre + "embed.norm.weight"], p[pre + "embed.norm.bias"], cfg.ln_eps)
+        if st.with_cls_token:
+            t = torch.cat([p[pre + "cls_token"].expand(B, 1, D), t], dim=1)
+        for j in range(st.depth):
+            t = block(t, (H, W), p, f"{pre}blocks.{j}.", cfg, st)
+        if st.with_cls_token:
+            tok, t = t[:, 0], t[:, 1:]
+        x = t.transpose(1, 2).reshape(B, D, H, W)
+    if tok is None:
+        return F.layer_norm(t, (t.shape[-1],), p["norm.weight"], p["norm.bias"], cfg.ln_eps).mean(dim=1)
+    return F.layer_norm(tok, (tok.shape[-1],), p["norm.weight"], p["norm.bias"], cfg.ln_eps)
+
+
+def forward(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig) -> Tensor:
+    return F.linear(forward_features(img, p, cfg), p["head.weight"], p["head.bias"])
+
+
+def loss_fn(logits: Tensor, target: Tensor, num_classes: int) -> Tensor:
+    if num_classes == 1:
+        return F.mse_loss(logits.squeeze(-1), target.float())
+    return F.cross_entropy(logits, target.long())
+
+
+def forward_backward(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg: CvTConfig):
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+    logits = forward(img, leaves, cfg)
+    loss = loss_fn(logits, target, cfg.num_classes)
+    loss.backward()
+    return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}
+
+
+def synthetic_batch(cfg: CvTConfig, batch: int, seed: int = 1234):
+    g = torch.Generator().manual_seed(seed)
+    img = torch.rand(batch, cfg.in_chans, cfg.img_size, cfg.img_size, generator=g)
+    if cfg.num_classes == 1:
+        tgt = torch.randn(batch, generator=g)
+    else:
+        tgt = torch.randint(0, cfg.num_classes, (batch,), generator=g)
+    return img, tgt

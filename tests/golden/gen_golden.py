@@ -143,6 +143,40 @@ def gen_mscvt():
     save(os.path.join(HERE, "mscvt_vit_stage.npz"), img, tgt, params, logits, loss, grads)
 
 
+def gen_mscvt_cvt():
+    """``mscvt_cvt_dwbn.npz``: MS_CvT's ConvolutionalVisionTransformer with the dw_bn q/k/v
+    projection (``old_codes/MS_CvT.py:124-144``: depthwise 3x3 + BatchNorm2d, training mode)
+    in two stages shaped like the reference's Keras spec (``models/CvT(Par).py:66-72``):
+    ConvEmbed k7 s4 (D 64, 1 head) and k3 s2 (D 128, 2 heads, cls token), 1-channel 32x32
+    input.  Pins ``oracle/cvt_ref.py`` in its MS_CvT knob setting."""
+    ms = load_mscvt()
+    spec = {
+        "NUM_STAGES": 2, "PATCH_SIZE": [7, 3], "PATCH_STRIDE": [4, 2], "PATCH_PADDING": [2, 1],
+        "DIM_EMBED": [64, 128], "DEPTH": [1, 1], "NUM_HEADS": [1, 2], "MLP_RATIO": [4.0, 4.0],
+        "QKV_BIAS": [False, False], "DROP_RATE": [0.0, 0.0], "ATTN_DROP_RATE": [0.0, 0.0],
+        "DROP_PATH_RATE": [0.0, 0.0], "CLS_TOKEN": [False, True], "QKV_PROJ_METHOD": ["dw_bn", "dw_bn"],
+        "KERNEL_QKV": [3, 3], "PADDING_Q": [1, 1], "PADDING_KV": [1, 1], "STRIDE_KV": [1, 1], "STRIDE_Q": [1, 1],
+    }
+    torch.manual_seed(0)
+    model = ms.ConvolutionalVisionTransformer(in_chans=1, num_classes=2, act_layer=nn.GELU,
+                                              norm_layer=partial(nn.LayerNorm, eps=1e-5), spec=spec)
+    randomize_(model, 5)
+    model.train()
+    g = torch.Generator().manual_seed(6)
+    img = torch.rand(4, 1, 32, 32, generator=g)
+    tgt = torch.randint(0, 2, (4,), generator=g)
+    logits = model(img)
+    loss = nn.functional.cross_entropy(logits, tgt)
+    loss.backward()
+    params, grads = {}, {}
+    for name, p in model.named_parameters():
+        n = (name.replace(".patch_embed.proj.", ".embed.").replace(".patch_embed.norm.", ".embed.norm.")
+             .replace(".conv.weight", ".weight"))
+        params[n] = p
+        grads[n] = p.grad
+    save(os.path.join(HERE, "mscvt_cvt_dwbn.npz"), img, tgt, params, logits, loss, grads)
+
+
 def gen_hf():
     from transformers import ViTConfig as HFConfig, ViTForImageClassification
     D, H, depth, P, img_size = 128, 2, 2, 8, 32
@@ -191,8 +225,11 @@ def gen_hf():
 
 if __name__ == "__main__":
     torch.set_num_threads(4)
-    gen_hf()  # before the MS_CvT stubs: a stub 'timm' module confuses transformers' import probe
+    if "--cvt-only" not in sys.argv:
+        gen_hf()  # before the MS_CvT stubs: a stub 'timm' module confuses transformers' import probe
     if os.path.exists(REF):
-        gen_mscvt()
+        if "--cvt-only" not in sys.argv:
+            gen_mscvt()
+        gen_mscvt_cvt()
     else:
         print("reference absent; MS_CvT fixture not regenerated")

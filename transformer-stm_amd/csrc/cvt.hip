@@ -1,0 +1,524 @@
+// cvt.hip — the convolutional pieces of the reference's CvT stages, gfx950.
+//
+//   * ConvEmbed: layers.Conv2D(embed_dim, kernel=k, strides=s, padding='same') at
+//     models/CvT(Par).py:203-212 (k7 s4, k3 s2 in the spec :66-72).  As a GEMM over patches:
+//     vitmi_conv_im2col builds [B*Ho*Wo][Kp] patch rows (column order kh, kw, c = the Keras
+//     kernel [kh][kw][Cin][Cout] flattened, zero-padded to Kp) with TF's asymmetric 'same'
+//     padding; vitmi_conv_col2im is its adjoint (input gradient, a gather over the
+//     overlapping windows: deterministic, no atomics).
+//   * Projection(method='dw_bn'): layers.DepthwiseConv2D(3, strides=1, 'same', no bias) +
+//     layers.BatchNormalization() in training mode (models/CvT(Par).py:92-94,104-106), applied
+//     to the spatial tokens of q, k and v (:154-156).  Batch statistics over (B, H, W) per
+//     channel, moving statistics updated with `momentum` (Keras 0.99).
+//
+// Layout: token-major rows [.., C] fp32 (NHWC), channels vectorised by 4.  The spatial tokens
+// of image b are rows b*img_stride + row_off + h*W + w, so the cls row of stage 3 (row 0 of
+// every image, :146-150) is skipped without a copy.  All kernels are HBM/L2-bound stencils and
+// reductions: per-channel partial sums by fixed-channel threads, block-reduced in LDS, finished
+// by a second tiny pass in a fixed order (deterministic).
+#include "common.h"
+
+namespace vitmi {
+
+struct ConvGeo {
+  int B, H, W, C, Ho, Wo, kh, kw, s, pt, pl;
+  int64_t ldx;          // floats between input rows
+  int64_t img_stride;   // input rows between images
+  int64_t row_off;      // first spatial row of an image
+};
+
+__device__ __forceinline__ int64_t in_row(const ConvGeo& g, int b, int h, int w) {
+  return (int64_t)b * g.img_stride + g.row_off + (int64_t)h * g.W + w;
+}
+
+// ---------------------------------------------------------------- im2col / col2im
+// patches[r][j], r = (b, oh, ow), j = (i, jj, c) < K = kh*kw*C, zero for j >= K or outside.
+template <typename T, int VEC>
+__global__ void conv_im2col_kernel(ConvGeo g, const float* __restrict__ x, T* __restrict__ patches, int Kp) {
+  const int K = g.kh * g.kw * g.C;
+  const int64_t rows = (int64_t)g.B * g.Ho * g.Wo;
+  const int64_t per_row = Kp / VEC;
+  const int64_t total = rows * per_row;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / per_row;
+    const int j = (int)(t - r * per_row) * VEC;
+    const int ow = (int)(r % g.Wo);
+    const int oh = (int)((r / g.Wo) % g.Ho);
+    const int b = (int)(r / ((int64_t)g.Wo * g.Ho));
+    float v[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) v[e] = 0.f;
+    if (j < K) {
+      const int c = j % g.C, tap = j / g.C;
+      const int i = tap / g.kw, jj = tap % g.kw;
+      const int h = oh * g.s - g.pt + i, w = ow * g.s - g.pl + jj;
+      if (h >= 0 && h < g.H && w >= 0 && w < g.W) {
+        const float* src = x + in_row(g, b, h, w) * g.ldx + c;
+        if constexpr (VEC == 4) {
+          const f32x4 q = *(const f32x4*)src;
+          v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+        } else {
+          v[0] = *src;
+        }
+      }
+    }
+    T* dst = patches + r * Kp + j;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) dst[e] = from_f32<T>(v[e]);
+  }
+}
+
+// dx[b,h,w,c] (+)= sum over the windows (oh, ow, i, jj) that read (h, w) of dpatches.
+template <typename T>
+__global__ void conv_col2im_kernel(ConvGeo g, const T* __restrict__ dp, int Kp, float* __restrict__ dx,
+                                   int accumulate) {
+  const int C4 = g.C / 4;
+  const int64_t total = (int64_t)g.B * g.H * g.W * C4;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C4) * 4;
+    const int64_t p = t / C4;
+    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H), b = (int)(p / ((int64_t)g.W * g.H));
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < g.kh; ++i) {
+      const int th = h + g.pt - i;
+      if (th < 0 || th % g.s) continue;
+      const int oh = th / g.s;
+      if (oh >= g.Ho) continue;
+      for (int jj = 0; jj < g.kw; ++jj) {
+        const int tw = w + g.pl - jj;
+        if (tw < 0 || tw % g.s) continue;
+        const int ow = tw / g.s;
+        if (ow >= g.Wo) continue;
+        const T* src = dp + (((int64_t)b * g.Ho + oh) * g.Wo + ow) * Kp + (i * g.kw + jj) * g.C + c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += to_f32(src[e]);
+      }
+    }
+    float* d = dx + in_row(g, b, h, w) * g.ldx + c;
+    if (accumulate) acc += *(const f32x4*)d;
+    *(f32x4*)d = acc;
+  }
+}
+
+// ---------------------------------------------------------------- depthwise 3x3 + BatchNorm
+// Thread (pixel lane pl, channel group cg) with cg = tid % C4 fixed for the whole grid-stride
+// loop: 256 / C4 pixels per block iteration (C4 divides 256).
+struct DwGeo {
+  int B, H, W, C;
+  int64_t ldx, x_img, x_off;   // input rows (LN output; cls row skipped through x_off)
+  int64_t ldz;                 // z / dz scratch rows: dense [B*H*W][C]
+};
+
+__device__ __forceinline__ int64_t dw_row(const DwGeo& g, int64_t p) {   // p = (b, h, w) linear
+  const int64_t hw = (int64_t)g.H * g.W;
+  return (p / hw) * g.x_img + g.x_off + p % hw;
+}
+
+// z = dwconv3x3(x) (same padding) -> z scratch; per-block partial sum / sum of squares.
+__global__ __launch_bounds__(256) void dw_fwd_stats_kernel(DwGeo g, const float* __restrict__ x,
+                                                           const float* __restrict__ wt,  // [3][3][C]
+                                                           float* __restrict__ z, float* __restrict__ part) {
+  __shared__ f32x4 red[2][256];
+  const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
+  const int c = cg * 4;
+  const int64_t n = (int64_t)g.B * g.H * g.W;
+  f32x4 wv[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wv[k] = *(const f32x4*)(wt + k * g.C + c);
+  f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t p = (int64_t)blockIdx.x * lanes + pl; p < n; p += (int64_t)gridDim.x * lanes) {
+    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H);
+    const int64_t base = p - (int64_t)h * g.W - w;   // (b, 0, 0)
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int hh = h + i - 1;
+      if (hh < 0 || hh >= g.H) continue;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int ww = w + j - 1;
+        if (ww < 0 || ww >= g.W) continue;
+        acc += wv[i * 3 + j] * *(const f32x4*)(x + dw_row(g, base + (int64_t)hh * g.W + ww) * g.ldx + c);
+      }
+    }
+    *(f32x4*)(z + p * g.ldz + c) = acc;
+    s1 += acc;
+    s2 += acc * acc;
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (pl == 0) {
+    for (int l = 1; l < lanes; ++l) {
+      s1 += red[0][l * C4 + cg];
+      s2 += red[1][l * C4 + cg];
+    }
+    *(f32x4*)(part + (int64_t)blockIdx.x * 2 * g.C + c) = s1;
+    *(f32x4*)(part + (int64_t)blockIdx.x * 2 * g.C + g.C + c) = s2;
+  }
+}
+
+// Fold the G block partials (fixed order) into mean / rstd; update the moving statistics.
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int G, int C, int64_t n, float eps,
+                                   float momentum, float* __restrict__ mean, float* __restrict__ rstd,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var, int training) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (!training) {   // inference: the moving statistics
+    mean[c] = run_mean[c];
+    rstd[c] = (float)(1.0 / sqrt((double)run_var[c] + (double)eps));
+    return;
+  }
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = 0; b < G; ++b) {
+    s1 += part[(int64_t)b * 2 * C + c];
+    s2 += part[(int64_t)b * 2 * C + C + c];
+  }
+  const double mu = s1 / (double)n;
+  double var = s2 / (double)n - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)mu;
+  rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * (float)mu;
+  if (run_var) run_var[c] = momentum * run_var[c] + (1.f - momentum) * (float)var;
+}
+
+// y = (z - mean) * rstd * gamma + beta  -> rows b*y_img + y_off + hw of y (out dtype)
+template <typename TY>
+__global__ void bn_apply_kernel(DwGeo g, const float* __restrict__ z, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                const float* __restrict__ beta, TY* __restrict__ y, int64_t ldy, int64_t y_img,
+                                int64_t y_off) {
+  const int C4 = g.C / 4;
+  const int64_t hw = (int64_t)g.H * g.W, total = (int64_t)g.B * hw * C4;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C4) * 4;
+    const int64_t p = t / C4;
+    const f32x4 zv = *(const f32x4*)(z + p * g.ldz + c);
+    const f32x4 o = (zv - *(const f32x4*)(mean + c)) * *(const f32x4*)(rstd + c) * *(const f32x4*)(gamma + c) +
+                    *(const f32x4*)(beta + c);
+    TY* d = y + ((p / hw) * y_img + y_off + p % hw) * ldy + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] = from_f32<TY>(o[e]);
+  }
+}
+
+// backward statistics: sum dy and sum dy * zhat per channel (dy rows like y's).
+template <typename TD>
+__global__ __launch_bounds__(256) void bn_bwd_stats_kernel(DwGeo g, const TD* __restrict__ dy, int64_t lddy,
+                                                           int64_t dy_img, int64_t dy_off,
+                                                           const float* __restrict__ z,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           float* __restrict__ part) {
+  __shared__ f32x4 red[2][256];
+  const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
+  const int c = cg * 4;
+  const int64_t hw = (int64_t)g.H * g.W, n = (int64_t)g.B * hw;
+  const f32x4 mu = *(const f32x4*)(mean + c), rs = *(const f32x4*)(rstd + c);
+  f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t p = (int64_t)blockIdx.x * lanes + pl; p < n; p += (int64_t)gridDim.x * lanes) {
+    const TD* src = dy + ((p / hw) * dy_img + dy_off + p % hw) * lddy + c;
+    f32x4 d;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] = to_f32(src[e]);
+    const f32x4 zh = (*(const f32x4*)(z + p * g.ldz + c) - mu) * rs;
+    s1 += d;
+    s2 += d * zh;
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (pl == 0) {
+    for (int l = 1; l < lanes; ++l) {
+      s1 += red[0][l * C4 + cg];
+      s2 += red[1][l * C4 + cg];
+    }
+    *(f32x4*)(part + (int64_t)blockIdx.x * 2 * g.C + c) = s1;
+    *(f32x4*)(part + (int64_t)blockIdx.x * 2 * g.C + g.C + c) = s2;
+  }
+}
+
+// sums -> dgamma/dbeta (+=), and the per-channel constants of dz: k1 = mean(dy), k2 = mean(dy zhat)
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C, int64_t n,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ kk) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = 0; b < G; ++b) {
+    s1 += part[(int64_t)b * 2 * C + c];
+    s2 += part[(int64_t)b * 2 * C + C + c];
+  }
+  if (dgamma) dgamma[c] += (float)s2;
+  if (dbeta) dbeta[c] += (float)s1;
+  kk[c] = (float)(s1 / (double)n);
+  kk[C + c] = (float)(s2 / (double)n);
+}
+
+// dz = gamma * rstd * (dy - k1 - zhat * k2) -> scratch; per-block partials of
+// dW[i][j][c] = sum_p dz[p][c] * x[p + (i-1, j-1)][c].
+template <typename TD>
+__global__ __launch_bounds__(256) void dw_bwd_dz_kernel(DwGeo g, const TD* __restrict__ dy, int64_t lddy,
+                                                        int64_t dy_img, int64_t dy_off,
+                                                        const float* __restrict__ z, const float* __restrict__ x,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ kk, float* __restrict__ dz,
+                                                        float* __restrict__ part) {
+  __shared__ f32x4 red[256];
+  const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
+  const int c = cg * 4;
+  const int64_t hw = (int64_t)g.H * g.W, n = (int64_t)g.B * hw;
+  const f32x4 mu = *(const f32x4*)(mean + c), rs = *(const f32x4*)(rstd + c);
+  const f32x4 gr = *(const f32x4*)(gamma + c) * rs;
+  const f32x4 k1 = *(const f32x4*)(kk + c), k2 = *(const f32x4*)(kk + g.C + c);
+  f32x4 dw[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) dw[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t p = (int64_t)blockIdx.x * lanes + pl; p < n; p += (int64_t)gridDim.x * lanes) {
+    const TD* src = dy + ((p / hw) * dy_img + dy_off + p % hw) * lddy + c;
+    f32x4 d;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] = to_f32(src[e]);
+    const f32x4 zh = (*(const f32x4*)(z + p * g.ldz + c) - mu) * rs;
+    const f32x4 dzv = gr * (d - k1 - zh * k2);
+    *(f32x4*)(dz + p * g.ldz + c) = dzv;
+    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H);
+    const int64_t base = p - (int64_t)h * g.W - w;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int hh = h + i - 1;
+      if (hh < 0 || hh >= g.H) continue;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int ww = w + j - 1;
+        if (ww < 0 || ww >= g.W) continue;
+        dw[i * 3 + j] += dzv * *(const f32x4*)(x + dw_row(g, base + (int64_t)hh * g.W + ww) * g.ldx + c);
+      }
+    }
+  }
+  for (int k = 0; k < 9; ++k) {
+    __syncthreads();
+    red[threadIdx.x] = dw[k];
+    __syncthreads();
+    if (pl == 0) {
+      f32x4 s = dw[k];
+      for (int l = 1; l < lanes; ++l) s += red[l * C4 + cg];
+      *(f32x4*)(part + ((int64_t)blockIdx.x * 9 + k) * g.C + c) = s;
+    }
+  }
+}
+
+// dW[k][c] += sum over blocks of the partials (fixed order)
+__global__ void dw_wgrad_finalize_kernel(const float* __restrict__ part, int G, int C, float* __restrict__ dwt) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 9 * C) return;
+  float s = 0.f;
+  for (int b = 0; b < G; ++b) s += part[(int64_t)b * 9 * C + e];
+  dwt[e] += s;
+}
+
+// dx[p] += sum_{i,j} w[i][j] * dz[p - (i-1, j-1)]   (rows of dx like x's)
+__global__ void dw_bwd_dx_kernel(DwGeo g, const float* __restrict__ dz, const float* __restrict__ wt,
+                                 float* __restrict__ dx) {
+  const int C4 = g.C / 4;
+  const int64_t total = (int64_t)g.B * g.H * g.W * C4;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C4) * 4;
+    const int64_t p = t / C4;
+    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H);
+    const int64_t base = p - (int64_t)h * g.W - w;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int hh = h - i + 1;
+      if (hh < 0 || hh >= g.H) continue;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int ww = w - j + 1;
+        if (ww < 0 || ww >= g.W) continue;
+        acc += *(const f32x4*)(wt + (i * 3 + j) * g.C + c) * *(const f32x4*)(dz + (base + (int64_t)hh * g.W + ww) * g.ldz + c);
+      }
+    }
+    float* d = dx + dw_row(g, p) * g.ldx + c;
+    *(f32x4*)d = *(const f32x4*)d + acc;
+  }
+}
+
+static unsigned grid_of(int64_t work, int per_block = 256, int cap = 4096) {
+  int64_t gsz = (work + per_block - 1) / per_block;
+  if (gsz > cap) gsz = cap;
+  return (unsigned)(gsz < 1 ? 1 : gsz);
+}
+
+static int dw_blocks(int64_t n, int C) {
+  const int lanes = 256 / (C / 4);
+  int64_t gsz = (n + lanes * 8 - 1) / (lanes * 8);   // >= 8 pixels per thread
+  if (gsz > 512) gsz = 512;
+  return (int)(gsz < 1 ? 1 : gsz);
+}
+
+static bool dw_channels_ok(int C) { return C >= 4 && C % 4 == 0 && 1024 % C == 0; }
+
+// TF 'same': Ho = ceil(H / s), pad_total = max((Ho - 1) s + k - H, 0), pad_before = total / 2
+static void same_pad(int H, int k, int s, int& Ho, int& pt) {
+  Ho = (H + s - 1) / s;
+  int tot = (Ho - 1) * s + k - H;
+  if (tot < 0) tot = 0;
+  pt = tot / 2;
+}
+
+}  // namespace vitmi
+
+using namespace vitmi;
+
+extern "C" int vitmi_conv_same_geometry(int H, int W, int kh, int kw, int s, int* Ho, int* Wo, int* pad_top,
+                                        int* pad_left) {
+  VITMI_CHECK_ARG(H > 0 && W > 0 && kh > 0 && kw > 0 && s > 0, "conv_same_geometry: bad sizes");
+  int ho, wo, pt, pl;
+  same_pad(H, kh, s, ho, pt);
+  same_pad(W, kw, s, wo, pl);
+  if (Ho) *Ho = ho;
+  if (Wo) *Wo = wo;
+  if (pad_top) *pad_top = pt;
+  if (pad_left) *pad_left = pl;
+  return VITMI_OK;
+}
+
+static int make_geo(ConvGeo& g, int B, int H, int W, int C, int kh, int kw, int s, int pt, int pl, int Ho, int Wo,
+                    int64_t ldx, int64_t img_stride, int64_t row_off) {
+  VITMI_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0 && kh > 0 && kw > 0 && s > 0, "conv: bad sizes");
+  VITMI_CHECK_ARG(pt >= 0 && pl >= 0 && pt < kh && pl < kw && Ho > 0 && Wo > 0, "conv: bad padding / output size");
+  VITMI_CHECK_ARG((Ho - 1) * s - pt < H && (Wo - 1) * s - pl < W, "conv: output window outside the input");
+  VITMI_CHECK_ARG(ldx >= C && img_stride >= (int64_t)H * W + row_off && row_off >= 0, "conv: bad row layout");
+  g.B = B; g.H = H; g.W = W; g.C = C; g.kh = kh; g.kw = kw; g.s = s;
+  g.Ho = Ho; g.Wo = Wo; g.pt = pt; g.pl = pl;
+  g.ldx = ldx; g.img_stride = img_stride; g.row_off = row_off;
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_conv_im2col(int dtype, int B, int H, int W, int C, int kh, int kw, int s, int pad_top,
+                                 int pad_left, int Ho, int Wo, const float* x, int64_t ldx, int64_t img_stride,
+                                 int64_t row_off, void* patches, int Kp, vitmi_stream_t stream) {
+  ConvGeo g;
+  if (int rc = make_geo(g, B, H, W, C, kh, kw, s, pad_top, pad_left, Ho, Wo, ldx, img_stride, row_off)) return rc;
+  VITMI_CHECK_ARG(x && patches, "conv_im2col: null pointer");
+  VITMI_CHECK_ARG(Kp >= kh * kw * C, "conv_im2col: Kp < kh*kw*C");
+  VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "conv_im2col: bad dtype");
+  const bool vec = C % 4 == 0 && Kp % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x % 16) == 0;
+  const int64_t work = (int64_t)B * g.Ho * g.Wo * Kp / (vec ? 4 : 1);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VITMI_BF16) {
+    if (vec) hipLaunchKernelGGL((conv_im2col_kernel<bf16, 4>), dim3(grid_of(work)), dim3(256), 0, st, g, x, (bf16*)patches, Kp);
+    else hipLaunchKernelGGL((conv_im2col_kernel<bf16, 1>), dim3(grid_of(work)), dim3(256), 0, st, g, x, (bf16*)patches, Kp);
+  } else {
+    if (vec) hipLaunchKernelGGL((conv_im2col_kernel<float, 4>), dim3(grid_of(work)), dim3(256), 0, st, g, x, (float*)patches, Kp);
+    else hipLaunchKernelGGL((conv_im2col_kernel<float, 1>), dim3(grid_of(work)), dim3(256), 0, st, g, x, (float*)patches, Kp);
+  }
+  VITMI_LAUNCH_CHECK("conv_im2col");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_conv_col2im(int dtype, int B, int H, int W, int C, int kh, int kw, int s, int pad_top,
+                                 int pad_left, int Ho, int Wo, const void* dpatches, int Kp, float* dx, int64_t ldx,
+                                 int64_t img_stride, int64_t row_off, int accumulate, vitmi_stream_t stream) {
+  ConvGeo g;
+  if (int rc = make_geo(g, B, H, W, C, kh, kw, s, pad_top, pad_left, Ho, Wo, ldx, img_stride, row_off)) return rc;
+  VITMI_CHECK_ARG(dpatches && dx, "conv_col2im: null pointer");
+  VITMI_CHECK_ARG(C % 4 == 0 && ldx % 4 == 0 && Kp >= kh * kw * C, "conv_col2im: C %% 4 == 0 required");
+  const int64_t work = (int64_t)B * H * W * (C / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VITMI_BF16)
+    hipLaunchKernelGGL(conv_col2im_kernel<bf16>, dim3(grid_of(work)), dim3(256), 0, st, g, (const bf16*)dpatches, Kp,
+                       dx, accumulate);
+  else
+    hipLaunchKernelGGL(conv_col2im_kernel<float>, dim3(grid_of(work)), dim3(256), 0, st, g, (const float*)dpatches,
+                       Kp, dx, accumulate);
+  VITMI_LAUNCH_CHECK("conv_col2im");
+  return VITMI_OK;
+}
+
+static int make_dw(DwGeo& g, int B, int H, int W, int C, int64_t ldx, int64_t x_img, int64_t x_off) {
+  VITMI_CHECK_ARG(B > 0 && H > 0 && W > 0, "dwconv: bad sizes");
+  VITMI_CHECK_ARG(dw_channels_ok(C), "dwconv: C must be a multiple of 4 dividing 1024 (got %d)", C);
+  VITMI_CHECK_ARG(ldx % 4 == 0 && ldx >= C && x_img >= (int64_t)H * W + x_off && x_off >= 0, "dwconv: bad row layout");
+  g.B = B; g.H = H; g.W = W; g.C = C; g.ldx = ldx; g.x_img = x_img; g.x_off = x_off; g.ldz = C;
+  return VITMI_OK;
+}
+
+extern "C" size_t vitmi_dwconv_bn_workspace_size(int B, int H, int W, int C) {
+  const int64_t n = (int64_t)B * H * W;
+  const int G = dw_blocks(n, C);
+  // partials (max of the stats pass and the 9-tap weight-grad pass) + dz scratch + k1/k2
+  return (size_t)G * 9 * C * sizeof(float) + (size_t)n * C * sizeof(float) + 2 * C * sizeof(float);
+}
+
+extern "C" int vitmi_dwconv_bn_fwd(int B, int H, int W, int C, const float* x, int64_t ldx, int64_t x_img,
+                                   int64_t x_off, const float* wt, const float* gamma, const float* beta,
+                                   float eps, float momentum, int training, float* run_mean, float* run_var,
+                                   float* z, float* mean, float* rstd, void* y, int y_dtype, int64_t ldy,
+                                   int64_t y_img, int64_t y_off, void* workspace, size_t ws_bytes,
+                                   vitmi_stream_t stream) {
+  DwGeo g;
+  if (int rc = make_dw(g, B, H, W, C, ldx, x_img, x_off)) return rc;
+  VITMI_CHECK_ARG(x && wt && gamma && beta && z && mean && rstd && y, "dwconv_bn_fwd: null pointer");
+  VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_dwconv_bn_workspace_size(B, H, W, C), "dwconv_bn_fwd: workspace");
+  VITMI_CHECK_ARG(ldy % 4 == 0 && y_img >= (int64_t)H * W + y_off, "dwconv_bn_fwd: bad output layout");
+  VITMI_CHECK_ARG(training || (run_mean && run_var), "dwconv_bn_fwd: inference needs the moving statistics");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n = (int64_t)B * H * W;
+  const int G = dw_blocks(n, C);
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(dw_fwd_stats_kernel, dim3(G), dim3(256), 0, st, g, x, wt, z, part);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, st, (const float*)part, G, C, n, eps,
+                     momentum, mean, rstd, run_mean, run_var, training);
+  const int64_t work = n * (C / 4);
+  if (y_dtype == VITMI_BF16)
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(grid_of(work)), dim3(256), 0, st, g, (const float*)z,
+                       (const float*)mean, (const float*)rstd, gamma, beta, (bf16*)y, ldy, y_img, y_off);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_of(work)), dim3(256), 0, st, g, (const float*)z,
+                       (const float*)mean, (const float*)rstd, gamma, beta, (float*)y, ldy, y_img, y_off);
+  VITMI_LAUNCH_CHECK("dwconv_bn_fwd");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, int dy_dtype, int64_t lddy,
+                                   int64_t dy_img, int64_t dy_off, const float* x, int64_t ldx, int64_t x_img,
+                                   int64_t x_off, const float* wt, const float* gamma, const float* z,
+                                   const float* mean, const float* rstd, float* dx, float* dwt, float* dgamma,
+                                   float* dbeta, void* workspace, size_t ws_bytes, vitmi_stream_t stream) {
+  DwGeo g;
+  if (int rc = make_dw(g, B, H, W, C, ldx, x_img, x_off)) return rc;
+  VITMI_CHECK_ARG(dy && x && wt && gamma && z && mean && rstd && dx && dwt, "dwconv_bn_bwd: null pointer");
+  VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_dwconv_bn_workspace_size(B, H, W, C), "dwconv_bn_bwd: workspace");
+  VITMI_CHECK_ARG(lddy % 4 == 0 && dy_img >= (int64_t)H * W + dy_off, "dwconv_bn_bwd: bad dy layout");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n = (int64_t)B * H * W;
+  const int G = dw_blocks(n, C);
+  float* part = (float*)workspace;
+  float* dz = part + (size_t)G * 9 * C;
+  float* kk = dz + (size_t)n * C;
+  if (dy_dtype == VITMI_BF16) {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<bf16>, dim3(G), dim3(256), 0, st, g, (const bf16*)dy, lddy, dy_img, dy_off,
+                       z, mean, rstd, part);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<float>, dim3(G), dim3(256), 0, st, g, (const float*)dy, lddy, dy_img,
+                       dy_off, z, mean, rstd, part);
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, st, (const float*)part, G, C, n,
+                     dgamma, dbeta, kk);
+  if (dy_dtype == VITMI_BF16)
+    hipLaunchKernelGGL(dw_bwd_dz_kernel<bf16>, dim3(G), dim3(256), 0, st, g, (const bf16*)dy, lddy, dy_img, dy_off, z,
+                       x, mean, rstd, gamma, (const float*)kk, dz, part);
+  else
+    hipLaunchKernelGGL(dw_bwd_dz_kernel<float>, dim3(G), dim3(256), 0, st, g, (const float*)dy, lddy, dy_img, dy_off,
+                       z, x, mean, rstd, gamma, (const float*)kk, dz, part);
+  hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3((9 * C + 255) / 256), dim3(256), 0, st, (const float*)part, G, C,
+                     dwt);
+  hipLaunchKernelGGL(dw_bwd_dx_kernel, dim3(grid_of(n * (C / 4))), dim3(256), 0, st, g, (const float*)dz, wt, dx);
+  VITMI_LAUNCH_CHECK("dwconv_bn_bwd");
+  return VITMI_OK;
+}

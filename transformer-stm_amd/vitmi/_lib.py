@@ -56,6 +56,12 @@ SIGNATURES = {
     "vitmi_dropout_hash": (U, [U, U, U, U]),
     "vitmi_linear_fwd_dropout": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P, S, U, U, U, F, P]),
     "vitmi_dropout_apply": (I, [L, L, P, L, P, I, L, U, U, U, F, P]),
+    "vitmi_conv_same_geometry": (I, [I, I, I, I, I, P, P, P, P]),
+    "vitmi_conv_im2col": (I, [I, I, I, I, I, I, I, I, I, I, I, I, P, L, L, L, P, I, P]),
+    "vitmi_conv_col2im": (I, [I, I, I, I, I, I, I, I, I, I, I, I, P, I, P, L, L, L, I, P]),
+    "vitmi_dwconv_bn_workspace_size": (S, [I, I, I, I]),
+    "vitmi_dwconv_bn_fwd": (I, [I, I, I, I, P, L, L, L, P, P, P, F, F, I, P, P, P, P, P, P, I, L, L, L, P, S, P]),
+    "vitmi_dwconv_bn_bwd": (I, [I, I, I, I, P, I, L, L, L, P, L, L, L, P, P, P, P, P, P, P, P, P, P, S, P]),
 }
 
 _lib = None
