@@ -301,3 +301,74 @@ def cast_bf16(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
         dst = torch.empty(src.shape, dtype=torch.bfloat16, device=src.device)
     check(lib().vitmi_cast_f32_bf16(src.numel(), _p(src), _p(dst), _s()), "cast")
     return dst
+
+
+# ---------------------------------------------------------------- CvT stages
+def conv_same_geometry(H: int, W: int, k: int, s: int) -> Tuple[int, int, int, int]:
+    """TF 'same' geometry of layers.Conv2D (models/CvT(Par).py:203-212): (Ho, Wo, pad_top, pad_left)."""
+    import ctypes
+    v = [ctypes.c_int(0) for _ in range(4)]
+    check(lib().vitmi_conv_same_geometry(H, W, k, k, s, *[ctypes.addressof(t) for t in v]), "conv_same_geometry")
+    return tuple(t.value for t in v)
+
+
+def conv_im2col(x: Tensor, B: int, H: int, W: int, C: int, k: int, s: int, geo, Kp: int,
+                out_dtype: torch.dtype, img_stride: Optional[int] = None, row_off: int = 0) -> Tensor:
+    """Patch rows [B*Ho*Wo, Kp] (column order kh, kw, c; zero past kh*kw*C) of the NHWC fp32
+    token rows of x (image b pixel (h, w) = row b*img_stride + row_off + h*W + w)."""
+    Ho, Wo, pt, pl = geo
+    _, ldx = _rows(x)
+    img_stride = H * W if img_stride is None else img_stride
+    out = torch.empty(B * Ho * Wo, Kp, dtype=out_dtype, device=x.device)
+    check(lib().vitmi_conv_im2col(dt(out_dtype), B, H, W, C, k, k, s, pt, pl, Ho, Wo, _p(x), ldx, img_stride, row_off,
+                                  _p(out), Kp, _s()), "conv_im2col")
+    return out
+
+
+def conv_col2im(dp: Tensor, B: int, H: int, W: int, C: int, k: int, s: int, geo, dx: Tensor,
+                img_stride: Optional[int] = None, row_off: int = 0, accumulate: bool = False) -> Tensor:
+    """dx (fp32 NHWC rows as in conv_im2col) (+)= the adjoint of im2col applied to dp [rows, Kp]."""
+    Ho, Wo, pt, pl = geo
+    _, ldx = _rows(dx)
+    img_stride = H * W if img_stride is None else img_stride
+    check(lib().vitmi_conv_col2im(dt(dp.dtype), B, H, W, C, k, k, s, pt, pl, Ho, Wo, _p(dp), dp.shape[-1], _p(dx), ldx,
+                                  img_stride, row_off, int(accumulate), _s()), "conv_col2im")
+    return dx
+
+
+def dwconv_bn_fwd(x: Tensor, B: int, H: int, W: int, w9: Tensor, gamma: Tensor, beta: Tensor, eps: float,
+                  momentum: float, training: bool, run_mean: Optional[Tensor], run_var: Optional[Tensor],
+                  y: Tensor, x_img: Optional[int] = None, x_off: int = 0, y_img: Optional[int] = None,
+                  y_off: int = 0):
+    """Projection('dw_bn') (models/CvT(Par).py:92-94): y rows <- BN(depthwise3x3(x)); w9 [3,3,C].
+    Returns the saved (z, mean, rstd)."""
+    C = x.shape[-1]
+    _, ldx = _rows(x)
+    _, ldy = _rows(y)
+    x_img = H * W if x_img is None else x_img
+    y_img = H * W if y_img is None else y_img
+    z = torch.empty(B * H * W, C, dtype=torch.float32, device=x.device)
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    ws = _ws(lib().vitmi_dwconv_bn_workspace_size(B, H, W, C), x)
+    check(lib().vitmi_dwconv_bn_fwd(B, H, W, C, _p(x), ldx, x_img, x_off, _p(w9), _p(gamma), _p(beta), float(eps),
+                                    float(momentum), int(training), _p(run_mean), _p(run_var), _p(z), _p(mean),
+                                    _p(rstd), _p(y), dt(y.dtype), ldy, y_img, y_off, _p(ws), ws.numel(), _s()),
+          "dwconv_bn_fwd")
+    return z, mean, rstd
+
+
+def dwconv_bn_bwd(dy: Tensor, x: Tensor, B: int, H: int, W: int, w9: Tensor, gamma: Tensor, z: Tensor,
+                  mean: Tensor, rstd: Tensor, dx: Tensor, dw9: Tensor, dgamma: Tensor, dbeta: Tensor,
+                  x_img: Optional[int] = None, x_off: int = 0, dy_img: Optional[int] = None, dy_off: int = 0) -> None:
+    """dx (rows as x) += d/dx; dw9/dgamma/dbeta += their gradients (fp32)."""
+    C = x.shape[-1]
+    _, ldx = _rows(x)
+    _, lddy = _rows(dy)
+    assert dx.stride() == x.stride()
+    x_img = H * W if x_img is None else x_img
+    dy_img = H * W if dy_img is None else dy_img
+    ws = _ws(lib().vitmi_dwconv_bn_workspace_size(B, H, W, C), x)
+    check(lib().vitmi_dwconv_bn_bwd(B, H, W, C, _p(dy), dt(dy.dtype), lddy, dy_img, dy_off, _p(x), ldx, x_img, x_off,
+                                    _p(w9), _p(gamma), _p(z), _p(mean), _p(rstd), _p(dx), _p(dw9), _p(dgamma),
+                                    _p(dbeta), _p(ws), ws.numel(), _s()), "dwconv_bn_bwd")
