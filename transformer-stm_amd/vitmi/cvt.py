@@ -1,0 +1,388 @@
+"""CvT: the reference's convolutional transformer on the MI355X path.
+
+``create_cvt_model`` (``models/CvT(Par).py:292-354``) with the stage spec ``:66-72``: per stage a
+strided ``ConvEmbed`` (Conv2D 'same', ``:194-217``) and one ``ConvTransformerBlock``
+(``:231-289``) whose q/k/v come from ``Projection('dw_bn')`` (depthwise 3x3 + BatchNorm,
+``:83-112``) followed by the q/k/v Dense layers composed with MultiHeadAttention's own
+projections (``:132-137,178-185``).  Module tree and parameter names follow MS_CvT's
+``ConvolutionalVisionTransformer`` (``old_codes/MS_CvT.py:491-623``)::
+
+    CvT(cfg)
+      stage{i}: CvTStageModule  (.embed: ConvEmbedSame (.norm if cfg.embed_norm), .cls_token,
+                                 .blocks[j]: CvTBlock (.norm1, .attn: CvTAttention
+                                 (.conv_proj_{q,k,v}: DwBnProjection (.bn), .proj_{q,k,v}, .proj),
+                                 .norm2 unless tied, .mlp (.fc1, .fc2)))
+      norm: LayerNorm, head: Linear
+
+Every op runs as a libvitmi kernel: conv-embed im2col + MFMA GEMM (+ col2im in the backward),
+dw_bn fwd/bwd, LayerNorm, the q/k/v/out/MLP GEMMs with fused epilogues and the attention
+kernels (N = 1024, 256 and 65 at 128x128 input).  Small glue (the cls-row copies) is torch
+tensor indexing on the GPU.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .modules import F32, LayerNorm, Linear, _check_cuda, _grad, _lp, cross_entropy, mse_loss  # noqa: F401
+
+Tensor = torch.Tensor
+
+
+@dataclass
+class CvTStage:
+    embed_dim: int
+    patch_size: int
+    stride: int
+    num_heads: int
+    with_cls_token: bool = False
+    depth: int = 1
+    padding: Optional[int] = None    # None: TF 'same' (Keras); an int: symmetric (torch / MS_CvT)
+
+
+def keras_spec() -> List[CvTStage]:
+    """models/CvT(Par).py:66-72 (projection_method 'dw_bn' :25, cls_token_switch True :28)."""
+    return [CvTStage(64, 7, 4, 1), CvTStage(128, 3, 2, 2), CvTStage(256, 3, 2, 4, with_cls_token=True)]
+
+
+@dataclass
+class CvTConfig:
+    img_size: int = 128
+    in_chans: int = 1
+    num_classes: int = 1
+    stages: List[CvTStage] = field(default_factory=keras_spec)
+    mlp_ratio: float = 4.0
+    attn_scale: str = "head"       # Keras MHA key_dim**-0.5; 'dim' = MS_CvT D**-0.5
+    ln_eps: float = 1e-6
+    bn_eps: float = 1e-3           # Keras BatchNormalization
+    bn_momentum: float = 0.99      # Keras convention: running <- m running + (1 - m) batch
+    qkv_bias: bool = True
+    tie_norms: bool = True         # the Keras block applies its one norm1 twice (:272,278)
+    embed_norm: bool = False       # the intended ConvEmbed LayerNorm is never built (:209)
+    dtype: str = "bf16"
+
+    def replace(self, **kw) -> "CvTConfig":
+        return dataclasses.replace(self, **kw)
+
+
+def _kpad(K: int) -> int:
+    return (K + 63) // 64 * 64   # the GEMM's K step (bf16 64, fp32 32)
+
+
+def _geometry(H: int, k: int, s: int, padding: Optional[int]):
+    """(Ho, Wo, pad_top, pad_left) for a square input."""
+    if padding is None:
+        return ops.conv_same_geometry(H, H, k, s)
+    Ho = (H + 2 * padding - k) // s + 1
+    return (Ho, Ho, padding, padding)
+
+
+# ======================================================================= ConvEmbed
+class ConvEmbedSame(nn.Module):
+    """layers.Conv2D(D, kernel=k, strides=s, padding='same') (models/CvT(Par).py:203-212) on
+    NHWC token rows, as im2col + MFMA GEMM.  ``weight`` keeps torch's [D, Cin, k, k] layout."""
+
+    def __init__(self, cin: int, dim: int, k: int, s: int, padding: Optional[int], norm: bool, eps: float,
+                 dtype: str):
+        super().__init__()
+        self.cin, self.dim, self.k, self.s, self.padding, self.dtype = cin, dim, k, s, padding, dtype
+        self.weight = nn.Parameter(torch.zeros(dim, cin, k, k))
+        self.bias = nn.Parameter(torch.zeros(dim))
+        self.norm = LayerNorm(dim, eps) if norm else None
+
+    def forward(self, x: Tensor, B: int, H: int, img_stride: Optional[int] = None, row_off: int = 0):
+        """x: fp32 rows [.., Cin] (image b pixel (h, w) = row b*img_stride + row_off + h*H + w).
+        Returns (tokens fp32 [B, Ho*Wo, D], Ho)."""
+        geo = _geometry(H, self.k, self.s, self.padding)
+        y = _ConvEmbedFn.apply(x, self, geo, B, H, img_stride, row_off, self.weight, self.bias)
+        y = y.view(B, geo[0] * geo[1], self.dim)
+        if self.norm is not None:
+            y = self.norm(y)
+        return y, geo[0]
+
+
+class _ConvEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mod, geo, B, H, img_stride, row_off, w, b):
+        T = ops.torch_dtype(mod.dtype)
+        C, D, k = mod.cin, mod.dim, mod.k
+        K = k * k * C
+        Kp = _kpad(K)
+        patches = ops.conv_im2col(x, B, H, H, C, k, mod.s, geo, Kp, T, img_stride, row_off)
+        wm = torch.zeros(D, Kp, dtype=T, device=x.device)          # [D][kh][kw][Cin], zero-padded
+        wm[:, :K] = w.detach().permute(0, 2, 3, 1).reshape(D, K).to(T)
+        y = ops.linear_fwd(patches, wm, b, F32)
+        ctx.save_for_backward(x, patches, wm)
+        ctx.mod, ctx.geo, ctx.dims = mod, geo, (B, H, img_stride, row_off)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, patches, wm = ctx.saved_tensors
+        mod, geo, (B, H, img_stride, row_off) = ctx.mod, ctx.geo, ctx.dims
+        T = patches.dtype
+        C, D, k = mod.cin, mod.dim, mod.k
+        K = k * k * C
+        dy = dy.contiguous().float()
+        dy_lp = dy if T == F32 else ops.cast_bf16(dy)
+        dwm = torch.zeros(D, wm.shape[1], dtype=torch.float32, device=dy.device)
+        ops.linear_wgrad(dy_lp, patches, dwm)
+        _grad(mod.weight).add_(dwm[:, :K].view(D, k, k, C).permute(0, 3, 1, 2))
+        ops.bias_grad(dy_lp, _grad(mod.bias))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dp = ops.linear_dgrad(dy_lp, wm, F32)
+            dx = torch.zeros_like(x)
+            ops.conv_col2im(dp, B, H, H, C, k, mod.s, geo, dx, img_stride, row_off)
+        return (dx,) + (None,) * 8
+
+
+# ======================================================================= dw_bn projection
+class _BN(nn.Module):
+    """layers.BatchNormalization parameters and moving statistics (models/CvT(Par).py:94)."""
+
+    def __init__(self, dim: int):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.bias = nn.Parameter(torch.zeros(dim))
+        self.register_buffer("running_mean", torch.zeros(dim))
+        self.register_buffer("running_var", torch.ones(dim))
+
+
+class DwBnProjection(nn.Module):
+    """Projection(method='dw_bn') (models/CvT(Par).py:83-112): DepthwiseConv2D(3, 'same', no
+    bias) + BatchNormalization.  ``weight`` [D, 1, 3, 3] (torch grouped-conv layout)."""
+
+    def __init__(self, dim: int):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(dim, 1, 3, 3))
+        self.bn = _BN(dim)
+
+    def w9(self) -> Tensor:
+        return self.weight.detach().view(-1, 9).t().contiguous()   # [3][3][D]
+
+
+class CvTAttention(nn.Module):
+    def __init__(self, dim: int, num_heads: int, qkv_bias: bool):
+        super().__init__()
+        self.num_heads = num_heads
+        self.conv_proj_q, self.conv_proj_k, self.conv_proj_v = (DwBnProjection(dim) for _ in range(3))
+        self.proj_q, self.proj_k, self.proj_v = (Linear(dim, dim, bias=qkv_bias) for _ in range(3))
+        self.proj = Linear(dim, dim)
+
+
+class _Mlp(nn.Module):
+    def __init__(self, dim: int, hidden: int):
+        super().__init__()
+        self.fc1 = Linear(dim, hidden)
+        self.fc2 = Linear(hidden, dim)
+
+
+class CvTBlock(nn.Module):
+    """ConvTransformerBlock (models/CvT(Par).py:231-289) with dw_bn q/k/v."""
+
+    def __init__(self, dim: int, num_heads: int, cfg: CvTConfig):
+        super().__init__()
+        self.norm1 = LayerNorm(dim, cfg.ln_eps)
+        self.attn = CvTAttention(dim, num_heads, cfg.qkv_bias)
+        self.tie_norms = cfg.tie_norms
+        if not cfg.tie_norms:
+            self.norm2 = LayerNorm(dim, cfg.ln_eps)
+        self.mlp = _Mlp(dim, int(dim * cfg.mlp_ratio))
+        self.cfg = cfg
+        self.dim = dim
+
+    @property
+    def _norm2(self) -> LayerNorm:
+        return self.norm1 if self.tie_norms else self.norm2
+
+    def forward(self, x: Tensor, H: int, W: int, with_cls: bool) -> Tensor:
+        _check_cuda(x)
+        return _CvTBlockFn.apply(x, self, H, W, with_cls, *self.parameters())
+
+
+class _CvTBlockFn(torch.autograd.Function):
+    """Fused CvT block: LN1 -> 3 x (dw_bn -> q/k/v GEMM) -> attention -> out-proj + residual ->
+    LN(2 or tied 1) -> fc1 + GELU -> fc2 + residual.  The cls row (stage 3) bypasses dw_bn
+    (models/CvT(Par).py:146-150,164-176)."""
+
+    @staticmethod
+    def forward(ctx, x, blk, H, W, with_cls, *params):
+        cfg = blk.cfg
+        T = ops.torch_dtype(cfg.dtype)
+        B, N, D = x.shape
+        M = B * N
+        off = 1 if with_cls else 0
+        a_ = blk.attn
+        Hh = a_.num_heads
+        dh = D // Hh
+        scale = dh ** -0.5 if cfg.attn_scale == "head" else D ** -0.5
+        x2 = x.contiguous().view(M, D)
+        n1, n2 = blk.norm1, blk._norm2
+        h, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, cfg.ln_eps, F32)
+        qkv = torch.empty(M, 3 * D, dtype=T, device=x.device)
+        saved_proj = []
+        for c_i, c in enumerate("qkv"):
+            cp = getattr(a_, f"conv_proj_{c}")
+            lin = getattr(a_, f"proj_{c}")
+            inp = torch.empty(M, D, dtype=T, device=x.device)
+            if with_cls:
+                inp.view(B, N, D)[:, 0] = h.view(B, N, D)[:, 0].to(T)
+            z, mean, rstd = ops.dwconv_bn_fwd(h, B, H, W, cp.w9(), cp.bn.weight, cp.bn.bias, cfg.bn_eps,
+                                              cfg.bn_momentum, blk.training, cp.bn.running_mean,
+                                              cp.bn.running_var, inp, x_img=N, x_off=off, y_img=N, y_off=off)
+            wl = _lp(blk, lin.weight, T)
+            ops.gemm(inp, wl, True, True, M, D, D, qkv[:, c_i * D:(c_i + 1) * D], ops.EPI_STORE, bias=lin.bias)
+            saved_proj += [inp, z, mean, rstd, wl]
+        o, lse = ops.attention_fwd(qkv, B, N, Hh, scale)
+        wo = _lp(blk, a_.proj.weight, T)
+        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2)
+        h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, cfg.ln_eps, T)
+        w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
+        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU)
+        out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
+        ctx.save_for_backward(x2, h, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wo, w1, w2, *saved_proj)
+        ctx.blk, ctx.dims = blk, (B, N, D, H, W, with_cls, scale)
+        return out.view(B, N, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x2, h, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wo, w1, w2, *sp) = ctx.saved_tensors
+        blk = ctx.blk
+        B, N, D, H, W, with_cls, scale = ctx.dims
+        cfg = blk.cfg
+        T = h2.dtype
+        lpT = None if T == F32 else T
+        M = B * N
+        off = 1 if with_cls else 0
+        a_, mlp = blk.attn, blk.mlp
+        n1, n2 = blk.norm1, blk._norm2
+        g2 = dout.contiguous().view(M, D).float()
+        g2_lp = g2 if T == F32 else ops.cast_bf16(g2)
+        # MLP
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u)
+        ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
+        ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
+        dh2 = ops.linear_dgrad(du, w1, T)
+        ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
+        ops.bias_grad(du, _grad(mlp.fc1.bias))
+        dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias), dres=g2,
+                                        lp_dtype=lpT)
+        if dx1_lp is None:
+            dx1_lp = dx1
+        # attention + out-projection
+        do = ops.linear_dgrad(dx1_lp, wo, T)
+        ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
+        ops.bias_grad(dx1_lp, _grad(a_.proj.bias))
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, scale)
+        # q/k/v GEMMs, the cls rows, dw_bn: all into the LN1-output gradient dh
+        dh = torch.zeros(M, D, dtype=torch.float32, device=g2.device)
+        for c_i, c in enumerate("qkv"):
+            inp, z, mean, rstd, wl = sp[5 * c_i:5 * c_i + 5]
+            cp = getattr(a_, f"conv_proj_{c}")
+            lin = getattr(a_, f"proj_{c}")
+            dq = dqkv[:, c_i * D:(c_i + 1) * D].contiguous()
+            dinp = ops.linear_dgrad(dq, wl, F32)
+            ops.linear_wgrad(dq, inp, _grad(lin.weight))
+            if lin.bias is not None:
+                ops.bias_grad(dq, _grad(lin.bias))
+            if with_cls:
+                dh.view(B, N, D)[:, 0] += dinp.view(B, N, D)[:, 0]
+            dw9 = torch.zeros(9, D, dtype=torch.float32, device=g2.device)
+            ops.dwconv_bn_bwd(dinp, h, B, H, W, cp.w9(), cp.bn.weight, z, mean, rstd, dh, dw9,
+                              _grad(cp.bn.weight), _grad(cp.bn.bias), x_img=N, x_off=off, dy_img=N, dy_off=off)
+            _grad(cp.weight).add_(dw9.t().reshape(D, 1, 3, 3))
+        dx, _ = ops.layernorm_bwd(dh, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias), dres=dx1, lp_dtype=None)
+        return (dx.view(B, N, D), None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 5)
+
+
+class _CvTHeadFn(torch.autograd.Function):
+    """Dense(num_classes) on the normed features (models/CvT(Par).py:350) on the small-C head kernel."""
+
+    @staticmethod
+    def forward(ctx, y, head, w, b):
+        y = y.contiguous().float()
+        ctx.save_for_backward(y)
+        ctx.head = head
+        return ops.head_fwd(y, w.detach(), b)
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        (y,) = ctx.saved_tensors
+        head = ctx.head
+        dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), _grad(head.weight),
+                          _grad(head.bias) if head.bias is not None else None)
+        return dy, None, None, None
+
+
+# ======================================================================= stages + model
+class CvTStageModule(nn.Module):
+    def __init__(self, cin: int, st: CvTStage, cfg: CvTConfig):
+        super().__init__()
+        self.spec = st
+        self.embed = ConvEmbedSame(cin, st.embed_dim, st.patch_size, st.stride, st.padding, cfg.embed_norm,
+                                   cfg.ln_eps, cfg.dtype)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, st.embed_dim)) if st.with_cls_token else None
+        self.blocks = nn.ModuleList([CvTBlock(st.embed_dim, st.num_heads, cfg) for _ in range(st.depth)])
+
+
+class CvT(nn.Module):
+    """create_cvt_model's image branch (models/CvT(Par).py:292-340) + LN(cls) -> Dense head.
+    ``forward(x [B, Cin, S, S] fp32) -> logits [B, num_classes]``."""
+
+    def __init__(self, cfg: CvTConfig):
+        super().__init__()
+        self.cfg = cfg
+        cin = cfg.in_chans
+        for i, st in enumerate(cfg.stages):
+            self.add_module(f"stage{i}", CvTStageModule(cin, st, cfg))
+            cin = st.embed_dim
+        self.norm = LayerNorm(cin, cfg.ln_eps)
+        self.head = Linear(cin, cfg.num_classes)
+
+    def stages(self) -> List[CvTStageModule]:
+        return [getattr(self, f"stage{i}") for i in range(len(self.cfg.stages))]
+
+    def forward_features(self, img: Tensor) -> Tensor:
+        _check_cuda(img)
+        B, C, S, _ = img.shape
+        # NCHW image -> NHWC rows (Cin = 1 for the SLS grayscale input: a view)
+        x = img.float().reshape(B * S * S, 1) if C == 1 else img.float().permute(0, 2, 3, 1).reshape(B * S * S, C)
+        H, img_stride, row_off = S, S * S, 0
+        tok = None
+        t = None
+        for stg in self.stages():
+            st = stg.spec
+            t, H = stg.embed(x, B, H, img_stride, row_off)          # [B, H*H, D] fp32
+            D = st.embed_dim
+            if stg.cls_token is not None:
+                t = torch.cat([stg.cls_token.expand(B, 1, D), t], dim=1)
+            for blk in stg.blocks:
+                t = blk(t, H, H, stg.cls_token is not None)
+            N = t.shape[1]
+            if stg.cls_token is not None:
+                tok = t[:, 0]
+                img_stride, row_off = N, 1
+            else:
+                img_stride, row_off = N, 0
+            x = t.reshape(B * N, D)
+        if tok is None:
+            return self.norm(t).mean(dim=1)
+        return self.norm(tok)
+
+    def forward(self, img: Tensor) -> Tensor:
+        return _CvTHeadFn.apply(self.forward_features(img), self.head, self.head.weight, self.head.bias)
+
+    def load_param_dict(self, d: Dict[str, Tensor]) -> None:
+        mine = dict(self.named_parameters())
+        missing = set(mine) - set(d)
+        if missing:
+            raise KeyError(f"missing parameters: {sorted(missing)[:5]}")
+        with torch.no_grad():
+            for k, p in mine.items():
+                p.copy_(d[k].reshape(p.shape).to(p.device, p.dtype))

@@ -63,7 +63,7 @@ def _ws(nbytes: int, like: Tensor) -> Tensor:
 
 def _rows(t: Tensor) -> Tuple[int, int]:
     """(rows, row stride) of a tensor viewed as [rows, last-dim] with unit inner stride."""
-    if t.stride(-1) != 1:
+    if t.stride(-1) != 1 and t.shape[-1] != 1:
         raise RuntimeError("vitmi: last dim must be contiguous")
     return t.numel() // t.shape[-1], t.stride(-2) if t.dim() > 1 else t.shape[-1]
 
