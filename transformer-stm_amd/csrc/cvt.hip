@@ -102,17 +102,24 @@ __global__ void conv_col2im_kernel(ConvGeo g, const T* __restrict__ dp, int Kp, 
 
 // ---------------------------------------------------------------- depthwise 3x3 + BatchNorm
 // Thread (pixel lane pl, channel group cg) with cg = tid % C4 fixed for the whole grid-stride
-// loop: 256 / C4 pixels per block iteration (C4 divides 256).
+// loop: 256 / C4 pixels per block iteration (C4 divides 256).  Pixel indices are 32-bit
+// (n = B*H*W < 2^31, checked on the host): one (b, h, w) split per pixel, none per tap.
 struct DwGeo {
   int B, H, W, C;
   int64_t ldx, x_img, x_off;   // input rows (LN output; cls row skipped through x_off)
   int64_t ldz;                 // z / dz scratch rows: dense [B*H*W][C]
 };
 
-__device__ __forceinline__ int64_t dw_row(const DwGeo& g, int64_t p) {   // p = (b, h, w) linear
-  const int64_t hw = (int64_t)g.H * g.W;
-  return (p / hw) * g.x_img + g.x_off + p % hw;
+__device__ __forceinline__ void dw_split(const DwGeo& g, uint32_t p, uint32_t& b, int& h, int& w) {
+  const uint32_t hw = (uint32_t)g.H * (uint32_t)g.W;
+  b = p / hw;
+  const uint32_t r = p - b * hw;
+  h = (int)(r / (uint32_t)g.W);
+  w = (int)(r - (uint32_t)h * (uint32_t)g.W);
 }
+
+// first row of image b in a [.., ld] row buffer with images every img rows after off
+__device__ __forceinline__ int64_t img_row0(uint32_t b, int64_t img, int64_t off) { return (int64_t)b * img + off; }
 
 // z = dwconv3x3(x) (same padding) -> z scratch; per-block partial sum / sum of squares.
 __global__ __launch_bounds__(256) void dw_fwd_stats_kernel(DwGeo g, const float* __restrict__ x,
@@ -121,14 +128,16 @@ __global__ __launch_bounds__(256) void dw_fwd_stats_kernel(DwGeo g, const float*
   __shared__ f32x4 red[2][256];
   const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
   const int c = cg * 4;
-  const int64_t n = (int64_t)g.B * g.H * g.W;
+  const uint32_t n = (uint32_t)g.B * g.H * g.W;
   f32x4 wv[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) wv[k] = *(const f32x4*)(wt + k * g.C + c);
   f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t p = (int64_t)blockIdx.x * lanes + pl; p < n; p += (int64_t)gridDim.x * lanes) {
-    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H);
-    const int64_t base = p - (int64_t)h * g.W - w;   // (b, 0, 0)
+  for (uint32_t p = blockIdx.x * lanes + pl; p < n; p += gridDim.x * lanes) {
+    uint32_t b;
+    int h, w;
+    dw_split(g, p, b, h, w);
+    const float* xb = x + img_row0(b, g.x_img, g.x_off) * g.ldx + c;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -138,10 +147,10 @@ __global__ __launch_bounds__(256) void dw_fwd_stats_kernel(DwGeo g, const float*
       for (int j = 0; j < 3; ++j) {
         const int ww = w + j - 1;
         if (ww < 0 || ww >= g.W) continue;
-        acc += wv[i * 3 + j] * *(const f32x4*)(x + dw_row(g, base + (int64_t)hh * g.W + ww) * g.ldx + c);
+        acc += wv[i * 3 + j] * *(const f32x4*)(xb + (int64_t)(hh * g.W + ww) * g.ldx);
       }
     }
-    *(f32x4*)(z + p * g.ldz + c) = acc;
+    *(f32x4*)(z + (int64_t)p * g.ldz + c) = acc;
     s1 += acc;
     s2 += acc * acc;
   }
@@ -158,21 +167,44 @@ __global__ __launch_bounds__(256) void dw_fwd_stats_kernel(DwGeo g, const float*
   }
 }
 
-// Fold the G block partials (fixed order) into mean / rstd; update the moving statistics.
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int G, int C, int64_t n, float eps,
-                                   float momentum, float* __restrict__ mean, float* __restrict__ rstd,
-                                   float* __restrict__ run_mean, float* __restrict__ run_var, int training) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Fixed-order fp64 sum over the G rows of column col of part[G][ld] by a 1024-thread block laid
+// out as 16 columns x 64 row groups (LDS tree in a fixed order: deterministic).  Every thread
+// of the block must call it; the result is valid in all threads of the column.
+constexpr int RED_COLS = 16, RED_ROWS = 64;
+__device__ __forceinline__ double block_colsum(const float* __restrict__ part, int G, int64_t ld, int col,
+                                               bool valid, double* red) {
+  const int cl = threadIdx.x % RED_COLS, rg = threadIdx.x / RED_COLS;
+  double s = 0.0;
+  if (valid) {
+#pragma unroll 4
+    for (int b = rg; b < G; b += RED_ROWS) s += part[(int64_t)b * ld + col];
+  }
+  red[rg * RED_COLS + cl] = s;
+  __syncthreads();
+  for (int st = RED_ROWS / 2; st > 0; st >>= 1) {
+    if (rg < st) red[rg * RED_COLS + cl] += red[(rg + st) * RED_COLS + cl];
+    __syncthreads();
+  }
+  const double r = red[cl];
+  __syncthreads();
+  return r;
+}
+
+// Fold the G block partials into mean / rstd; update the moving statistics.
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ part, int G, int C, int64_t n,
+                                                           float eps, float momentum, float* __restrict__ mean,
+                                                           float* __restrict__ rstd, float* __restrict__ run_mean,
+                                                           float* __restrict__ run_var, int training) {
+  __shared__ double red[RED_ROWS * RED_COLS];
+  const int c = blockIdx.x * RED_COLS + threadIdx.x % RED_COLS;
+  const bool ok = c < C;
+  const double s1 = block_colsum(part, G, 2 * C, c, training && ok, red);
+  const double s2 = block_colsum(part, G, 2 * C, C + c, training && ok, red);
+  if (threadIdx.x >= RED_COLS || !ok) return;
   if (!training) {   // inference: the moving statistics
     mean[c] = run_mean[c];
     rstd[c] = (float)(1.0 / sqrt((double)run_var[c] + (double)eps));
     return;
-  }
-  double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < G; ++b) {
-    s1 += part[(int64_t)b * 2 * C + c];
-    s2 += part[(int64_t)b * 2 * C + C + c];
   }
   const double mu = s1 / (double)n;
   double var = s2 / (double)n - mu * mu;
@@ -189,15 +221,15 @@ __global__ void bn_apply_kernel(DwGeo g, const float* __restrict__ z, const floa
                                 const float* __restrict__ rstd, const float* __restrict__ gamma,
                                 const float* __restrict__ beta, TY* __restrict__ y, int64_t ldy, int64_t y_img,
                                 int64_t y_off) {
-  const int C4 = g.C / 4;
-  const int64_t hw = (int64_t)g.H * g.W, total = (int64_t)g.B * hw * C4;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+  const uint32_t C4 = g.C / 4, hw = (uint32_t)g.H * g.W;
+  const uint32_t total = (uint32_t)g.B * hw * C4;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int c = (int)(t % C4) * 4;
-    const int64_t p = t / C4;
-    const f32x4 zv = *(const f32x4*)(z + p * g.ldz + c);
+    const uint32_t p = t / C4, b = p / hw;
+    const f32x4 zv = *(const f32x4*)(z + (int64_t)p * g.ldz + c);
     const f32x4 o = (zv - *(const f32x4*)(mean + c)) * *(const f32x4*)(rstd + c) * *(const f32x4*)(gamma + c) +
                     *(const f32x4*)(beta + c);
-    TY* d = y + ((p / hw) * y_img + y_off + p % hw) * ldy + c;
+    TY* d = y + (img_row0(b, y_img, y_off) + (p - b * hw)) * ldy + c;
 #pragma unroll
     for (int e = 0; e < 4; ++e) d[e] = from_f32<TY>(o[e]);
   }
@@ -214,15 +246,16 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(DwGeo g, const TD* __
   __shared__ f32x4 red[2][256];
   const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
   const int c = cg * 4;
-  const int64_t hw = (int64_t)g.H * g.W, n = (int64_t)g.B * hw;
+  const uint32_t hw = (uint32_t)g.H * g.W, n = (uint32_t)g.B * hw;
   const f32x4 mu = *(const f32x4*)(mean + c), rs = *(const f32x4*)(rstd + c);
   f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t p = (int64_t)blockIdx.x * lanes + pl; p < n; p += (int64_t)gridDim.x * lanes) {
-    const TD* src = dy + ((p / hw) * dy_img + dy_off + p % hw) * lddy + c;
+  for (uint32_t p = blockIdx.x * lanes + pl; p < n; p += gridDim.x * lanes) {
+    const uint32_t b = p / hw;
+    const TD* src = dy + (img_row0(b, dy_img, dy_off) + (p - b * hw)) * lddy + c;
     f32x4 d;
 #pragma unroll
     for (int e = 0; e < 4; ++e) d[e] = to_f32(src[e]);
-    const f32x4 zh = (*(const f32x4*)(z + p * g.ldz + c) - mu) * rs;
+    const f32x4 zh = (*(const f32x4*)(z + (int64_t)p * g.ldz + c) - mu) * rs;
     s1 += d;
     s2 += d * zh;
   }
@@ -240,16 +273,15 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(DwGeo g, const TD* __
 }
 
 // sums -> dgamma/dbeta (+=), and the per-channel constants of dz: k1 = mean(dy), k2 = mean(dy zhat)
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C, int64_t n,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ kk) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < G; ++b) {
-    s1 += part[(int64_t)b * 2 * C + c];
-    s2 += part[(int64_t)b * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C,
+                                                               int64_t n, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta, float* __restrict__ kk) {
+  __shared__ double red[RED_ROWS * RED_COLS];
+  const int c = blockIdx.x * RED_COLS + threadIdx.x % RED_COLS;
+  const bool ok = c < C;
+  const double s1 = block_colsum(part, G, 2 * C, c, ok, red);
+  const double s2 = block_colsum(part, G, 2 * C, C + c, ok, red);
+  if (threadIdx.x >= RED_COLS || !ok) return;
   if (dgamma) dgamma[c] += (float)s2;
   if (dbeta) dbeta[c] += (float)s1;
   kk[c] = (float)(s1 / (double)n);
@@ -270,23 +302,26 @@ __global__ __launch_bounds__(256) void dw_bwd_dz_kernel(DwGeo g, const TD* __res
   __shared__ f32x4 red[256];
   const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
   const int c = cg * 4;
-  const int64_t hw = (int64_t)g.H * g.W, n = (int64_t)g.B * hw;
+  const uint32_t n = (uint32_t)g.B * g.H * g.W;
   const f32x4 mu = *(const f32x4*)(mean + c), rs = *(const f32x4*)(rstd + c);
   const f32x4 gr = *(const f32x4*)(gamma + c) * rs;
   const f32x4 k1 = *(const f32x4*)(kk + c), k2 = *(const f32x4*)(kk + g.C + c);
   f32x4 dw[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) dw[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t p = (int64_t)blockIdx.x * lanes + pl; p < n; p += (int64_t)gridDim.x * lanes) {
-    const TD* src = dy + ((p / hw) * dy_img + dy_off + p % hw) * lddy + c;
+  for (uint32_t p = blockIdx.x * lanes + pl; p < n; p += gridDim.x * lanes) {
+    uint32_t b;
+    int h, w;
+    dw_split(g, p, b, h, w);
+    const int hw_i = h * g.W + w;
+    const TD* src = dy + (img_row0(b, dy_img, dy_off) + hw_i) * lddy + c;
     f32x4 d;
 #pragma unroll
     for (int e = 0; e < 4; ++e) d[e] = to_f32(src[e]);
-    const f32x4 zh = (*(const f32x4*)(z + p * g.ldz + c) - mu) * rs;
+    const f32x4 zh = (*(const f32x4*)(z + (int64_t)p * g.ldz + c) - mu) * rs;
     const f32x4 dzv = gr * (d - k1 - zh * k2);
-    *(f32x4*)(dz + p * g.ldz + c) = dzv;
-    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H);
-    const int64_t base = p - (int64_t)h * g.W - w;
+    *(f32x4*)(dz + (int64_t)p * g.ldz + c) = dzv;
+    const float* xb = x + img_row0(b, g.x_img, g.x_off) * g.ldx + c;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int hh = h + i - 1;
@@ -295,7 +330,7 @@ __global__ __launch_bounds__(256) void dw_bwd_dz_kernel(DwGeo g, const TD* __res
       for (int j = 0; j < 3; ++j) {
         const int ww = w + j - 1;
         if (ww < 0 || ww >= g.W) continue;
-        dw[i * 3 + j] += dzv * *(const f32x4*)(x + dw_row(g, base + (int64_t)hh * g.W + ww) * g.ldx + c);
+        dw[i * 3 + j] += dzv * *(const f32x4*)(xb + (int64_t)(hh * g.W + ww) * g.ldx);
       }
     }
   }
@@ -312,24 +347,27 @@ __global__ __launch_bounds__(256) void dw_bwd_dz_kernel(DwGeo g, const TD* __res
 }
 
 // dW[k][c] += sum over blocks of the partials (fixed order)
-__global__ void dw_wgrad_finalize_kernel(const float* __restrict__ part, int G, int C, float* __restrict__ dwt) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= 9 * C) return;
-  float s = 0.f;
-  for (int b = 0; b < G; ++b) s += part[(int64_t)b * 9 * C + e];
-  dwt[e] += s;
+__global__ __launch_bounds__(1024) void dw_wgrad_finalize_kernel(const float* __restrict__ part, int G, int C,
+                                                                 float* __restrict__ dwt) {
+  __shared__ double red[RED_ROWS * RED_COLS];
+  const int e = blockIdx.x * RED_COLS + threadIdx.x % RED_COLS;
+  const bool ok = e < 9 * C;
+  const double s = block_colsum(part, G, 9 * C, e, ok, red);
+  if (threadIdx.x < RED_COLS && ok) dwt[e] += (float)s;
 }
 
 // dx[p] += sum_{i,j} w[i][j] * dz[p - (i-1, j-1)]   (rows of dx like x's)
 __global__ void dw_bwd_dx_kernel(DwGeo g, const float* __restrict__ dz, const float* __restrict__ wt,
                                  float* __restrict__ dx) {
-  const int C4 = g.C / 4;
-  const int64_t total = (int64_t)g.B * g.H * g.W * C4;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+  const uint32_t C4 = g.C / 4;
+  const uint32_t total = (uint32_t)g.B * g.H * g.W * C4;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int c = (int)(t % C4) * 4;
-    const int64_t p = t / C4;
-    const int w = (int)(p % g.W), h = (int)((p / g.W) % g.H);
-    const int64_t base = p - (int64_t)h * g.W - w;
+    const uint32_t p = t / C4;
+    uint32_t b;
+    int h, w;
+    dw_split(g, p, b, h, w);
+    const float* zb = dz + ((int64_t)p - (h * g.W + w)) * g.ldz + c;   // (b, 0, 0)
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -339,10 +377,10 @@ __global__ void dw_bwd_dx_kernel(DwGeo g, const float* __restrict__ dz, const fl
       for (int j = 0; j < 3; ++j) {
         const int ww = w - j + 1;
         if (ww < 0 || ww >= g.W) continue;
-        acc += *(const f32x4*)(wt + (i * 3 + j) * g.C + c) * *(const f32x4*)(dz + (base + (int64_t)hh * g.W + ww) * g.ldz + c);
+        acc += *(const f32x4*)(wt + (i * 3 + j) * g.C + c) * *(const f32x4*)(zb + (int64_t)(hh * g.W + ww) * g.ldz);
       }
     }
-    float* d = dx + dw_row(g, p) * g.ldx + c;
+    float* d = dx + (img_row0(b, g.x_img, g.x_off) + h * g.W + w) * g.ldx + c;
     *(f32x4*)d = *(const f32x4*)d + acc;
   }
 }
@@ -356,7 +394,7 @@ static unsigned grid_of(int64_t work, int per_block = 256, int cap = 4096) {
 static int dw_blocks(int64_t n, int C) {
   const int lanes = 256 / (C / 4);
   int64_t gsz = (n + lanes * 8 - 1) / (lanes * 8);   // >= 8 pixels per thread
-  if (gsz > 512) gsz = 512;
+  if (gsz > 1024) gsz = 1024;
   return (int)(gsz < 1 ? 1 : gsz);
 }
 
@@ -441,7 +479,7 @@ extern "C" int vitmi_conv_col2im(int dtype, int B, int H, int W, int C, int kh, 
 }
 
 static int make_dw(DwGeo& g, int B, int H, int W, int C, int64_t ldx, int64_t x_img, int64_t x_off) {
-  VITMI_CHECK_ARG(B > 0 && H > 0 && W > 0, "dwconv: bad sizes");
+  VITMI_CHECK_ARG(B > 0 && H > 0 && W > 0 && (int64_t)B * H * W * (C / 4) < (1LL << 31), "dwconv: bad sizes");
   VITMI_CHECK_ARG(dw_channels_ok(C), "dwconv: C must be a multiple of 4 dividing 1024 (got %d)", C);
   VITMI_CHECK_ARG(ldx % 4 == 0 && ldx >= C && x_img >= (int64_t)H * W + x_off && x_off >= 0, "dwconv: bad row layout");
   g.B = B; g.H = H; g.W = W; g.C = C; g.ldx = ldx; g.x_img = x_img; g.x_off = x_off; g.ldz = C;
@@ -472,7 +510,7 @@ extern "C" int vitmi_dwconv_bn_fwd(int B, int H, int W, int C, const float* x, i
   const int G = dw_blocks(n, C);
   float* part = (float*)workspace;
   hipLaunchKernelGGL(dw_fwd_stats_kernel, dim3(G), dim3(256), 0, st, g, x, wt, z, part);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, st, (const float*)part, G, C, n, eps,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + RED_COLS - 1) / RED_COLS), dim3(1024), 0, st, (const float*)part, G, C, n, eps,
                      momentum, mean, rstd, run_mean, run_var, training);
   const int64_t work = n * (C / 4);
   if (y_dtype == VITMI_BF16)
@@ -508,7 +546,7 @@ extern "C" int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, i
     hipLaunchKernelGGL(bn_bwd_stats_kernel<float>, dim3(G), dim3(256), 0, st, g, (const float*)dy, lddy, dy_img,
                        dy_off, z, mean, rstd, part);
   }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, st, (const float*)part, G, C, n,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + RED_COLS - 1) / RED_COLS), dim3(1024), 0, st, (const float*)part, G, C, n,
                      dgamma, dbeta, kk);
   if (dy_dtype == VITMI_BF16)
     hipLaunchKernelGGL(dw_bwd_dz_kernel<bf16>, dim3(G), dim3(256), 0, st, g, (const bf16*)dy, lddy, dy_img, dy_off, z,
@@ -516,7 +554,7 @@ extern "C" int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, i
   else
     hipLaunchKernelGGL(dw_bwd_dz_kernel<float>, dim3(G), dim3(256), 0, st, g, (const float*)dy, lddy, dy_img, dy_off,
                        z, x, mean, rstd, gamma, (const float*)kk, dz, part);
-  hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3((9 * C + 255) / 256), dim3(256), 0, st, (const float*)part, G, C,
+  hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3((9 * C + RED_COLS - 1) / RED_COLS), dim3(1024), 0, st, (const float*)part, G, C,
                      dwt);
   hipLaunchKernelGGL(dw_bwd_dx_kernel, dim3(grid_of(n * (C / 4))), dim3(256), 0, st, g, (const float*)dz, wt, dx);
   VITMI_LAUNCH_CHECK("dwconv_bn_bwd");

@@ -378,6 +378,32 @@ class CvT(nn.Module):
     def forward(self, img: Tensor) -> Tensor:
         return _CvTHeadFn.apply(self.forward_features(img), self.head, self.head.weight, self.head.bias)
 
+    def reset_parameters(self, seed: int = 0) -> None:
+        """Keras initialisers: glorot_uniform kernels (Dense, Conv2D, DepthwiseConv2D), zero
+        biases / betas, unit gammas, cls token ~ N(0, 0.02)."""
+        g = torch.Generator().manual_seed(seed)
+        with torch.no_grad():
+            for name, p in self.named_parameters():
+                leaf, parent = name.rsplit(".", 1)[-1], name.split(".")[-2]
+                if parent in ("norm1", "norm2", "norm", "bn"):
+                    t = torch.ones(p.shape) if leaf == "weight" else torch.zeros(p.shape)
+                elif leaf == "bias":
+                    t = torch.zeros(p.shape)
+                elif leaf == "cls_token":
+                    t = 0.02 * torch.randn(p.shape, generator=g)
+                else:
+                    rf = p.shape[2] * p.shape[3] if p.dim() == 4 else 1
+                    fan_in, fan_out = p.shape[1] * rf, p.shape[0] * rf
+                    if "conv_proj" in name:               # depthwise: one input channel per filter
+                        fan_in, fan_out = rf, rf
+                    lim = (6.0 / (fan_in + fan_out)) ** 0.5
+                    t = (torch.rand(p.shape, generator=g) * 2 - 1) * lim
+                p.copy_(t.to(p.device))
+            for m in self.modules():
+                if isinstance(m, _BN):
+                    m.running_mean.zero_()
+                    m.running_var.fill_(1.0)
+
     def load_param_dict(self, d: Dict[str, Tensor]) -> None:
         mine = dict(self.named_parameters())
         missing = set(mine) - set(d)
