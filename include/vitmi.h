@@ -218,6 +218,31 @@ int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, int dy_dtype
                         float* dw, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
                         vitmi_stream_t stream);
 
+/* Projection(method='avg') (models/CvT(Par).py:95-96,107-108): AveragePooling2D(pool 3,
+ * stride 1, padding 'same') over [B, H, W, C] token rows laid out like vitmi_dwconv_bn_fwd's
+ * (image b pixel p at row b*x_img + x_off + p), the mean over the in-bounds taps (TF 'same'
+ * pooling excludes the padding from the divisor; count_pad=1: always 9, torch's AvgPool2d as in
+ * old_codes/MS_CvT.py:145-153).  y (bf16 | f32) rows likewise.  The
+ * backward ACCUMULATES dx += pool^T(dy).  C % 4 == 0, 1024 % C == 0. */
+int vitmi_avgpool3_fwd(int B, int H, int W, int C, const float* x, int64_t ldx, int64_t x_img, int64_t x_off,
+                       void* y, int y_dtype, int64_t ldy, int64_t y_img, int64_t y_off, int count_pad,
+                       vitmi_stream_t stream);
+int vitmi_avgpool3_bwd(int B, int H, int W, int C, const void* dy, int dy_dtype, int64_t lddy, int64_t dy_img,
+                       int64_t dy_off, float* dx, int64_t ldx, int64_t x_img, int64_t x_off, int count_pad,
+                       vitmi_stream_t stream);
+
+/* Small fp32 Dense layers: Proc_Dense_1/2 = layers.Dense(256, activation='relu') on the
+ * standardised process parameters (models/CvT(Par).py:343-344).  y = act(x W^T + b),
+ * act 0 = linear, 1 = relu; x [M][ldx], W [N][K] fp32, y [M][ldy].  The backward takes the
+ * forward's output y (the relu mask), writes dx = (dy * act'(y)) W when dx != NULL and
+ * ACCUMULATES dW += (dy * act'(y))^T x, db += column sums (db may be NULL).  Exact fp32 FMA
+ * in a fixed order (deterministic). */
+int vitmi_dense_f32_fwd(int M, int N, int K, const float* x, int64_t ldx, const float* w, const float* b, float* y,
+                        int64_t ldy, int act, vitmi_stream_t stream);
+int vitmi_dense_f32_bwd(int M, int N, int K, const float* dy, int64_t lddy, const float* y, int64_t ldy,
+                        const float* x, int64_t ldx, const float* w, float* dx, int64_t lddx, float* dw, float* db,
+                        int act, vitmi_stream_t stream);
+
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
 

@@ -24,8 +24,10 @@ stage    ConvEmbed (Conv2D 'same', ``:194-217``)      ConvTransformerBlock (``:2
   build holds the composition ``proj_{q,k,v}``), softmax(QK^T / sqrt(D/H)) V, output Dense
   composed with ``self.proj`` into ``proj``.
 * block: ``x += Attn(LN1(x)); x += MLP(LN1(x))`` with the SAME norm1 used twice (``:248,272,278``).
-* head: LN(cls) (eps 1e-6, ``:328``) -> Dense(num_classes).  The reference concatenates a
-  process-parameter MLP before its Dense(1) (``:343-350``, SURVEY §8f row 2, not built yet).
+* ``Projection('avg')``: AveragePooling2D(3, 1, 'same') for k and v, q stays linear
+  (``:95-96,107-108,130-132``); ``'linear'``: identity (``qkv_method`` per stage).
+* head: LN(cls) (eps 1e-6, ``:328``) [ ++ the process-parameter MLP Dense(256, relu) x 2,
+  ``:343-347``, when ``proc_dim`` > 0, SURVEY §8f row 2 ] -> Dense(num_classes) (``:350``).
 
 Knobs (``CvTConfig``) cover MS_CvT's semantics too (``old_codes/MS_CvT.py``: symmetric conv
 padding, embed LayerNorm, attention scale 1/sqrt(D) ``:100``, no q/k/v bias ``:82``, BN eps 1e-5,
@@ -53,6 +55,7 @@ class CvTStage:
     with_cls_token: bool = False
     depth: int = 1
     padding: Optional[int] = None    # None: TF 'same'; an int: symmetric (MS_CvT PATCH_PADDING)
+    qkv_method: str = "dw_bn"        # 'dw_bn' | 'avg' (q stays 'linear') | 'linear'  (:25,83-112,130-132)
 
 
 def keras_spec() -> List[CvTStage]:
@@ -74,6 +77,9 @@ class CvTConfig:
     qkv_bias: bool = True
     tie_norms: bool = True
     embed_norm: bool = False
+    avg_count_pad: bool = False       # 'avg' divisor: False = TF 'same' in-bounds count; True = torch's 9
+    proc_dim: int = 0                 # process parameters (5 in the reference, :392); 0 = image only
+    proc_hidden: int = 256            # Proc_Dense_1/2 width (:343-344)
     dtype: str = "bf16"
 
     def replace(self, **kw) -> "CvTConfig":
@@ -108,9 +114,10 @@ def param_shapes(cfg: CvTConfig) -> Dict[str, tuple]:
             s[b + "norm1.weight"] = (D,)
             s[b + "norm1.bias"] = (D,)
             for c in "qkv":
-                s[b + f"attn.conv_proj_{c}.weight"] = (D, 1, 3, 3)
-                s[b + f"attn.conv_proj_{c}.bn.weight"] = (D,)
-                s[b + f"attn.conv_proj_{c}.bn.bias"] = (D,)
+                if st.qkv_method == "dw_bn":
+                    s[b + f"attn.conv_proj_{c}.weight"] = (D, 1, 3, 3)
+                    s[b + f"attn.conv_proj_{c}.bn.weight"] = (D,)
+                    s[b + f"attn.conv_proj_{c}.bn.bias"] = (D,)
                 s[b + f"attn.proj_{c}.weight"] = (D, D)
                 if cfg.qkv_bias:
                     s[b + f"attn.proj_{c}.bias"] = (D,)
@@ -128,9 +135,24 @@ def param_shapes(cfg: CvTConfig) -> Dict[str, tuple]:
     D = cfg.stages[-1].embed_dim
     s["norm.weight"] = (D,)
     s["norm.bias"] = (D,)
+    if cfg.proc_dim:
+        Hp = cfg.proc_hidden
+        s["proc.fc1.weight"] = (Hp, cfg.proc_dim)
+        s["proc.fc1.bias"] = (Hp,)
+        s["proc.fc2.weight"] = (Hp, Hp)
+        s["proc.fc2.bias"] = (Hp,)
+        D += Hp
     s["head.weight"] = (cfg.num_classes, D)
     s["head.bias"] = (cfg.num_classes,)
     return s
+
+
+def qkv_methods(st: CvTStage) -> Tuple[str, str, str]:
+    """Per-projection methods: 'avg' keeps q linear (models/CvT(Par).py:130-132)."""
+    m = st.qkv_method
+    if m not in ("dw_bn", "avg", "linear"):
+        raise ValueError(f"unknown qkv_method {m}")
+    return ("linear" if m == "avg" else m, m, m)
 
 
 def init_params(cfg: CvTConfig, seed: int = 0) -> Dict[str, Tensor]:
@@ -181,9 +203,14 @@ def block(x: Tensor, hw: Tuple[int, int], p: Dict[str, Tensor], pre: str, cfg: C
     cls, sp = (h[:, :1], h[:, 1:]) if st.with_cls_token else (None, h)
     img = sp.transpose(1, 2).reshape(B, D, H, W)
     proj = []
-    for c in "qkv":
+    for c, m in zip("qkv", qkv_methods(st)):
         a = pre + f"attn.conv_proj_{c}."
-        t = dw_bn(img, p[a + "weight"], p[a + "bn.weight"], p[a + "bn.bias"], cfg.bn_eps)
+        if m == "dw_bn":
+            t = dw_bn(img, p[a + "weight"], p[a + "bn.weight"], p[a + "bn.bias"], cfg.bn_eps)
+        elif m == "avg":   # AveragePooling2D(3, 1, 'same') (:95-96,107-108)
+            t = F.avg_pool2d(img, 3, 1, 1, count_include_pad=cfg.avg_count_pad)
+        else:
+            t = img
         t = t.flatten(2).transpose(1, 2)
         if cls is not None:
             t = torch.cat([cls, t], dim=1)
@@ -223,8 +250,18 @@ def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig) -> Tenso
     return F.layer_norm(tok, (tok.shape[-1],), p["norm.weight"], p["norm.bias"], cfg.ln_eps)
 
 
-def forward(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig) -> Tensor:
-    return F.linear(forward_features(img, p, cfg), p["head.weight"], p["head.bias"])
+def proc_features(proc: Tensor, p: Dict[str, Tensor]) -> Tensor:
+    """Proc_Dense_1/2: Dense(256, relu) x 2 on the standardised process parameters (:343-344)."""
+    h = F.relu(F.linear(proc, p["proc.fc1.weight"], p["proc.fc1.bias"]))
+    return F.relu(F.linear(h, p["proc.fc2.weight"], p["proc.fc2.bias"]))
+
+
+def forward(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, proc: Optional[Tensor] = None) -> Tensor:
+    """Image features (+ concatenated process features, :347) -> Final_Dense (:350)."""
+    f = forward_features(img, p, cfg)
+    if cfg.proc_dim:
+        f = torch.cat([f, proc_features(proc, p)], dim=1)
+    return F.linear(f, p["head.weight"], p["head.bias"])
 
 
 def loss_fn(logits: Tensor, target: Tensor, num_classes: int) -> Tensor:
@@ -233,12 +270,19 @@ def loss_fn(logits: Tensor, target: Tensor, num_classes: int) -> Tensor:
     return F.cross_entropy(logits, target.long())
 
 
-def forward_backward(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg: CvTConfig):
+def forward_backward(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg: CvTConfig,
+                     proc: Optional[Tensor] = None):
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    logits = forward(img, leaves, cfg)
+    logits = forward(img, leaves, cfg, proc)
     loss = loss_fn(logits, target, cfg.num_classes)
     loss.backward()
     return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}
+
+
+def synthetic_proc(cfg: CvTConfig, batch: int, seed: int = 4321) -> Tensor:
+    """Standardised process parameters (zero mean / unit variance like StandardScaler, :402-403)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(batch, cfg.proc_dim, generator=g)
 
 
 def synthetic_batch(cfg: CvTConfig, batch: int, seed: int = 1234):

@@ -177,6 +177,38 @@ def gen_mscvt_cvt():
     save(os.path.join(HERE, "mscvt_cvt_dwbn.npz"), img, tgt, params, logits, loss, grads)
 
 
+def gen_mscvt_cvt_avg():
+    """``mscvt_cvt_avg.npz``: as ``gen_mscvt_cvt`` with the other two q/k/v projection methods
+    (``old_codes/MS_CvT.py:145-157``): 'avg' in both stages (AvgPool2d(3, 1, 1) on k and v, q
+    'linear' = identity), the cls token in stage 2.  (An all-'linear' stage cannot run in
+    MS_CvT: ``Attention.forward`` reads q before assignment when no conv_proj exists, ``:190-198``.)"""
+    ms = load_mscvt()
+    spec = {
+        "NUM_STAGES": 2, "PATCH_SIZE": [7, 3], "PATCH_STRIDE": [4, 2], "PATCH_PADDING": [2, 1],
+        "DIM_EMBED": [64, 128], "DEPTH": [1, 1], "NUM_HEADS": [1, 2], "MLP_RATIO": [4.0, 4.0],
+        "QKV_BIAS": [False, False], "DROP_RATE": [0.0, 0.0], "ATTN_DROP_RATE": [0.0, 0.0],
+        "DROP_PATH_RATE": [0.0, 0.0], "CLS_TOKEN": [False, True], "QKV_PROJ_METHOD": ["avg", "avg"],
+        "KERNEL_QKV": [3, 3], "PADDING_Q": [1, 1], "PADDING_KV": [1, 1], "STRIDE_KV": [1, 1], "STRIDE_Q": [1, 1],
+    }
+    torch.manual_seed(0)
+    model = ms.ConvolutionalVisionTransformer(in_chans=1, num_classes=2, act_layer=nn.GELU,
+                                              norm_layer=partial(nn.LayerNorm, eps=1e-5), spec=spec)
+    randomize_(model, 7)
+    model.train()
+    g = torch.Generator().manual_seed(8)
+    img = torch.rand(4, 1, 32, 32, generator=g)
+    tgt = torch.randint(0, 2, (4,), generator=g)
+    logits = model(img)
+    loss = nn.functional.cross_entropy(logits, tgt)
+    loss.backward()
+    params, grads = {}, {}
+    for name, p in model.named_parameters():
+        n = name.replace(".patch_embed.proj.", ".embed.").replace(".patch_embed.norm.", ".embed.norm.")
+        params[n] = p
+        grads[n] = p.grad
+    save(os.path.join(HERE, "mscvt_cvt_avg.npz"), img, tgt, params, logits, loss, grads)
+
+
 def gen_hf():
     from transformers import ViTConfig as HFConfig, ViTForImageClassification
     D, H, depth, P, img_size = 128, 2, 2, 8, 32
@@ -231,5 +263,6 @@ if __name__ == "__main__":
         if "--cvt-only" not in sys.argv:
             gen_mscvt()
         gen_mscvt_cvt()
+        gen_mscvt_cvt_avg()
     else:
         print("reference absent; MS_CvT fixture not regenerated")

@@ -4,6 +4,8 @@ tests/golden/gen_golden.py): dw_bn q/k/v projections (depthwise 3x3 + training-m
 BatchNorm), strided overlapping conv embeddings, a cls token in the last stage.  No GPU."""
 import os
 
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
@@ -11,6 +13,7 @@ import torch
 from oracle import cvt_ref
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "mscvt_cvt_dwbn.npz")
+GOLD_AVG = os.path.join(os.path.dirname(__file__), "golden", "mscvt_cvt_avg.npz")
 
 
 def mscvt_cfg():
@@ -24,8 +27,15 @@ def mscvt_cfg():
         dtype="fp32")
 
 
-def load():
-    z = np.load(GOLD)
+def mscvt_avg_cfg():
+    """mscvt_cfg with the 'avg' q/k/v projection in both stages (torch AvgPool2d counts the
+    padding: avg_count_pad)."""
+    c = mscvt_cfg()
+    return c.replace(stages=[dataclasses.replace(s, qkv_method="avg") for s in c.stages], avg_count_pad=True)
+
+
+def load(path=GOLD):
+    z = np.load(path)
     params = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p::")}
     grads = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("g::")}
     return (torch.from_numpy(z["input"]), torch.from_numpy(z["target"]), params,
@@ -66,3 +76,39 @@ def test_keras_spec_shapes():
     img, tgt = cvt_ref.synthetic_batch(cfg, 2)
     out = cvt_ref.forward(img, p, cfg)
     assert out.shape == (2, 1)
+
+
+def test_cvt_oracle_matches_mscvt_avg_golden():
+    img, tgt, params, logits_ref, loss_ref, grads_ref = load(GOLD_AVG)
+    cfg = mscvt_avg_cfg()
+    assert set(cvt_ref.param_shapes(cfg)) == set(params)
+    logits, loss, grads = cvt_ref.forward_backward(img, tgt, params, cfg)
+    assert (logits - logits_ref).abs().max().item() < 1e-5
+    assert abs(loss.item() - loss_ref) < 1e-5
+    for k, g in grads_ref.items():
+        den = max(g.norm().item(), 1e-4)
+        assert (grads[k] - g).norm().item() / den < 1e-4, k
+
+
+def test_avg_projection_same_padding_divisor():
+    # TF AveragePooling2D 'same' divides by the in-bounds count: a constant image stays constant
+    cfg = cvt_ref.CvTConfig(img_size=32, stages=[cvt_ref.CvTStage(64, 7, 4, 1, qkv_method="avg")])
+    x = torch.ones(1, 4, 5, 5)
+    y = torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=cfg.avg_count_pad)
+    assert torch.allclose(y, x)
+    assert cvt_ref.qkv_methods(cfg.stages[0]) == ("linear", "avg", "avg")
+
+
+def test_proc_head_is_concat_then_dense():
+    """models/CvT(Par).py:343-350: Dense(256, relu) x 2 on the process parameters, concatenated
+    AFTER the image features, then Final_Dense; restated with explicit matrices."""
+    cfg = cvt_ref.CvTConfig(img_size=32, proc_dim=5)
+    p = cvt_ref.init_params(cfg, 1)
+    img, _ = cvt_ref.synthetic_batch(cfg, 3)
+    proc = cvt_ref.synthetic_proc(cfg, 3)
+    f = cvt_ref.forward_features(img, p, cfg)
+    h = torch.clamp(proc @ p["proc.fc1.weight"].t() + p["proc.fc1.bias"], min=0)
+    h = torch.clamp(h @ p["proc.fc2.weight"].t() + p["proc.fc2.bias"], min=0)
+    W = p["head.weight"]
+    ref = f @ W[:, :f.shape[1]].t() + h @ W[:, f.shape[1]:].t() + p["head.bias"]
+    assert torch.allclose(cvt_ref.forward(img, p, cfg, proc), ref, atol=1e-5)

@@ -135,3 +135,34 @@ def test_dwconv_bn_inference_uses_moving_stats():
     z = F.conv2d(x.view(B, H, H, C).permute(0, 3, 1, 2), w, None, padding=1, groups=C)
     ref = F.batch_norm(z, rm, rv, gamma, beta, training=False, eps=1e-3).permute(0, 2, 3, 1).reshape(-1, C)
     assert rel(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize("B,H,C,cls,count_pad", [(3, 8, 64, False, False), (2, 7, 128, True, False),
+                                                 (2, 16, 64, False, True), (2, 5, 256, True, True)])
+def test_avgpool3_fwd_bwd(B, H, C, cls, count_pad):
+    """Projection('avg') (models/CvT(Par).py:95-96): 3x3 stride-1 'same' average pooling; the
+    TF divisor counts in-bounds taps, count_pad divides by 9 (torch, MS_CvT)."""
+    g = torch.Generator().manual_seed(4)
+    N = H * H + (1 if cls else 0)
+    off = 1 if cls else 0
+    x = torch.randn(B, N, C, generator=g)
+    xs = x[:, off:].reshape(B, H, H, C).permute(0, 3, 1, 2).clone().requires_grad_(True)
+    ref = F.avg_pool2d(xs, 3, 1, 1, count_include_pad=count_pad)
+    dy = torch.randn_like(ref)
+    (ref * dy).sum().backward()
+    y = torch.zeros(B, N, C, device=DEV, dtype=torch.float32)
+    ops.avgpool3_fwd(x.to(DEV).view(-1, C), B, H, H, y.view(-1, C), x_img=N, x_off=off, y_img=N, y_off=off,
+                     count_pad=count_pad)
+    assert rel(y[:, off:].reshape(B, H, H, C), ref.detach().permute(0, 2, 3, 1)) < 1e-6
+    dyd = torch.zeros(B, N, C, device=DEV)
+    dyd[:, off:] = dy.permute(0, 2, 3, 1).reshape(B, H * H, C).to(DEV)
+    dx = torch.ones(B, N, C, device=DEV)
+    ops.avgpool3_bwd(dyd.view(-1, C), B, H, H, dx.view(-1, C), dy_img=N, dy_off=off, x_img=N, x_off=off,
+                     count_pad=count_pad)
+    assert rel(dx[:, off:].reshape(B, H, H, C) - 1, xs.grad.permute(0, 2, 3, 1)) < 1e-6
+    if cls:
+        assert torch.equal(dx[:, 0], torch.ones(B, C, device=DEV))
+    yb = torch.zeros(B, N, C, device=DEV, dtype=torch.bfloat16)
+    ops.avgpool3_fwd(x.to(DEV).view(-1, C), B, H, H, yb.view(-1, C), x_img=N, x_off=off, y_img=N, y_off=off,
+                     count_pad=count_pad)
+    assert torch.equal(yb.float(), y.to(torch.bfloat16).float())

@@ -32,16 +32,25 @@ def mscvt_cfg():
     return m()
 
 
+def mscvt_avg_cfg():
+    from test_cvt_oracle import mscvt_avg_cfg as m
+    return m()
+
+
+def with_method(ocfg, method):
+    return ocfg.replace(stages=[dataclasses.replace(s, qkv_method=method) for s in ocfg.stages])
+
+
 def rel(a, b, floor=1e-12):
     a, b = a.detach().double().cpu(), b.detach().double().cpu()
     return ((a - b).norm() / max(b.norm().item(), floor)).item()
 
 
-def run_product(pcfg, params, img, tgt):
+def run_product(pcfg, params, img, tgt, proc=None):
     model = cvt.CvT(pcfg).to(DEV)
     model.load_param_dict(params)
     model.train()
-    logits = model(img.to(DEV))
+    logits = model(img.to(DEV), None if proc is None else proc.to(DEV))
     if pcfg.num_classes == 1:
         loss = mse_loss(logits, tgt.to(DEV))
     else:
@@ -54,20 +63,23 @@ def run_product(pcfg, params, img, tgt):
 
 def test_param_names_match_oracle():
     # pure host check (no kernels): the module tree names every oracle parameter
-    for ocfg in (mscvt_cfg(), cvt_ref.CvTConfig(img_size=64)):
+    for ocfg in (mscvt_cfg(), cvt_ref.CvTConfig(img_size=64), mscvt_avg_cfg(),
+                 with_method(cvt_ref.CvTConfig(img_size=64, proc_dim=5), "linear")):
         model = cvt.CvT(product_cfg(ocfg))
         shapes = {k: tuple(p.shape) for k, p in model.named_parameters()}
         assert shapes == {k: tuple(s) for k, s in cvt_ref.param_shapes(ocfg).items()}
 
 
 @pytest.mark.gpu
-def test_cvt_matches_mscvt_golden_fp32():
+@pytest.mark.parametrize("fixture", ["dwbn", "avg"])
+def test_cvt_matches_mscvt_golden_fp32(fixture):
     import os
-    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "mscvt_cvt_dwbn.npz"))
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", f"mscvt_cvt_{fixture}.npz"))
     params = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p::")}
     gref = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("g::")}
     img, tgt = torch.from_numpy(z["input"]), torch.from_numpy(z["target"])
-    _, logits, loss, grads = run_product(product_cfg(mscvt_cfg()), params, img, tgt)
+    ocfg = mscvt_cfg() if fixture == "dwbn" else mscvt_avg_cfg()
+    _, logits, loss, grads = run_product(product_cfg(ocfg), params, img, tgt)
     assert rel(logits, torch.from_numpy(z["logits"])) < 1e-4
     assert abs(loss.item() - float(z["loss"])) < 1e-4 * max(1.0, abs(float(z["loss"])))
     for k, g in gref.items():
@@ -75,14 +87,20 @@ def test_cvt_matches_mscvt_golden_fp32():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype,img_size,batch,ncls", [("fp32", 64, 4, 1), ("fp32", 64, 3, 3),
-                                                        ("bf16", 64, 4, 1), ("bf16", 128, 2, 2)])
-def test_cvt_keras_spec_vs_oracle(dtype, img_size, batch, ncls):
-    ocfg = cvt_ref.CvTConfig(img_size=img_size, num_classes=ncls, dtype="fp32")
+@pytest.mark.parametrize("dtype,img_size,batch,ncls,method,proc_dim", [
+    ("fp32", 64, 4, 1, "dw_bn", 0), ("fp32", 64, 3, 3, "dw_bn", 0), ("bf16", 64, 4, 1, "dw_bn", 0),
+    ("bf16", 128, 2, 2, "dw_bn", 0),
+    ("fp32", 64, 4, 1, "avg", 0), ("fp32", 64, 3, 1, "linear", 0), ("bf16", 64, 4, 1, "avg", 0),
+    # the reference's production model: dw_bn + the 5-parameter process MLP head (:343-350)
+    ("fp32", 64, 4, 1, "dw_bn", 5), ("bf16", 128, 4, 1, "dw_bn", 5)])
+def test_cvt_keras_spec_vs_oracle(dtype, img_size, batch, ncls, method, proc_dim):
+    ocfg = with_method(cvt_ref.CvTConfig(img_size=img_size, num_classes=ncls, dtype="fp32", proc_dim=proc_dim),
+                       method)
     params = cvt_ref.init_params(ocfg, seed=5)
     img, tgt = cvt_ref.synthetic_batch(ocfg, batch, seed=7)
-    logits_ref, loss_ref, gref = cvt_ref.forward_backward(img, tgt, params, ocfg)
-    _, logits, loss, grads = run_product(product_cfg(ocfg, dtype), params, img, tgt)
+    proc = cvt_ref.synthetic_proc(ocfg, batch) if proc_dim else None
+    logits_ref, loss_ref, gref = cvt_ref.forward_backward(img, tgt, params, ocfg, proc)
+    _, logits, loss, grads = run_product(product_cfg(ocfg, dtype), params, img, tgt, proc)
     tl, tg = (1e-4, 1e-3) if dtype == "fp32" else (3e-2, 8e-2)
     assert rel(logits, logits_ref) < tl
     assert abs(loss.item() - loss_ref.item()) < tl * max(1.0, abs(loss_ref.item()))
@@ -92,6 +110,8 @@ def test_cvt_keras_spec_vs_oracle(dtype, img_size, batch, ncls):
     # (the BN beta only in stages without a cls token: the cls key bypasses dw_bn)
     zero = [k for k in gref if k.endswith("attn.proj_k.bias") or (
         k.endswith("attn.conv_proj_k.bn.bias") and not ocfg.stages[int(k[5])].with_cls_token)]
+    # (the matching query bias exists only when the q projection has one)
+    zero = [k for k in zero if k.replace("_k.", "_q.") in gref]
     bad = {}
     for k, g in gref.items():
         if k in zero:
@@ -135,3 +155,25 @@ def test_cvt_moving_stats_and_eval_mode():
     assert torch.equal(bn.running_mean, rm) and torch.equal(bn.running_var, rv)
     assert torch.equal(l1, l2)
     assert rel(l1, logits_tr) > 1e-6      # moving stats after one step differ from the batch stats
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,act", [(256, 256, 5, 1), (7, 256, 256, 1), (33, 3, 17, 0)])
+def test_dense_f32_kernels(M, N, K, act):
+    """the small fp32 Dense kernels (Proc_Dense_1/2) vs torch fp32 autograd on the CPU"""
+    from vitmi import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    x, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / K ** 0.5, torch.randn(N, generator=g)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.linear(xr, wr, br)
+    if act:
+        yr = torch.relu(yr)
+    dy = torch.randn(M, N, generator=g)
+    (yr * dy).sum().backward()
+    y = ops.dense_f32_fwd(x.to(DEV), w.to(DEV), b.to(DEV), act)
+    dw, db = torch.ones(N, K, device=DEV), torch.zeros(N, device=DEV)
+    dx = ops.dense_f32_bwd(dy.to(DEV), y, x.to(DEV), w.to(DEV), dw, db, act)
+    assert rel(y, yr) < 1e-6
+    assert rel(dx, xr.grad) < 1e-6
+    assert rel(dw - 1, wr.grad) < 1e-6          # accumulates
+    assert rel(db, br.grad) < 1e-6

@@ -560,3 +560,113 @@ extern "C" int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, i
   VITMI_LAUNCH_CHECK("dwconv_bn_bwd");
   return VITMI_OK;
 }
+
+// ---------------------------------------------------------------- 'avg' projection
+// AveragePooling2D(pool 3, stride 1, padding 'same') (models/CvT(Par).py:95-96,107-108): the
+// mean over the in-bounds taps (TF 'same' pooling excludes the padding from the count); with
+// count_pad the divisor is always 9 (torch AvgPool2d(3, 1, 1), MS_CvT old_codes/MS_CvT.py:145-153).
+__device__ __forceinline__ float inb3(int i, int n) { return (float)(3 - (i == 0) - (i == n - 1)); }
+
+template <typename TY>
+__global__ void avgpool3_fwd_kernel(DwGeo g, const float* __restrict__ x, TY* __restrict__ y, int64_t ldy,
+                                    int64_t y_img, int64_t y_off, int count_pad) {
+  const uint32_t C4 = g.C / 4, hw = (uint32_t)g.H * g.W;
+  const uint32_t total = (uint32_t)g.B * hw * C4;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int c = (int)(t % C4) * 4;
+    uint32_t b;
+    int h, w;
+    dw_split(g, t / C4, b, h, w);
+    const float* xb = x + img_row0(b, g.x_img, g.x_off) * g.ldx + c;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = -1; i <= 1; ++i) {
+      const int hh = h + i;
+      if (hh < 0 || hh >= g.H) continue;
+#pragma unroll
+      for (int j = -1; j <= 1; ++j) {
+        const int ww = w + j;
+        if (ww < 0 || ww >= g.W) continue;
+        acc += *(const f32x4*)(xb + (int64_t)(hh * g.W + ww) * g.ldx);
+      }
+    }
+    acc *= count_pad ? 1.f / 9.f : 1.f / (inb3(h, g.H) * inb3(w, g.W));
+    TY* d = y + (img_row0(b, y_img, y_off) + h * g.W + w) * ldy + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] = from_f32<TY>(acc[e]);
+  }
+}
+
+// dx[p] += sum over the windows q containing p of dy[q] / count(q)
+template <typename TD>
+__global__ void avgpool3_bwd_kernel(DwGeo g, const TD* __restrict__ dy, int64_t lddy, int64_t dy_img,
+                                    int64_t dy_off, float* __restrict__ dx, int count_pad) {
+  const uint32_t C4 = g.C / 4, hw = (uint32_t)g.H * g.W;
+  const uint32_t total = (uint32_t)g.B * hw * C4;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int c = (int)(t % C4) * 4;
+    uint32_t b;
+    int h, w;
+    dw_split(g, t / C4, b, h, w);
+    const TD* db = dy + img_row0(b, dy_img, dy_off) * lddy + c;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = -1; i <= 1; ++i) {
+      const int hh = h + i;
+      if (hh < 0 || hh >= g.H) continue;
+#pragma unroll
+      for (int j = -1; j <= 1; ++j) {
+        const int ww = w + j;
+        if (ww < 0 || ww >= g.W) continue;
+        const TD* s = db + (int64_t)(hh * g.W + ww) * lddy;
+        const float r = count_pad ? 1.f / 9.f : 1.f / (inb3(hh, g.H) * inb3(ww, g.W));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += to_f32(s[e]) * r;
+      }
+    }
+    float* d = dx + (img_row0(b, g.x_img, g.x_off) + h * g.W + w) * g.ldx + c;
+    *(f32x4*)d = *(const f32x4*)d + acc;
+  }
+}
+
+extern "C" int vitmi_avgpool3_fwd(int B, int H, int W, int C, const float* x, int64_t ldx, int64_t x_img,
+                                  int64_t x_off, void* y, int y_dtype, int64_t ldy, int64_t y_img, int64_t y_off,
+                                  int count_pad, vitmi_stream_t stream) {
+  DwGeo g;
+  if (int rc = make_dw(g, B, H, W, C, ldx, x_img, x_off)) return rc;
+  VITMI_CHECK_ARG(x && y, "avgpool3_fwd: null pointer");
+  VITMI_CHECK_ARG(ldy % 4 == 0 && ldy >= C && y_img >= (int64_t)H * W + y_off && y_off >= 0,
+                  "avgpool3_fwd: bad output layout");
+  VITMI_CHECK_ARG(y_dtype == VITMI_BF16 || y_dtype == VITMI_F32, "avgpool3_fwd: bad dtype");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t work = (int64_t)B * H * W * (C / 4);
+  if (y_dtype == VITMI_BF16)
+    hipLaunchKernelGGL(avgpool3_fwd_kernel<bf16>, dim3(grid_of(work)), dim3(256), 0, st, g, x, (bf16*)y, ldy, y_img,
+                       y_off, count_pad);
+  else
+    hipLaunchKernelGGL(avgpool3_fwd_kernel<float>, dim3(grid_of(work)), dim3(256), 0, st, g, x, (float*)y, ldy, y_img,
+                       y_off, count_pad);
+  VITMI_LAUNCH_CHECK("avgpool3_fwd");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_avgpool3_bwd(int B, int H, int W, int C, const void* dy, int dy_dtype, int64_t lddy,
+                                  int64_t dy_img, int64_t dy_off, float* dx, int64_t ldx, int64_t x_img,
+                                  int64_t x_off, int count_pad, vitmi_stream_t stream) {
+  DwGeo g;
+  if (int rc = make_dw(g, B, H, W, C, ldx, x_img, x_off)) return rc;
+  VITMI_CHECK_ARG(dy && dx, "avgpool3_bwd: null pointer");
+  VITMI_CHECK_ARG(lddy % 4 == 0 && lddy >= C && dy_img >= (int64_t)H * W + dy_off && dy_off >= 0,
+                  "avgpool3_bwd: bad dy layout");
+  VITMI_CHECK_ARG(dy_dtype == VITMI_BF16 || dy_dtype == VITMI_F32, "avgpool3_bwd: bad dtype");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t work = (int64_t)B * H * W * (C / 4);
+  if (dy_dtype == VITMI_BF16)
+    hipLaunchKernelGGL(avgpool3_bwd_kernel<bf16>, dim3(grid_of(work)), dim3(256), 0, st, g, (const bf16*)dy, lddy,
+                       dy_img, dy_off, dx, count_pad);
+  else
+    hipLaunchKernelGGL(avgpool3_bwd_kernel<float>, dim3(grid_of(work)), dim3(256), 0, st, g, (const float*)dy, lddy,
+                       dy_img, dy_off, dx, count_pad);
+  VITMI_LAUNCH_CHECK("avgpool3_bwd");
+  return VITMI_OK;
+}

@@ -3,7 +3,7 @@
 ``create_cvt_model`` (``models/CvT(Par).py:292-354``) with the stage spec ``:66-72``: per stage a
 strided ``ConvEmbed`` (Conv2D 'same', ``:194-217``) and one ``ConvTransformerBlock``
 (``:231-289``) whose q/k/v come from ``Projection('dw_bn')`` (depthwise 3x3 + BatchNorm,
-``:83-112``) followed by the q/k/v Dense layers composed with MultiHeadAttention's own
+``:83-112``; or 'avg' pooling / 'linear' identity, ``qkv_method``) followed by the q/k/v Dense layers composed with MultiHeadAttention's own
 projections (``:132-137,178-185``).  Module tree and parameter names follow MS_CvT's
 ``ConvolutionalVisionTransformer`` (``old_codes/MS_CvT.py:491-623``)::
 
@@ -12,7 +12,7 @@ projections (``:132-137,178-185``).  Module tree and parameter names follow MS_C
                                  .blocks[j]: CvTBlock (.norm1, .attn: CvTAttention
                                  (.conv_proj_{q,k,v}: DwBnProjection (.bn), .proj_{q,k,v}, .proj),
                                  .norm2 unless tied, .mlp (.fc1, .fc2)))
-      norm: LayerNorm, head: Linear
+      norm: LayerNorm, proc: ProcMlp (.fc1, .fc2; cfg.proc_dim > 0), head: Linear
 
 Every op runs as a libvitmi kernel: conv-embed im2col + MFMA GEMM (+ col2im in the backward),
 dw_bn fwd/bwd, LayerNorm, the q/k/v/out/MLP GEMMs with fused epilogues and the attention
@@ -43,6 +43,15 @@ class CvTStage:
     with_cls_token: bool = False
     depth: int = 1
     padding: Optional[int] = None    # None: TF 'same' (Keras); an int: symmetric (torch / MS_CvT)
+    qkv_method: str = "dw_bn"        # 'dw_bn' | 'avg' (q stays 'linear') | 'linear'  (:25,83-112,130-132)
+
+
+def qkv_methods(st: CvTStage):
+    """Per-projection methods: 'avg' keeps q linear (models/CvT(Par).py:130-132)."""
+    m = st.qkv_method
+    if m not in ("dw_bn", "avg", "linear"):
+        raise ValueError(f"unknown qkv_method {m}")
+    return ("linear" if m == "avg" else m, m, m)
 
 
 def keras_spec() -> List[CvTStage]:
@@ -64,6 +73,9 @@ class CvTConfig:
     qkv_bias: bool = True
     tie_norms: bool = True         # the Keras block applies its one norm1 twice (:272,278)
     embed_norm: bool = False       # the intended ConvEmbed LayerNorm is never built (:209)
+    avg_count_pad: bool = False    # 'avg' divisor: TF 'same' in-bounds count (False) or torch's 9
+    proc_dim: int = 0              # process parameters (5 in the reference, :392); 0 = image only
+    proc_hidden: int = 256         # Proc_Dense_1/2 width (:343-344)
     dtype: str = "bf16"
 
     def replace(self, **kw) -> "CvTConfig":
@@ -168,10 +180,13 @@ class DwBnProjection(nn.Module):
 
 
 class CvTAttention(nn.Module):
-    def __init__(self, dim: int, num_heads: int, qkv_bias: bool):
+    def __init__(self, dim: int, num_heads: int, qkv_bias: bool, methods=("dw_bn",) * 3):
         super().__init__()
         self.num_heads = num_heads
-        self.conv_proj_q, self.conv_proj_k, self.conv_proj_v = (DwBnProjection(dim) for _ in range(3))
+        self.methods = tuple(methods)
+        for c, m in zip("qkv", self.methods):
+            if m == "dw_bn":
+                setattr(self, f"conv_proj_{c}", DwBnProjection(dim))
         self.proj_q, self.proj_k, self.proj_v = (Linear(dim, dim, bias=qkv_bias) for _ in range(3))
         self.proj = Linear(dim, dim)
 
@@ -186,10 +201,10 @@ class _Mlp(nn.Module):
 class CvTBlock(nn.Module):
     """ConvTransformerBlock (models/CvT(Par).py:231-289) with dw_bn q/k/v."""
 
-    def __init__(self, dim: int, num_heads: int, cfg: CvTConfig):
+    def __init__(self, dim: int, num_heads: int, cfg: CvTConfig, methods=("dw_bn",) * 3):
         super().__init__()
         self.norm1 = LayerNorm(dim, cfg.ln_eps)
-        self.attn = CvTAttention(dim, num_heads, cfg.qkv_bias)
+        self.attn = CvTAttention(dim, num_heads, cfg.qkv_bias, methods)
         self.tie_norms = cfg.tie_norms
         if not cfg.tie_norms:
             self.norm2 = LayerNorm(dim, cfg.ln_eps)
@@ -227,15 +242,26 @@ class _CvTBlockFn(torch.autograd.Function):
         h, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, cfg.ln_eps, F32)
         qkv = torch.empty(M, 3 * D, dtype=T, device=x.device)
         saved_proj = []
-        for c_i, c in enumerate("qkv"):
-            cp = getattr(a_, f"conv_proj_{c}")
+        h_lp = None
+        for c_i, (c, meth) in enumerate(zip("qkv", a_.methods)):
             lin = getattr(a_, f"proj_{c}")
-            inp = torch.empty(M, D, dtype=T, device=x.device)
-            if with_cls:
-                inp.view(B, N, D)[:, 0] = h.view(B, N, D)[:, 0].to(T)
-            z, mean, rstd = ops.dwconv_bn_fwd(h, B, H, W, cp.w9(), cp.bn.weight, cp.bn.bias, cfg.bn_eps,
-                                              cfg.bn_momentum, blk.training, cp.bn.running_mean,
-                                              cp.bn.running_var, inp, x_img=N, x_off=off, y_img=N, y_off=off)
+            z = mean = rstd = None
+            if meth == "linear":                       # identity projection: the LN output itself
+                if h_lp is None:
+                    h_lp = h if T == F32 else ops.cast_bf16(h)
+                inp = h_lp
+            else:
+                inp = torch.empty(M, D, dtype=T, device=x.device)
+                if with_cls:
+                    inp.view(B, N, D)[:, 0] = h.view(B, N, D)[:, 0].to(T)
+                if meth == "dw_bn":
+                    cp = getattr(a_, f"conv_proj_{c}")
+                    z, mean, rstd = ops.dwconv_bn_fwd(h, B, H, W, cp.w9(), cp.bn.weight, cp.bn.bias, cfg.bn_eps,
+                                                      cfg.bn_momentum, blk.training, cp.bn.running_mean,
+                                                      cp.bn.running_var, inp, x_img=N, x_off=off, y_img=N, y_off=off)
+                else:                                  # 'avg'
+                    ops.avgpool3_fwd(h, B, H, W, inp, x_img=N, x_off=off, y_img=N, y_off=off,
+                                     count_pad=cfg.avg_count_pad)
             wl = _lp(blk, lin.weight, T)
             ops.gemm(inp, wl, True, True, M, D, D, qkv[:, c_i * D:(c_i + 1) * D], ops.EPI_STORE, bias=lin.bias)
             saved_proj += [inp, z, mean, rstd, wl]
@@ -282,23 +308,66 @@ class _CvTBlockFn(torch.autograd.Function):
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, scale)
         # q/k/v GEMMs, the cls rows, dw_bn: all into the LN1-output gradient dh
         dh = torch.zeros(M, D, dtype=torch.float32, device=g2.device)
-        for c_i, c in enumerate("qkv"):
+        for c_i, (c, meth) in enumerate(zip("qkv", a_.methods)):
             inp, z, mean, rstd, wl = sp[5 * c_i:5 * c_i + 5]
-            cp = getattr(a_, f"conv_proj_{c}")
             lin = getattr(a_, f"proj_{c}")
             dq = dqkv[:, c_i * D:(c_i + 1) * D].contiguous()
             dinp = ops.linear_dgrad(dq, wl, F32)
             ops.linear_wgrad(dq, inp, _grad(lin.weight))
             if lin.bias is not None:
                 ops.bias_grad(dq, _grad(lin.bias))
+            if meth == "linear":
+                dh.add_(dinp)
+                continue
             if with_cls:
                 dh.view(B, N, D)[:, 0] += dinp.view(B, N, D)[:, 0]
+            if meth == "avg":
+                ops.avgpool3_bwd(dinp, B, H, W, dh, dy_img=N, dy_off=off, x_img=N, x_off=off,
+                                 count_pad=cfg.avg_count_pad)
+                continue
+            cp = getattr(a_, f"conv_proj_{c}")
             dw9 = torch.zeros(9, D, dtype=torch.float32, device=g2.device)
             ops.dwconv_bn_bwd(dinp, h, B, H, W, cp.w9(), cp.bn.weight, z, mean, rstd, dh, dw9,
                               _grad(cp.bn.weight), _grad(cp.bn.bias), x_img=N, x_off=off, dy_img=N, dy_off=off)
             _grad(cp.weight).add_(dw9.t().reshape(D, 1, 3, 3))
         dx, _ = ops.layernorm_bwd(dh, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias), dres=dx1, lp_dtype=None)
         return (dx.view(B, N, D), None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 5)
+
+
+class ProcMlp(nn.Module):
+    """Proc_Dense_1/2: Dense(hidden, relu) x 2 on the standardised process parameters
+    (models/CvT(Par).py:343-344), on the small fp32 Dense kernels."""
+
+    def __init__(self, dim: int, hidden: int):
+        super().__init__()
+        self.fc1 = Linear(dim, hidden)
+        self.fc2 = Linear(hidden, hidden)
+
+    def forward(self, proc: Tensor) -> Tensor:
+        _check_cuda(proc)
+        return _ProcMlpFn.apply(proc, self, *self.parameters())
+
+
+class _ProcMlpFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        x = x.contiguous().float()
+        h = ops.dense_f32_fwd(x, mod.fc1.weight.detach(), mod.fc1.bias, ops.ACT_RELU)
+        y = ops.dense_f32_fwd(h, mod.fc2.weight.detach(), mod.fc2.bias, ops.ACT_RELU)
+        ctx.save_for_backward(x, h, y)
+        ctx.mod = mod
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, y = ctx.saved_tensors
+        mod = ctx.mod
+        dy = dy.contiguous().float()
+        dh = ops.dense_f32_bwd(dy, y, h, mod.fc2.weight.detach(), _grad(mod.fc2.weight), _grad(mod.fc2.bias),
+                               ops.ACT_RELU)
+        dx = ops.dense_f32_bwd(dh, h, x, mod.fc1.weight.detach(), _grad(mod.fc1.weight), _grad(mod.fc1.bias),
+                               ops.ACT_RELU, want_dx=ctx.needs_input_grad[0])
+        return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 
 
 class _CvTHeadFn(torch.autograd.Function):
@@ -328,7 +397,8 @@ class CvTStageModule(nn.Module):
         self.embed = ConvEmbedSame(cin, st.embed_dim, st.patch_size, st.stride, st.padding, cfg.embed_norm,
                                    cfg.ln_eps, cfg.dtype)
         self.cls_token = nn.Parameter(torch.zeros(1, 1, st.embed_dim)) if st.with_cls_token else None
-        self.blocks = nn.ModuleList([CvTBlock(st.embed_dim, st.num_heads, cfg) for _ in range(st.depth)])
+        self.blocks = nn.ModuleList([CvTBlock(st.embed_dim, st.num_heads, cfg, qkv_methods(st))
+                                     for _ in range(st.depth)])
 
 
 class CvT(nn.Module):
@@ -343,6 +413,9 @@ class CvT(nn.Module):
             self.add_module(f"stage{i}", CvTStageModule(cin, st, cfg))
             cin = st.embed_dim
         self.norm = LayerNorm(cin, cfg.ln_eps)
+        if cfg.proc_dim:
+            self.proc = ProcMlp(cfg.proc_dim, cfg.proc_hidden)
+            cin += cfg.proc_hidden
         self.head = Linear(cin, cfg.num_classes)
 
     def stages(self) -> List[CvTStageModule]:
@@ -375,8 +448,14 @@ class CvT(nn.Module):
             return self.norm(t).mean(dim=1)
         return self.norm(tok)
 
-    def forward(self, img: Tensor) -> Tensor:
-        return _CvTHeadFn.apply(self.forward_features(img), self.head, self.head.weight, self.head.bias)
+    def forward(self, img: Tensor, proc: Optional[Tensor] = None) -> Tensor:
+        """Image features [++ Proc_Dense_2 features (:347)] -> Final_Dense (:350)."""
+        f = self.forward_features(img)
+        if self.cfg.proc_dim:
+            if proc is None:
+                raise ValueError("this CvT takes process parameters (cfg.proc_dim > 0): forward(img, proc)")
+            f = torch.cat([f, self.proc(proc.to(f.device, torch.float32))], dim=1)
+        return _CvTHeadFn.apply(f, self.head, self.head.weight, self.head.bias)
 
     def reset_parameters(self, seed: int = 0) -> None:
         """Keras initialisers: glorot_uniform kernels (Dense, Conv2D, DepthwiseConv2D), zero

@@ -372,3 +372,55 @@ def dwconv_bn_bwd(dy: Tensor, x: Tensor, B: int, H: int, W: int, w9: Tensor, gam
     check(lib().vitmi_dwconv_bn_bwd(B, H, W, C, _p(dy), dt(dy.dtype), lddy, dy_img, dy_off, _p(x), ldx, x_img, x_off,
                                     _p(w9), _p(gamma), _p(z), _p(mean), _p(rstd), _p(dx), _p(dw9), _p(dgamma),
                                     _p(dbeta), _p(ws), ws.numel(), _s()), "dwconv_bn_bwd")
+
+
+def avgpool3_fwd(x: Tensor, B: int, H: int, W: int, y: Tensor, x_img: Optional[int] = None, x_off: int = 0,
+                 y_img: Optional[int] = None, y_off: int = 0, count_pad: bool = False) -> Tensor:
+    """Projection('avg'): 3x3 stride-1 'same' average pooling (padding excluded from the count)
+    of the fp32 rows x into the rows of y (bf16 | fp32)."""
+    C = x.shape[-1]
+    _, ldx = _rows(x)
+    _, ldy = _rows(y)
+    x_img = H * W if x_img is None else x_img
+    y_img = H * W if y_img is None else y_img
+    check(lib().vitmi_avgpool3_fwd(B, H, W, C, _p(x), ldx, x_img, x_off, _p(y), dt(y.dtype), ldy, y_img, y_off,
+                                   int(count_pad), _s()), "avgpool3_fwd")
+    return y
+
+
+def avgpool3_bwd(dy: Tensor, B: int, H: int, W: int, dx: Tensor, dy_img: Optional[int] = None, dy_off: int = 0,
+                 x_img: Optional[int] = None, x_off: int = 0, count_pad: bool = False) -> None:
+    """dx (fp32 rows) += avgpool3^T(dy)."""
+    C = dx.shape[-1]
+    _, lddy = _rows(dy)
+    _, ldx = _rows(dx)
+    x_img = H * W if x_img is None else x_img
+    dy_img = H * W if dy_img is None else dy_img
+    check(lib().vitmi_avgpool3_bwd(B, H, W, C, _p(dy), dt(dy.dtype), lddy, dy_img, dy_off, _p(dx), ldx, x_img, x_off,
+                                   int(count_pad), _s()), "avgpool3_bwd")
+
+
+# ---------------------------------------------------------------- small fp32 Dense (SURVEY §8f row 2)
+ACT_LINEAR, ACT_RELU = 0, 1
+
+
+def dense_f32_fwd(x: Tensor, w: Tensor, b: Optional[Tensor], act: int = ACT_LINEAR) -> Tensor:
+    """y = act(x W^T + b) on the small fp32 Dense kernel (Proc_Dense_1/2)."""
+    M, ldx = _rows(x)
+    N, K = w.shape
+    assert x.dtype == torch.float32 and w.is_contiguous() and x.shape[-1] == K
+    y = torch.empty(M, N, dtype=torch.float32, device=x.device)
+    check(lib().vitmi_dense_f32_fwd(M, N, K, _p(x), ldx, _p(w), _p(b), _p(y), N, act, _s()), "dense_f32_fwd")
+    return y
+
+
+def dense_f32_bwd(dy: Tensor, y: Tensor, x: Tensor, w: Tensor, dw: Tensor, db: Optional[Tensor],
+                  act: int = ACT_LINEAR, want_dx: bool = True) -> Optional[Tensor]:
+    M, lddy = _rows(dy)
+    _, ldy = _rows(y)
+    _, ldx = _rows(x)
+    N, K = w.shape
+    dx = torch.empty(M, K, dtype=torch.float32, device=x.device) if want_dx else None
+    check(lib().vitmi_dense_f32_bwd(M, N, K, _p(dy), lddy, _p(y), ldy, _p(x), ldx, _p(w), _p(dx), K, _p(dw), _p(db),
+                                    act, _s()), "dense_f32_bwd")
+    return dx
