@@ -3,7 +3,7 @@
 
 BASELINE.json metric: "images/sec fwd+bwd ViT-B/16 224px bs=256/GPU at 1/2/4/8 MI355X;
 % MFMA roofline".  One step = forward + CE loss + full backward (hand-written gfx950
-kernels) + RCCL gradient all-reduce (N>1) + Adam update (torch.optim), on a synthetic
+kernels) + RCCL gradient all-reduce (N>1) + Keras Adam update (one fused vitmi launch), on a synthetic
 batch of 256 images/GPU already resident in HBM, random-init ViT-B/16 weights.
 
 Launch:  python bench.py [--gpus 1 --steps 10 --warmup 3]
@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from vitmi import dp, ops  # noqa: E402
+from vitmi import dp, ops, optim  # noqa: E402
 from vitmi.config import config_c3  # noqa: E402
 from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=16)
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-optimizer", action="store_true", help="diagnostic only: skip Adam")
+    ap.add_argument("--optimizer", choices=["vitmi", "torch"], default="vitmi",
+                    help="vitmi: Keras Adam, one fused launch over the arena (+ bf16 shadow); torch: fused torch Adam")
     args = ap.parse_args()
 
     rank, world, local = dp.init_from_env("nccl")
@@ -82,10 +84,13 @@ def main():
     model.reset_parameters(seed=0)
     red = dp.attach(model, bucket_mb=args.bucket_mb)
     dp.broadcast_parameters(model)
-    try:
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
-    except (RuntimeError, TypeError):
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, foreach=True)
+    if args.optimizer == "vitmi":
+        opt = optim.Adam(model, learning_rate=1e-3)     # keras.optimizers.Adam(1e-3), models/CvT(Par).py:458
+    else:
+        try:
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+        except (RuntimeError, TypeError):
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3, foreach=True)
     arena = model.arena()
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -154,6 +159,7 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (torch.rand images in [0,1), randint labels; random-init trunc_normal(.02) weights)",
         "config": {"workload": "ViT-B/16 224x224x3 fwd + CE loss + bwd + RCCL grad all-reduce + Adam step",
+                   "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
                    "model": "vit_base_16", "global_batch": B * world, "seq_len": cfg.seq_len,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd bf16 [{M}x{F_}x{D}] +bias+GELU",

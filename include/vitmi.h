@@ -243,6 +243,17 @@ int vitmi_dense_f32_bwd(int M, int N, int K, const float* dy, int64_t lddy, cons
                         const float* x, int64_t ldx, const float* w, float* dx, int64_t lddx, float* dw, float* db,
                         int act, vitmi_stream_t stream);
 
+/* Keras Adam step (models/CvT(Par).py:458-460: keras.optimizers.Adam(1e-3); beta_1 0.9,
+ * beta_2 0.999, epsilon 1e-7) over n fp32 parameters in place:
+ *   g' = g * grad_scale;  m += (g' - m)(1 - b1);  v += (g'^2 - v)(1 - b2);
+ *   p -= alpha m / (sqrt(v) + eps),   alpha = lr sqrt(1 - b2^t) / (1 - b1^t) (caller, step t >= 1).
+ * p_lp (optional, bf16) receives the updated parameters' operand shadow in the same pass.
+ * (1 - beta) is formed in double and rounded once (Keras' Python-float hyper-parameters).
+ * Explicitly rounded fp32 ops in this order: bit-identical to a float32 evaluation.  Buffers
+ * 16-byte aligned (a ParamArena's flat buffers; one launch for the whole model). */
+int vitmi_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_lp, float alpha, double beta_1,
+                    double beta_2, float epsilon, float grad_scale, vitmi_stream_t stream);
+
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
 

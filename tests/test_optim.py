@@ -1,0 +1,77 @@
+"""The reference's optimizer (keras Adam, models/CvT(Par).py:458-460) and LR schedule
+(:357-360) on the fused vitmi kernel vs oracle/optim_ref.py: bit-exact fp32 (the kernel and
+the oracle do the same IEEE-rounded ops in the same order)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import optim_ref
+from vitmi import optim
+
+DEV = "cuda"
+
+
+def test_alpha_and_schedule_host():
+    for t in (1, 2, 10, 1000):
+        assert optim.keras_alpha(1e-3, 0.9, 0.999, t) == float(optim_ref.keras_alpha(1e-3, 0.9, 0.999, t))
+    lr = 1e-3
+    for e in range(0, 201):
+        lr_ref = optim_ref.lr_scheduler(e, lr)
+        lr = optim.keras_step_decay(e, lr)
+        assert lr == lr_ref
+    assert abs(lr - 1e-3 * 0.8 ** 4) < 1e-15
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,scale", [(1, 1.0), (7, 1.0), (1_000_003, 1.0), (4096, 0.25)])
+def test_adam_per_tensor_bit_exact(n, scale):
+    g = torch.Generator().manual_seed(n)
+    p = torch.randn(n, generator=g)
+    ref = (p.numpy().copy(), np.zeros(n, np.float32), np.zeros(n, np.float32))
+    pd = p.to(DEV).requires_grad_(True)
+    opt = optim.Adam([pd], learning_rate=1e-3, grad_scale=scale)
+    for t in range(1, 4):
+        gr = torch.randn(n, generator=g) * (10.0 ** (t - 2))
+        pd.grad = gr.to(DEV)
+        opt.step()
+        ref = optim_ref.adam_step(ref[0], gr.numpy(), ref[1], ref[2], 1e-3, t, grad_scale=scale)
+        torch.cuda.synchronize()
+        assert np.array_equal(pd.detach().cpu().numpy(), ref[0]), t
+        assert np.array_equal(opt._m[0].cpu().numpy(), ref[1])
+        assert np.array_equal(opt._v[0].cpu().numpy(), ref[2])
+
+
+@pytest.mark.gpu
+def test_adam_arena_single_launch_and_bf16_shadow():
+    from vitmi.config import ViTConfig
+    from vitmi.modules import VisionTransformer, cross_entropy
+    cfg = ViTConfig(img_size=32, patch_size=8, in_chans=3, num_classes=3, embed_dim=128, depth=2, num_heads=2,
+                    dtype="bf16")
+    model = VisionTransformer(cfg).to(DEV)
+    model.reset_parameters(seed=1)
+    opt = optim.Adam(model, learning_rate=1e-3)
+    arena = model.arena()
+    p0 = arena.flat.cpu().numpy().copy()
+    m0 = np.zeros_like(p0)
+    v0 = np.zeros_like(p0)
+    g = torch.Generator().manual_seed(2)
+    img = torch.rand(4, 3, 32, 32, generator=g).to(DEV)
+    tgt = torch.randint(0, 3, (4,), generator=g).to(DEV)
+    for t in (1, 2):
+        opt.zero_grad()
+        cross_entropy(model(img), tgt).backward()
+        grad = arena.grad.cpu().numpy().copy()
+        opt.step()
+        torch.cuda.synchronize()
+        p0, m0, v0 = optim_ref.adam_step(p0, grad, m0, v0, 1e-3, t)
+        assert np.array_equal(arena.flat.cpu().numpy(), p0)
+        # the shadow the next forward's GEMMs read == bf16(updated params), without a cast pass
+        assert torch.equal(arena.flat_lp, arena.flat.to(torch.bfloat16))
+        v_before = arena._lp_version
+        arena.refresh_lp()
+        assert arena._lp_version == v_before
+    # an in-place torch update of a parameter invalidates the shadow
+    with torch.no_grad():
+        model.head.weight.add_(1.0)
+    arena.refresh_lp()
+    assert torch.equal(arena.flat_lp, arena.flat.to(torch.bfloat16))

@@ -21,6 +21,7 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_int64
 F = ctypes.c_float
+D = ctypes.c_double
 S = ctypes.c_size_t
 U = ctypes.c_uint32
 
@@ -62,6 +63,7 @@ SIGNATURES = {
     "vitmi_dwconv_bn_workspace_size": (S, [I, I, I, I]),
     "vitmi_dwconv_bn_fwd": (I, [I, I, I, I, P, L, L, L, P, P, P, F, F, I, P, P, P, P, P, P, I, L, L, L, P, S, P]),
     "vitmi_dwconv_bn_bwd": (I, [I, I, I, I, P, I, L, L, L, P, L, L, L, P, P, P, P, P, P, P, P, P, P, S, P]),
+    "vitmi_adam_step": (I, [L, P, P, P, P, P, F, D, D, F, F, P]),
     "vitmi_dense_f32_fwd": (I, [I, I, I, P, L, P, P, P, L, I, P]),
     "vitmi_dense_f32_bwd": (I, [I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, P]),
     "vitmi_avgpool3_fwd": (I, [I, I, I, I, P, L, L, L, P, I, L, L, L, I, P]),

@@ -604,6 +604,7 @@ class ParamArena:
         self.flat = torch.zeros(n, dtype=F32, device=device)
         self.grad = torch.zeros(n, dtype=F32, device=device)
         self.flat_lp = torch.empty(n, dtype=torch.bfloat16, device=device) if want_lp else None
+        self._lp_version: Optional[int] = None
         with torch.no_grad():
             for p, o in zip(ordered, offs):
                 self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
@@ -624,9 +625,25 @@ class ParamArena:
     def lp(self, p: Tensor) -> Tensor:
         return self.view(self.flat_lp, p)
 
+    def _stamp(self) -> int:
+        # version counters only grow: any in-place torch write to the flat buffer or to a
+        # parameter (p.data is a view of it but keeps its own counter) raises this sum
+        return self.flat._version + sum(p._version for p in self.params)
+
     def refresh_lp(self) -> None:
-        if self.flat_lp is not None:
-            ops.cast_bf16(self.flat, self.flat_lp)
+        """Re-cast the bf16 shadow unless it is current: no in-place torch write since the
+        last cast or since vitmi Adam wrote params and shadow together."""
+        if self.flat_lp is None:
+            return
+        stamp = self._stamp()
+        if self._lp_version == stamp:
+            return
+        ops.cast_bf16(self.flat, self.flat_lp)
+        self._lp_version = stamp
+
+    def mark_lp_fresh(self) -> None:
+        """The fused optimizer wrote params and shadow through raw pointers (no version bump)."""
+        self._lp_version = self._stamp()
 
     def bind_grads(self) -> None:
         ps, views = self.params, self._grad_views

@@ -1,0 +1,132 @@
+"""The reference's optimizer and learning-rate schedule on the fused vitmi kernel.
+
+``model.compile(optimizer=keras.optimizers.Adam(learning_rate=1e-3), loss='mean_squared_error')``
+(``models/CvT(Par).py:458-460``) and ``lr_scheduler`` (``:357-360``: x0.8 every 50 epochs).
+
+``Adam`` runs Keras' update (include/vitmi.h ``vitmi_adam_step``): ONE launch over a model's
+ParamArena (every parameter, gradient and moment at the same flat offsets), which also writes
+the bf16 operand shadow the next forward's GEMMs read; models without an arena (the CvT) get
+one launch per parameter tensor.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+import torch
+
+from . import ops
+from ._lib import check, lib
+
+Tensor = torch.Tensor
+
+
+def keras_alpha(lr: float, beta_1: float, beta_2: float, step: int) -> float:
+    """alpha = lr sqrt(1 - b2^t) / (1 - b1^t), in float32 like Keras' update_step."""
+    f = np.float32
+    b1p = np.power(f(beta_1), f(step), dtype=np.float32)
+    b2p = np.power(f(beta_2), f(step), dtype=np.float32)
+    return float(f(lr) * np.sqrt(f(1) - b2p, dtype=np.float32) / (f(1) - b1p))
+
+
+class Adam:
+    """keras.optimizers.Adam(learning_rate, beta_1=0.9, beta_2=0.999, epsilon=1e-7).
+
+    ``target``: a model with ``arena()`` (VisionTransformer: single fused launch + bf16 shadow
+    refresh) or an iterable of parameters.  ``grad_scale`` multiplies the gradients as they are
+    read (e.g. 1/world for a sum all-reduce)."""
+
+    def __init__(self, target, learning_rate: float = 1e-3, beta_1: float = 0.9, beta_2: float = 0.999,
+                 epsilon: float = 1e-7, grad_scale: float = 1.0):
+        self.learning_rate = float(learning_rate)
+        self.beta_1, self.beta_2, self.epsilon = float(beta_1), float(beta_2), float(epsilon)
+        self.grad_scale = float(grad_scale)
+        self.iterations = 0
+        self._model = target if hasattr(target, "arena") else None
+        if self._model is not None:
+            arena = self._model.arena()
+            self._arena = arena
+            self.params: List[Tensor] = list(arena.params)
+            self._m = torch.zeros_like(arena.flat)
+            self._v = torch.zeros_like(arena.flat)
+        else:
+            self._arena = None
+            self.params = [p for p in target if p.requires_grad]
+            self._m = [torch.zeros_like(p) for p in self.params]
+            self._v = [torch.zeros_like(p) for p in self.params]
+
+    # -- keras-style schedule hook
+    @property
+    def lr(self) -> float:
+        return self.learning_rate
+
+    @lr.setter
+    def lr(self, v: float) -> None:
+        self.learning_rate = float(v)
+
+    def zero_grad(self) -> None:
+        if self._arena is not None:
+            self._arena.grad.zero_()
+            return
+        for p in self.params:
+            if p.grad is not None:
+                p.grad.zero_()
+
+    @torch.no_grad()
+    def step(self) -> None:
+        self.iterations += 1
+        alpha = keras_alpha(self.learning_rate, self.beta_1, self.beta_2, self.iterations)
+        if self._arena is not None:
+            arena = self._model.arena()
+            if arena is not self._arena:
+                raise RuntimeError("vitmi Adam: the model's parameter arena was rebuilt after the optimizer "
+                                   "was created (model moved?); create the optimizer after placing the model")
+            for p in (self.params[0], self.params[-1]):     # bind_grads binds all or none
+                if p.grad is None or p.grad.data_ptr() != arena.view(arena.grad, p).data_ptr():
+                    raise RuntimeError("vitmi Adam: gradients are not bound to the arena (run a forward first)")
+            lp = arena.flat_lp
+            check(lib().vitmi_adam_step(arena.numel, ops._p(arena.flat), ops._p(arena.grad), ops._p(self._m),
+                                        ops._p(self._v), ops._p(lp), alpha, self.beta_1, self.beta_2, self.epsilon,
+                                        self.grad_scale, ops._s()), "adam_step")
+            arena.mark_lp_fresh()
+            return
+        for p, m, v in zip(self.params, self._m, self._v):
+            if p.grad is None:
+                continue
+            if not (p.is_contiguous() and p.grad.is_contiguous()):
+                raise RuntimeError("vitmi Adam: parameters and gradients must be contiguous")
+            check(lib().vitmi_adam_step(p.numel(), ops._p(p), ops._p(p.grad), ops._p(m), ops._p(v), None, alpha,
+                                        self.beta_1, self.beta_2, self.epsilon, self.grad_scale, ops._s()),
+                  "adam_step")
+
+    # -- checkpointing (Keras saves the optimizer variables with the model weights)
+    def state_dict(self) -> Dict:
+        if self._arena is not None:
+            return {"iterations": self.iterations, "learning_rate": self.learning_rate, "m": self._m.clone(),
+                    "v": self._v.clone()}
+        return {"iterations": self.iterations, "learning_rate": self.learning_rate,
+                "m": [t.clone() for t in self._m], "v": [t.clone() for t in self._v]}
+
+    def load_state_dict(self, sd: Dict) -> None:
+        self.iterations = int(sd["iterations"])
+        self.learning_rate = float(sd["learning_rate"])
+        with torch.no_grad():
+            if self._arena is not None:
+                self._m.copy_(sd["m"])
+                self._v.copy_(sd["v"])
+            else:
+                for dst, src in zip(self._m, sd["m"]):
+                    dst.copy_(src)
+                for dst, src in zip(self._v, sd["v"]):
+                    dst.copy_(src)
+
+
+def keras_step_decay(epoch: int, lr: float, every: int = 50, factor: float = 0.8) -> float:
+    """lr_scheduler (models/CvT(Par).py:357-360): x0.8 at every 50th epoch (epoch > 0)."""
+    if epoch > 0 and epoch % every == 0:
+        return lr * factor
+    return lr
+
+
+__all__ = ["Adam", "keras_alpha", "keras_step_decay"]
+
