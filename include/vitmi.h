@@ -254,6 +254,22 @@ int vitmi_dense_f32_bwd(int M, int N, int K, const float* dy, int64_t lddy, cons
 int vitmi_adam_step(int64_t n, float* p, const float* g, float* m, float* v, void* p_lp, float alpha, double beta_1,
                     double beta_2, float epsilon, float grad_scale, vitmi_stream_t stream);
 
+/* SLS data pipeline (models/CvT(Par).py:414-428).
+ * vitmi_sls_resize_table (host): cv2 INTER_LINEAR table of one axis, ssize -> dsize:
+ *   ofs[d] first source index, w[2d], w[2d+1] its Q11 weights (OpenCV 8-bit fixed point).
+ * vitmi_sls_preprocess: n decoded uint8 frames (interleaved 3 channels, RGB, or BGR if bgr=1;
+ *   frame i row y at src + i*img_bytes + y*row_bytes) -> cv2.resize to Wo x Ho ->
+ *   BGR2GRAY -> /255.0 -> fp32 out[n][Ho*Wo].  Tables are device copies of the two axis
+ *   tables (xofs/xw for W -> Wo, yofs/yw for H -> Ho).
+ * vitmi_gather_rows: dst[i] = src[idx[i]] for n rows of row_bytes (batch assembly from the
+ *   HBM-resident dataset; idx device int64; an index outside [0, n_src) gives a zero row). */
+int vitmi_sls_resize_table(int ssize, int dsize, int* ofs, short* w);
+int vitmi_sls_preprocess(int n, int H, int W, const void* src, int64_t img_bytes, int64_t row_bytes, int bgr, int Ho,
+                         int Wo, const int* xofs, const short* xw, const int* yofs, const short* yw, float* out,
+                         vitmi_stream_t stream);
+int vitmi_gather_rows(int64_t n, int64_t row_bytes, const void* src, int64_t n_src, const int64_t* idx, void* dst,
+                      vitmi_stream_t stream);
+
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
 

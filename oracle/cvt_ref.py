@@ -226,7 +226,7 @@ def block(x: Tensor, hw: Tuple[int, int], p: Dict[str, Tensor], pre: str, cfg: C
     return x + y
 
 
-def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig) -> Tensor:
+def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, capture: Optional[list] = None) -> Tensor:
     """Stages 1..S; returns LN(final cls token) [B, D] (the token mean without cls, :337-340)."""
     x = img
     tok = None
@@ -242,6 +242,8 @@ def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig) -> Tenso
             t = torch.cat([p[pre + "cls_token"].expand(B, 1, D), t], dim=1)
         for j in range(st.depth):
             t = block(t, (H, W), p, f"{pre}blocks.{j}.", cfg, st)
+        if capture is not None:
+            capture.append((t, H, st.with_cls_token))
         if st.with_cls_token:
             tok, t = t[:, 0], t[:, 1:]
         x = t.transpose(1, 2).reshape(B, D, H, W)
@@ -256,9 +258,10 @@ def proc_features(proc: Tensor, p: Dict[str, Tensor]) -> Tensor:
     return F.relu(F.linear(h, p["proc.fc2.weight"], p["proc.fc2.bias"]))
 
 
-def forward(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, proc: Optional[Tensor] = None) -> Tensor:
+def forward(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, proc: Optional[Tensor] = None,
+            capture: Optional[list] = None) -> Tensor:
     """Image features (+ concatenated process features, :347) -> Final_Dense (:350)."""
-    f = forward_features(img, p, cfg)
+    f = forward_features(img, p, cfg, capture)
     if cfg.proc_dim:
         f = torch.cat([f, proc_features(proc, p)], dim=1)
     return F.linear(f, p["head.weight"], p["head.bias"])
@@ -293,3 +296,26 @@ def synthetic_batch(cfg: CvTConfig, batch: int, seed: int = 1234):
     else:
         tgt = torch.randint(0, cfg.num_classes, (batch,), generator=g)
     return img, tgt
+
+
+def gradcam(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, proc: Optional[Tensor] = None, stage: int = -1,
+            batch_size: int = 1) -> Tensor:
+    """make_gradcam_heatmap (tools/grad_cam_CvT.py:422-481) per batch of ``batch_size``: grads of
+    predictions[:, 0] wrt the stage's spatial output A [b, H, W, C]; pooled = mean over (0, 1, 2);
+    heatmap = sum_c pooled[c] A[0, :, :, c]; max(heatmap, 0) / max(heatmap).  (BatchNorm in
+    training mode here: use it with 'avg' / 'linear' projections for an inference-mode match.)"""
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+    out = []
+    for lo in range(0, img.shape[0], batch_size):
+        cap = []
+        pr = None if proc is None else proc[lo:lo + batch_size]
+        logits = forward(img[lo:lo + batch_size], p, cfg, pr, capture=cap)
+        t, H, has_cls = cap[stage]
+        g = torch.autograd.grad(logits[:, 0].sum(), t)[0]
+        A, G = (t[:, 1:], g[:, 1:]) if has_cls else (t, g)
+        n, _, C = A.shape
+        A, G = A.reshape(n, H, H, C), G.reshape(n, H, H, C)
+        pooled = G.mean(dim=(0, 1, 2))
+        hm = (pooled * A[0]).sum(-1)
+        out.append((torch.clamp(hm, min=0) / hm.max()).detach())
+    return torch.stack(out, 0)

@@ -63,6 +63,9 @@ SIGNATURES = {
     "vitmi_dwconv_bn_workspace_size": (S, [I, I, I, I]),
     "vitmi_dwconv_bn_fwd": (I, [I, I, I, I, P, L, L, L, P, P, P, F, F, I, P, P, P, P, P, P, I, L, L, L, P, S, P]),
     "vitmi_dwconv_bn_bwd": (I, [I, I, I, I, P, I, L, L, L, P, L, L, L, P, P, P, P, P, P, P, P, P, P, S, P]),
+    "vitmi_sls_resize_table": (I, [I, I, P, P]),
+    "vitmi_sls_preprocess": (I, [I, I, I, P, L, L, I, I, I, P, P, P, P, P, P]),
+    "vitmi_gather_rows": (I, [L, L, P, L, P, P, P]),
     "vitmi_adam_step": (I, [L, P, P, P, P, P, F, D, D, F, F, P]),
     "vitmi_dense_f32_fwd": (I, [I, I, I, P, L, P, P, P, L, I, P]),
     "vitmi_dense_f32_bwd": (I, [I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, P]),

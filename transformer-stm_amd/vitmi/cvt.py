@@ -429,7 +429,9 @@ class CvT(nn.Module):
         H, img_stride, row_off = S, S * S, 0
         tok = None
         t = None
-        for stg in self.stages():
+        cap = getattr(self, "_capture_stage", None)
+        stages = self.stages()
+        for si, stg in enumerate(stages):
             st = stg.spec
             t, H = stg.embed(x, B, H, img_stride, row_off)          # [B, H*H, D] fp32
             D = st.embed_dim
@@ -437,6 +439,10 @@ class CvT(nn.Module):
                 t = torch.cat([stg.cls_token.expand(B, 1, D), t], dim=1)
             for blk in stg.blocks:
                 t = blk(t, H, H, stg.cls_token is not None)
+            if cap is not None and si == cap % len(stages):     # Grad-CAM's activation (vitmi.gradcam)
+                if t.requires_grad:
+                    t.retain_grad()
+                self._captured = (t, H, stg.cls_token is not None)
             N = t.shape[1]
             if stg.cls_token is not None:
                 tok = t[:, 0]
