@@ -55,7 +55,27 @@ struct GemmArgs {
   // dropout of the *_DROP epilogues (see drop_hash in common.h)
   uint32_t drop_seed, drop_site, drop_thresh;
   float drop_scale;
+  // gemm256 tile order: groups of group_m tile-rows, column-major inside a group, so the 32
+  // tiles an XCD runs concurrently span ~group_m A panels x 32/group_m B panels (L2 reuse);
+  // 1 = plain row-major order
+  int group_m;
 };
+
+// (tile-row, tile-col) of tile index tl in the grouped order (a bijection on [0, tm*tn))
+__device__ __forceinline__ void tile_rc(const GemmArgs& g, int tl, int& tm, int& tn) {
+  const int G = g.group_m;
+  if (G <= 1) {
+    tm = tl / g.tiles_n;
+    tn = tl - tm * g.tiles_n;
+    return;
+  }
+  const int tiles_m = (int)((g.M + 255) / 256);
+  const int per = G * g.tiles_n;
+  const int grp = tl / per, r = tl - grp * per;
+  const int gm = min(G, tiles_m - grp * G);
+  tn = r / gm;
+  tm = grp * G + (r - tn * gm);
+}
 
 // internal epilogues: split-K partial slab, and GELU / residual with a fused dropout
 enum { EPI_PARTIAL = 100, EPI_GELU_DROP = 101, EPI_RESIDUAL_DROP = 102 };
@@ -493,8 +513,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       ks0_ = (v % g.nsplit) * g.ksplit;
       nk_ = min(g.ksplit, nk - ks0_);
     }
-    m0_ = (int64_t)(tl / g.tiles_n) * BM;
-    n0_ = (int64_t)(tl % g.tiles_n) * BN;
+    int tm_, tn_;
+    tile_rc(g, tl, tm_, tn_);
+    m0_ = (int64_t)tm_ * BM;
+    n0_ = (int64_t)tn_ * BN;
   };
   auto sub = [&](int buf, int which) -> char* { return smem + buf * STAGE + which * HALF; };
   // issue half `which` (0=A0 1=B0 2=A1 3=B1) of K-step t into buffer buf
@@ -840,8 +862,10 @@ __global__ __launch_bounds__(256) void gemm_tail_fixup_kernel(GemmArgs g, int nt
     const int e = (int)(i % (256 * 64)) * 4;
     const int rl = e >> 8, cl = e & 255;
     const int tile = g.t_full + t;
-    const int64_t row = (int64_t)(tile / g.tiles_n) * 256 + rl;
-    const int64_t col = (int64_t)(tile % g.tiles_n) * 256 + cl;
+    int tm, tn;
+    tile_rc(g, tile, tm, tn);
+    const int64_t row = (int64_t)tm * 256 + rl;
+    const int64_t col = (int64_t)tn * 256 + cl;
     if (row >= g.M || col >= g.N) continue;
     f32x4 a = {0.f, 0.f, 0.f, 0.f};
     for (int z = 0; z < g.nsplit; ++z)
@@ -866,6 +890,7 @@ static int g_cus = 256;   // compute units of the current device (set on first u
 static int g_grid_override = 0;   // VITMI_GEMM_GRID: 0 = persistent (one block per CU), -1 = one block per tile
 static int g_fold = 1;            // VITMI_GEMM_FOLD: 1 = split-K folded into persistent units, 0 = gridDim.z
 static int g_split256 = 1;        // VITMI_GEMM_SPLIT256: 1 = few-tile split-K GEMMs on gemm256
+static int g_group_m = 1;         // VITMI_GEMM_GROUP: gemm256 tile-row group (1 = row-major order)
 
 static void init_cus() {
   static bool done = false;
@@ -873,6 +898,7 @@ static void init_cus() {
   if (const char* e = getenv("VITMI_GEMM_GRID")) g_grid_override = atoi(e);
   if (const char* e = getenv("VITMI_GEMM_FOLD")) g_fold = atoi(e);
   if (const char* e = getenv("VITMI_GEMM_SPLIT256")) g_split256 = atoi(e);
+  if (const char* e = getenv("VITMI_GEMM_GROUP")) g_group_m = atoi(e);
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
@@ -939,6 +965,7 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (big) {
       g.tiles_n = (int)((g.N + 255) / 256);
+      g.group_m = g_group_m;
       int nwg = (int)((g.M + 255) / 256) * g.tiles_n;
       g.kz = 1;
       g.ntiles = nwg;
