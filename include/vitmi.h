@@ -90,6 +90,17 @@ size_t vitmi_linear_dgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_
 /* dW[N,K] (f32) += dy[M,N]^T x[M,K]; uses split-K over M with fp32 partial slabs */
 int vitmi_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* x,
                        float* dw, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+/* Linear dgrad with the bias gradient of its OUTPUT fused: dx = dy W (optionally * aux, DGELU)
+ * and db[k] += sum_m dx[m][k] (fp32).  The bias of the layer whose INPUT gradient dx is: for
+ * the MLP, du = (g W2) * gelu'(u) is fc1's output gradient, so db = fc1's bias gradient
+ * (models/CvT(Par).py:254; Keras Dense bias).  On the gemm256 DGELU path the column sums come
+ * from the epilogue registers (one fp32 partial row per 128 output rows, folded in a fixed
+ * order), elsewhere from a second pass over dx.  workspace >= vitmi_linear_dgrad_bias_workspace_size. */
+size_t vitmi_linear_dgrad_bias_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
+int vitmi_linear_dgrad_bias(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* w, void* dx,
+                            int dx_dtype, int epilogue, const void* aux, float* db, void* workspace, size_t ws_bytes,
+                            vitmi_stream_t stream);
+
 size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
 /* db[N] (f32) += sum_m dy[m, n]  (dy [M][ldy] of `dtype`) */
 int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, int64_t ldy, float* db,

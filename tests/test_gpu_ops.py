@@ -150,6 +150,32 @@ def test_linear_wgrad_split_units(M, N, K):
     assert rel(dw, ref) < 2e-5
 
 
+@pytest.mark.parametrize("M,N,K,T,epi", [(197 * 64 + 3, 768, 3072, BF, "dgelu"), (50432 // 8, 768, 3072, BF, "dgelu"),
+                                         (197 * 8, 256, 1024, BF, "dgelu"), (300, 128, 512, BF, "store"),
+                                         (197 * 4, 768, 3072, torch.float32, "dgelu")])
+def test_linear_dgrad_fused_bias(M, N, K, T, epi):
+    """dgrad + the column sums of its output (fc1's bias gradient): fused into the gemm256
+    DGELU epilogue for bf16 (ragged M), a second pass elsewhere; == dgrad then bias_grad."""
+    dy = rnd(M, N, dtype=T, seed=31)
+    w = (rnd(N, K, seed=32) * 0.05).to(T)
+    aux = (rnd(M, K, seed=33).abs() + 0.1).to(T) if epi == "dgelu" else None
+    e = ops.EPI_DGELU if epi == "dgelu" else ops.EPI_STORE
+    dyd, wd = dy.to(DEV), w.to(DEV).contiguous()
+    auxd = aux.to(DEV) if aux is not None else None
+    ref = ops.linear_dgrad(dyd, wd, T, e, aux=auxd)
+    db_ref = torch.full((K,), 0.5, device=DEV)
+    ops.bias_grad(ref, db_ref)
+    db = torch.full((K,), 0.5, device=DEV)
+    dx = ops.linear_dgrad(dyd, wd, T, e, aux=auxd, bias_grad=db)
+    # (the fused launch runs without the tail K-split: last-round tiles may round differently)
+    assert rel(dx, ref) < (3e-3 if T == BF else 1e-6)
+    # fused sums add the fp32 values before the bf16 rounding of dx: within bf16 noise
+    tol = 2e-3 if T == BF else 1e-5
+    assert rel(db, db_ref) < tol
+    dxf = ref.float()
+    assert rel(db - 0.5, dxf.sum(0)) < tol
+
+
 @pytest.mark.parametrize("T", [BF, torch.float32])
 def test_bias_grad(T):
     dy = rnd(197 * 3 + 1, 2304, dtype=T, seed=14)

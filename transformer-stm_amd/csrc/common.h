@@ -96,4 +96,7 @@ __device__ __forceinline__ uint32_t clamp_bytes(int64_t b) {
   return b <= 0 ? 0u : (b > 0x7fffffff ? 0x7fffffffu : (uint32_t)b);
 }
 
+// db[n] += sum_z part[z][n] in a fixed order (elementwise.hip)
+int launch_colsum_finish(int64_t N, int Z, const float* part, float* db, hipStream_t s);
+
 }  // namespace vitmi

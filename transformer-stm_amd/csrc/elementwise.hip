@@ -157,6 +157,12 @@ __global__ __launch_bounds__(1024) void colsum_finish_kernel(int64_t N, int Z, c
   }
 }
 
+int launch_colsum_finish(int64_t N, int Z, const float* part, float* db, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, N, Z, part, db);
+  VITMI_LAUNCH_CHECK("colsum_finish");
+  return VITMI_OK;
+}
+
 // number of row chunks: enough blocks to fill the chip (~1024) for the vector kernel
 static int colsum_splits(int64_t M, int64_t N) {
   const int64_t colblocks = (N + 511) / 512;

@@ -59,6 +59,9 @@ struct GemmArgs {
   // tiles an XCD runs concurrently span ~group_m A panels x 32/group_m B panels (L2 reuse);
   // 1 = plain row-major order
   int group_m;
+  // gemm256 DGELU epilogue: column sums of the output (the bias gradient of the layer whose
+  // input gradient this is), one fp32 row per 128-row half tile: colsum[(2*tm + wm)*N + col]
+  float* colsum;
 };
 
 // (tile-row, tile-col) of tile index tl in the grouped order (a bijection on [0, tm*tn))
@@ -733,6 +736,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           bv[ni] = *(const f32x4*)(smem + 2 * STAGE + tpar * 1024 + (wn * 64 + ni * 16 + lc4) * 4);
       }
       [[maybe_unused]] __amdgpu_buffer_rsrc_t ru = rc;
+      [[maybe_unused]] f32x4 csum[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                                        f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
       if constexpr (EB == VITMI_EPI_BIAS_GELU)
         ru = make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand
@@ -771,6 +776,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         } else if constexpr (EPI == VITMI_EPI_DGELU) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= (float)ldb[e];   // aux = gelu'(u) from the forward
+          csum[ni] += v;                                       // rows >= M hold 0 (zero A rows)
         }
         if constexpr (CES == 4) {
           asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
@@ -807,6 +813,30 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           for (int h = 0; h < RB; ++h)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) emit(RB * mp + h, ni, ld4[h][ni], ldu[h][ni]);
+        }
+        if constexpr (EPI == VITMI_EPI_DGELU) {
+          if (g.colsum) {
+            // sum the wave's 128 rows: 8 row groups in registers (above), then the 16 lanes
+            // of a column group (lane & 15 = row); lanes 0/16/32/48 store 4 columns per ni
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float x = csum[ni][e];
+                x += __shfl_xor(x, 1, 64);
+                x += __shfl_xor(x, 2, 64);
+                x += __shfl_xor(x, 4, 64);
+                x += __shfl_xor(x, 8, 64);
+                csum[ni][e] = x;
+              }
+            const int64_t prow = (m0 / BM) * 2 + wm;
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.colsum + prow * g.N + n0, clamp_bytes((g.N - n0) * 4));
+            const uint32_t cb = lr == 0 ? (uint32_t)((wn * 64 + lc4) * 4) : 0x80000000u;
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+              asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"
+                           :: "v"(csum[ni]), "v"(cok[ni] ? cb : 0x80000000u), "s"(rs), "i"(ni * 64) : "memory");
+          }
         }
       } else {
         // store-only epilogues go row by row: the 4 column groups of a row (one 128-B line
@@ -985,7 +1015,8 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       const char* tenv = getenv("VITMI_GEMM_TAIL");   // 0: no tail split (A/B timing)
       // measured: pays off for long reductions (>= 16 K-steps) and for the DGELU epilogue
       // (whose partial units skip its aux loads); a wash or a loss for K = 768 otherwise
-      const bool tail_ok = g.k_per_split / 64 >= 16 || EPI == VITMI_EPI_DGELU;
+      // (no tail split with fused column sums: every tile must run the full epilogue)
+      const bool tail_ok = (g.k_per_split / 64 >= 16 || EPI == VITMI_EPI_DGELU) && g.colsum == nullptr;
       if (splits == 1 && tail_ok && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM && g.tail_ws && !(tenv && atoi(tenv) == 0) &&
           tail_plan(nwg, gx, (int)(g.k_per_split / 64), S, ks, ntail) &&
           g.tail_ws_bytes >= (size_t)ntail * S * 256 * 256 * sizeof(float)) {
@@ -1067,7 +1098,8 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
                      int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
                      int epi, const float* bias, void* aux, int64_t ldaux, const float* residual,
                      int64_t ldr, void* ws, size_t ws_bytes, hipStream_t s, bool allow_split,
-                     const GemmArgs* drop = nullptr) {
+                     const GemmArgs* drop = nullptr, float* colsum = nullptr, bool* colsum_done = nullptr) {
+  if (colsum_done) *colsum_done = false;
   VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "gemm: bad dtype %d", dtype);
   VITMI_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return VITMI_OK;
@@ -1138,6 +1170,10 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
     g.k_per_split = (K > 0 ? ktiles : 1) * BK;
     g.tail_ws = (float*)ws;   // tail split of the persistent gemm256 launch (if it fits)
     g.tail_ws_bytes = ws ? ws_bytes : 0;
+    if (colsum && big_ok && dtype == VITMI_BF16 && epi == VITMI_EPI_DGELU) {
+      g.colsum = colsum;      // fused column sums (gemm256 DGELU epilogue only)
+      if (colsum_done) *colsum_done = true;
+    }
     if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
     return dispatch<float>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
   }
@@ -1228,6 +1264,36 @@ extern "C" int vitmi_linear_dgrad(int dtype, int64_t M, int64_t N, int64_t K, co
   // dx[M,K] = dy[M,N] . W[N,K]: reduction over N; A = dy (k-major), B = W as [N][K] (n-major)
   return gemm_impl(dtype, 1, 0, M, K, N, dy, N, w, K, dx, K, dx_dtype, epilogue, nullptr,
                    const_cast<void*>(aux), K, nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, false);
+}
+
+// Column-sum partial rows of the fused DGELU epilogue (two per 256-row tile).
+static int64_t colsum_rows(int64_t M) { return ((M + 255) / 256) * 2; }
+
+extern "C" size_t vitmi_linear_dgrad_bias_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
+  const size_t fused = (size_t)colsum_rows(M) * K * sizeof(float);
+  const size_t unfused = vitmi_bias_grad_workspace_size(M, K);   // the GEMM runs without a tail split
+  return fused > unfused ? fused : unfused;
+}
+
+extern "C" int vitmi_linear_dgrad_bias(int dtype, int64_t M, int64_t N, int64_t K, const void* dy,
+                                       const void* w, void* dx, int dx_dtype, int epilogue, const void* aux,
+                                       float* db, void* workspace, size_t ws_bytes, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_DGELU,
+                  "linear_dgrad_bias: bad epilogue %d", epilogue);
+  VITMI_CHECK_ARG(db != nullptr, "linear_dgrad_bias: db is null");
+  VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_linear_dgrad_bias_workspace_size(dtype, M, N, K),
+                  "linear_dgrad_bias: workspace too small");
+  if (M == 0 || K == 0) return VITMI_OK;
+  hipStream_t s = (hipStream_t)stream;
+  bool fused = false;
+  // the partial rows live in the workspace; the tail split is off on this path, so the
+  // GEMM itself needs no other workspace
+  int rc = gemm_impl(dtype, 1, 0, M, K, N, dy, N, w, K, dx, K, dx_dtype, epilogue, nullptr, const_cast<void*>(aux),
+                     K, nullptr, 0, nullptr, 0, s, false, nullptr, (float*)workspace, &fused);
+  if (rc) return rc;
+  if (fused) return launch_colsum_finish(K, (int)colsum_rows(M), (const float*)workspace, db, s);
+  // other paths (128x128 kernel, fp32): separate column-sum pass over dx
+  return vitmi_bias_grad(dx_dtype, M, K, dx, K, db, workspace, ws_bytes, stream);
 }
 
 extern "C" size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {

@@ -66,6 +66,8 @@ SIGNATURES = {
     "vitmi_sls_resize_table": (I, [I, I, P, P]),
     "vitmi_sls_preprocess": (I, [I, I, I, P, L, L, I, I, I, P, P, P, P, P, P]),
     "vitmi_gather_rows": (I, [L, L, P, L, P, P, P]),
+    "vitmi_linear_dgrad_bias_workspace_size": (S, [I, L, L, L]),
+    "vitmi_linear_dgrad_bias": (I, [I, L, L, L, P, P, P, I, I, P, P, P, S, P]),
     "vitmi_adam_step": (I, [L, P, P, P, P, P, F, D, D, F, F, P]),
     "vitmi_dense_f32_fwd": (I, [I, I, I, P, L, P, P, P, L, I, P]),
     "vitmi_dense_f32_bwd": (I, [I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, P]),

@@ -291,12 +291,11 @@ class _CvTBlockFn(torch.autograd.Function):
         g2 = dout.contiguous().view(M, D).float()
         g2_lp = g2 if T == F32 else ops.cast_bf16(g2)
         # MLP
-        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u)
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias))
         ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
         ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
         dh2 = ops.linear_dgrad(du, w1, T)
         ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
-        ops.bias_grad(du, _grad(mlp.fc1.bias))
         dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias), dres=g2,
                                         lp_dtype=lpT)
         if dx1_lp is None:

@@ -316,12 +316,11 @@ class _MlpFn(torch.autograd.Function):
         T = xo.dtype
         g = dy.contiguous().float().view(-1, dy.shape[-1])
         g_lp = _take_lp(g, T)
-        du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u)
+        du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mod.fc1.bias))
         ops.linear_wgrad(g_lp, a, _grad(mod.fc2.weight))
         ops.bias_grad(g_lp, _grad(mod.fc2.bias))
         dx = ops.linear_dgrad(du, w1, F32)
         ops.linear_wgrad(du, xo, _grad(mod.fc1.weight))
-        ops.bias_grad(du, _grad(mod.fc1.bias))
         return (dx.view(ctx.shape), None, None, None, None, None)
 
 
@@ -410,13 +409,13 @@ class _BlockFn(torch.autograd.Function):
             g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
         # MLP branch
         dev = g2.device
-        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u)
+        # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias))
         with _OnSide(dev, g2_lp, act, du, h2):
             ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
             if not ctx.bias_done:
                 ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
             ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
-            ops.bias_grad(du, _grad(mlp.fc1.bias))
         dh2 = ops.linear_dgrad(du, w1, T)
         # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
         if drop is None:

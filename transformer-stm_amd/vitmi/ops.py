@@ -7,6 +7,7 @@ fallback — a missing library or a bad shape raises.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -124,17 +125,37 @@ def dropout_apply(x: Tensor, seed: int, site: int, rate: float, out_dtype: torch
 
 
 def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = EPI_STORE,
-                 aux: Optional[Tensor] = None) -> Tensor:
-    """dx[M,K] = dy[M,N] W[N,K] (optionally * aux, the gelu' saved by the forward)."""
+                 aux: Optional[Tensor] = None, bias_grad: Optional[Tensor] = None) -> Tensor:
+    """dx[M,K] = dy[M,N] W[N,K] (optionally * aux, the gelu' saved by the forward).
+    ``bias_grad`` (fp32 [K]) += column sums of dx, fused into the GEMM epilogue where the
+    kernel allows (vitmi_linear_dgrad_bias)."""
     assert dy.is_contiguous() and w.is_contiguous() and dy.dtype == w.dtype
     M, N = dy.numel() // dy.shape[-1], dy.shape[-1]
     K = w.shape[1]
     dx = torch.empty(*dy.shape[:-1], K, dtype=out_dtype, device=dy.device)
+    if bias_grad is not None and not _FUSED_BIAS:       # A/B switch: separate column-sum pass
+        dx = linear_dgrad(dy, w, out_dtype, epilogue, aux)
+        bias_grad_(dx, bias_grad)
+        return dx
+    if bias_grad is not None:
+        assert bias_grad.dtype == torch.float32 and bias_grad.is_contiguous() and bias_grad.numel() == K
+        nws = lib().vitmi_linear_dgrad_bias_workspace_size(dt(dy.dtype), M, N, K)
+        ws = _ws(nws, dy)
+        check(lib().vitmi_linear_dgrad_bias(dt(dy.dtype), M, N, K, _p(dy), _p(w), _p(dx), dt(out_dtype), epilogue,
+                                            _p(aux), _p(bias_grad), _p(ws), ws.numel(), _s()), "linear_dgrad_bias")
+        return dx
     nws = lib().vitmi_linear_dgrad_workspace_size(dt(dy.dtype), M, N, K)
     ws = _ws(nws, dy) if nws else None
     check(lib().vitmi_linear_dgrad(dt(dy.dtype), M, N, K, _p(dy), _p(w), _p(dx), dt(out_dtype),
                                    epilogue, _p(aux), _p(ws), nws, _s()), "linear_dgrad")
     return dx
+
+
+_FUSED_BIAS = os.environ.get("VITMI_FUSED_BIAS", "1") != "0"
+
+
+def bias_grad_(dy: Tensor, db: Tensor) -> None:
+    bias_grad(dy, db)
 
 
 def linear_wgrad(dy: Tensor, x: Tensor, dw: Tensor) -> None:
