@@ -137,6 +137,14 @@ int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, con
                         const void* o, const void* dout, const float* lse, void* dqkv,
                         void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_attention_bwd_workspace_size(int B, int N, int H);
+/* vitmi_attention_bwd plus the qkv bias gradient: dbias[3*H*dh] += column sums of dqkv (the
+ * q/k/v Dense biases, models/CvT(Par).py:132-134).  On the whole-sequence bf16 path (N <= 256)
+ * the sums come from the dQ and dK/dV kernels' registers (per (batch, head) block, then a
+ * fixed-order fold over the batch); elsewhere from a second pass over dqkv. */
+size_t vitmi_attention_bwd_bias_workspace_size(int B, int N, int H);
+int vitmi_attention_bwd_bias(int dtype, int B, int N, int H, int dh, float scale, const void* qkv, const void* o,
+                             const void* dout, const float* lse, void* dqkv, float* dbias, void* workspace,
+                             size_t ws_bytes, vitmi_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Patch embedding Conv2D(k=P, s=P) as a GEMM (models/CvT(Par).py:203-212;

@@ -273,6 +273,26 @@ def test_attention_fwd_bwd(B, N, H, T, attn_path):
         assert rel(d[:, i], g[:, i]) < (2e-2 if T == BF else 1e-5), name
 
 
+@pytest.mark.parametrize("B,N,H,T", [(2, 197, 2, BF), (3, 17, 1, BF), (1, 256, 3, BF), (2, 1, 2, BF),
+                                     (2, 300, 1, BF), (2, 33, 2, torch.float32)])
+def test_attention_bwd_fused_bias(B, N, H, T):
+    """the q/k/v bias gradient out of the attention backward kernels (padded keys of the
+    whole-sequence kernels excluded) == a column-sum pass over dqkv"""
+    D = 64 * H
+    qkv = rnd(B * N, 3 * D, dtype=T, seed=25).to(DEV)
+    o, lse = ops.attention_fwd(qkv, B, N, H, 0.125)
+    do = rnd(B * N, D, dtype=T, seed=26).to(DEV)
+    ref = ops.attention_bwd(qkv, o, do, lse, B, N, H, 0.125)
+    db_ref = torch.full((3 * D,), 0.25, device=DEV)
+    ops.bias_grad(ref, db_ref)
+    db = torch.full((3 * D,), 0.25, device=DEV)
+    dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, H, 0.125, bias_grad=db)
+    assert torch.equal(dqkv, ref)
+    # fused sums add fp32 values before dqkv's bf16 rounding
+    assert rel(db, db_ref) < (3e-3 if T == BF else 1e-5)
+    assert rel(db - 0.25, ref.float().sum(0)) < (3e-3 if T == BF else 1e-5)
+
+
 def test_attention_softmax_spike(attn_path):
     """A key row that dominates one query forces the online-softmax rescale branch."""
     B, N, H = 1, 197, 1

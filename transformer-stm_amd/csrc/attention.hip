@@ -601,6 +601,27 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   }
 }
 
+// Column sums of a [rows][64] fp32 LDS image (row pitch 65 floats: conflict-free row writes and
+// column reads) over its first 32*nw rows, in a fixed order: thread (c = tid % 64, row group
+// rg = tid / 64) sums rows 32rg..32rg+31 of column c, then 64 threads fold the groups.
+// part[c] = mul * sum.  All threads of the block must call it.
+__device__ __forceinline__ void lds_colsum64(const float* img, int nw, float* __restrict__ part, float mul,
+                                             float (*red)[64]) {
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  float t = 0.f;
+  if (rg < nw) {
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) t += img[(rg * 32 + i) * 65 + c];
+  }
+  red[rg][c] = t;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float u = 0.f;
+    for (int w = 0; w < nw; ++w) u += red[w][threadIdx.x];
+    part[threadIdx.x] = u * mul;
+  }
+}
+
 // dQ (+ delta = rowsum(dO * O)): grid B*H, block 64*NW, wave w owns queries 32w..+31, K and V
 // of the whole sequence in LDS.  Keys >= N need no mask: their K rows are zero in LDS, so
 // their dS (whatever it is) meets a zero row of K in dQ = dS K.
@@ -608,8 +629,10 @@ template <int NPMAX>
 __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dq_seq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
-    float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128];
+    float scale, float* __restrict__ colsum) {
+  // K | V images; after the loop also the [NP][65] fp32 image of the fused bias column sums
+  constexpr int SMEM = 2 * NPMAX * 128 > NPMAX * 65 * 4 ? 2 * NPMAX * 128 : NPMAX * 65 * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6, NP = nw * 32;
@@ -679,16 +702,46 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dq_seq_bf16(
       for (int d2 = 0; d2 < 2; ++d2) dqt[d2] = mfma32(frag_tr(kt, k0 + 16 * s, 32 * d2, lane), sb, dqt[d2]);
     }
   }
-  if (!qok) return;
-  bf16* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
+  if (qok) {
+    bf16* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
 #pragma unroll
-  for (int d2 = 0; d2 < 2; ++d2)
+    for (int d2 = 0; d2 < 2; ++d2)
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 32 * d2 + 8 * g4 + 4 * h;
-      store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale, dqt[d2][4 * g4 + 2] * scale,
-             dqt[d2][4 * g4 + 3] * scale);
-    }
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * d2 + 8 * g4 + 4 * h;
+        store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale, dqt[d2][4 * g4 + 2] * scale,
+               dqt[d2][4 * g4 + 3] * scale);
+      }
+  }
+  if (colsum) {
+    // Bias gradients of this (batch, head), from exact identities of softmax attention:
+    //   q: sum_q dQ[q]                          (rows q >= N are 0 here: P = 0 there)
+    //   k: sum_k dK[k] = sum_q (sum_k dS[q][k]) Q[q] = 0, since every row of dS sums to 0
+    //      (softmax is invariant to a shift shared by all keys)
+    //   v: sum_k dV[k] = sum_q (sum_k P[q][k]) dO[q] = sum_q dO[q], since rows of P sum to 1
+    // so the dK/dV kernel needs no reduction (its padded-key lanes would need masking) and
+    // the v part is a column sum of the dO rows this kernel already holds (zero past N).
+    // The rows go through the K/V LDS area (free after the loop), not through shuffles,
+    // which would keep extra registers live.
+    __shared__ float red[NPMAX / 32][64];
+    float* img = (float*)smem;   // [NP][65] fp32 <= 2 * NPMAX * 128 bytes
+    float* part = colsum + (int64_t)b * 3 * D + hd * DH;
+    __syncthreads();
+#pragma unroll
+    for (int d2 = 0; d2 < 2; ++d2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) img[q * 65 + 32 * d2 + acc_row(r, h)] = dqt[d2][r];
+    __syncthreads();
+    lds_colsum64(img, nw, part, scale, red);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) img[q * 65 + 16 * s + 8 * h + j] = (float)df[s][j];
+    __syncthreads();
+    lds_colsum64(img, nw, part + 2 * D, 1.f, red);
+    if (threadIdx.x < 64) part[D + threadIdx.x] = 0.f;
+  }
 }
 
 // dK/dV: grid B*H, block 64*NW, wave w owns keys 32w..+31; Q, dO, lse*log2e and delta of the
@@ -696,7 +749,8 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dq_seq_bf16(
 template <int NPMAX>
 __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale,
+    float* __restrict__ colsum) {
   // one LDS object: [Q | dO] images, then L2[NPMAX], delta[NPMAX]
   __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128 + 2 * NPMAX * 4];
   const int lane = threadIdx.x & 63;
@@ -766,18 +820,20 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
       }
     }
   }
-  if (key >= N) return;
-  bf16* row = dqkv + ((int64_t)b * N + key) * ld;
+  if (key < N) {
+    bf16* row = dqkv + ((int64_t)b * N + key) * ld;
 #pragma unroll
-  for (int d2 = 0; d2 < 2; ++d2)
+    for (int d2 = 0; d2 < 2; ++d2)
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 32 * d2 + 8 * g4 + 4 * h;
-      store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
-             dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
-      store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
-             dvt[d2][4 * g4 + 3]);
-    }
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * d2 + 8 * g4 + 4 * h;
+        store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
+               dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
+        store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
+               dvt[d2][4 * g4 + 3]);
+      }
+  }
+  (void)colsum;   // the k / v bias gradients come from the dQ kernel (see there)
 }
 
 // ============================================ persistent, pipelined whole-sequence kernels
@@ -1360,10 +1416,10 @@ extern "C" size_t vitmi_attention_bwd_workspace_size(int B, int N, int H) {
   return (size_t)B * H * N * sizeof(float);
 }
 
-extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale,
-                                   const void* qkv, const void* o, const void* dout,
-                                   const float* lse, void* dqkv, void* workspace, size_t ws_bytes,
-                                   vitmi_stream_t stream) {
+static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scale, const void* qkv, const void* o,
+                              const void* dout, const float* lse, void* dqkv, void* workspace, size_t ws_bytes,
+                              vitmi_stream_t stream, float* colsum, bool* colsum_done) {
+  if (colsum_done) *colsum_done = false;
   if (int rc = attn_check(dtype, B, N, H, dh)) return rc;
   VITMI_CHECK_ARG(qkv && o && dout && lse && dqkv, "attention_bwd: null pointer");
   VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_attention_bwd_workspace_size(B, N, H),
@@ -1375,16 +1431,17 @@ extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float
   if (dtype == VITMI_BF16 && seq_path(N)) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
     const dim3 block(64 * ((N + 31) / 32));
-    if (const int g = pp_grid(B * H)) {
+    if (const int g = colsum ? 0 : pp_grid(B * H)) {
       hipLaunchKernelGGL(attn_bwd_dq_pp_bf16<SEQ_MAX>, dim3(g), block, 0, s, (const bf16*)qkv, (const bf16*)o,
                          (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, B * H);
       hipLaunchKernelGGL(attn_bwd_dkv_pp_bf16<SEQ_MAX>, dim3(g), block, 0, s, (const bf16*)qkv,
                          (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, B * H);
     } else {
       hipLaunchKernelGGL(attn_bwd_dq_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
-                         (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale);
+                         (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
       hipLaunchKernelGGL(attn_bwd_dkv_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
-                         (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
+                         (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum);
+      if (colsum_done) *colsum_done = colsum != nullptr;
     }
   } else if (dtype == VITMI_BF16) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
@@ -1404,4 +1461,36 @@ extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float
   }
   VITMI_LAUNCH_CHECK("attention_bwd");
   return VITMI_OK;
+}
+
+extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale,
+                                   const void* qkv, const void* o, const void* dout,
+                                   const float* lse, void* dqkv, void* workspace, size_t ws_bytes,
+                                   vitmi_stream_t stream) {
+  return attention_bwd_impl(dtype, B, N, H, dh, scale, qkv, o, dout, lse, dqkv, workspace, ws_bytes, stream, nullptr,
+                            nullptr);
+}
+
+extern "C" size_t vitmi_attention_bwd_bias_workspace_size(int B, int N, int H) {
+  const size_t delta = ((size_t)B * H * N * sizeof(float) + 255) / 256 * 256;
+  const size_t part = (size_t)B * 3 * H * DH * sizeof(float);
+  const size_t fallback = vitmi_bias_grad_workspace_size((int64_t)B * N, 3LL * H * DH);
+  return delta + (part > fallback ? part : fallback);
+}
+
+extern "C" int vitmi_attention_bwd_bias(int dtype, int B, int N, int H, int dh, float scale, const void* qkv,
+                                        const void* o, const void* dout, const float* lse, void* dqkv,
+                                        float* dbias, void* workspace, size_t ws_bytes, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(dbias != nullptr, "attention_bwd_bias: dbias is null");
+  VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_attention_bwd_bias_workspace_size(B, N, H),
+                  "attention_bwd_bias: workspace too small");
+  const size_t delta = ((size_t)B * H * N * sizeof(float) + 255) / 256 * 256;
+  float* part = (float*)((char*)workspace + delta);
+  bool done = false;
+  if (int rc = attention_bwd_impl(dtype, B, N, H, dh, scale, qkv, o, dout, lse, dqkv, workspace, delta,
+                                  stream, part, &done))
+    return rc;
+  const int64_t D3 = 3LL * H * DH;
+  if (done) return launch_colsum_finish(D3, B, part, dbias, (hipStream_t)stream);
+  return vitmi_bias_grad(dtype, (int64_t)B * N, D3, dqkv, D3, dbias, part, ws_bytes - delta, stream);
 }

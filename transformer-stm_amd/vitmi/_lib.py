@@ -68,6 +68,8 @@ SIGNATURES = {
     "vitmi_gather_rows": (I, [L, L, P, L, P, P, P]),
     "vitmi_linear_dgrad_bias_workspace_size": (S, [I, L, L, L]),
     "vitmi_linear_dgrad_bias": (I, [I, L, L, L, P, P, P, I, I, P, P, P, S, P]),
+    "vitmi_attention_bwd_bias_workspace_size": (S, [I, I, I]),
+    "vitmi_attention_bwd_bias": (I, [I, I, I, I, I, F, P, P, P, P, P, P, P, S, P]),
     "vitmi_adam_step": (I, [L, P, P, P, P, P, F, D, D, F, F, P]),
     "vitmi_dense_f32_fwd": (I, [I, I, I, P, L, P, P, P, L, I, P]),
     "vitmi_dense_f32_bwd": (I, [I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, P]),

@@ -273,11 +273,10 @@ class _AttentionFn(torch.autograd.Function):
         do = ops.linear_dgrad(g_lp, wo, T)
         ops.linear_wgrad(g_lp, o, _grad(mod.proj.weight))
         ops.bias_grad(g_lp, _grad(mod.proj.bias))
-        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, mod.num_heads, mod.scale)
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, mod.num_heads, mod.scale,
+                                 bias_grad=_grad(mod.qkv.bias) if mod.qkv.bias is not None else None)
         dx = ops.linear_dgrad(dqkv, wq, F32)
         ops.linear_wgrad(dqkv, xo, _grad(mod.qkv.weight))
-        if mod.qkv.bias is not None:
-            ops.bias_grad(dqkv, _grad(mod.qkv.bias))
         return (dx.view(B, N, D), None) + (None,) * len(mod._params())
 
 
@@ -432,11 +431,11 @@ class _BlockFn(torch.autograd.Function):
         do = ops.linear_dgrad(dx1_lp, wo, T)
         with _OnSide(dev, dx1_lp, o):
             ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
-        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale)
+        # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale,
+                                 bias_grad=_grad(a_.qkv.bias) if a_.qkv.bias is not None else None)
         with _OnSide(dev, dqkv, h1):
             ops.linear_wgrad(dqkv, h1, _grad(a_.qkv.weight))
-            if a_.qkv.bias is not None:
-                ops.bias_grad(dqkv, _grad(a_.qkv.bias))
         dh1 = ops.linear_dgrad(dqkv, wq, T)
         prev = ctx.prev_bias
         dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),

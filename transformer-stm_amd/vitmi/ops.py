@@ -151,7 +151,11 @@ def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = 
     return dx
 
 
-_FUSED_BIAS = os.environ.get("VITMI_FUSED_BIAS", "1") != "0"
+_FUSED_BIAS = os.environ.get("VITMI_FUSED_BIAS", "1") != "0"          # fc1 bias in the DGELU dgrad
+# qkv bias from the attention backward (q: dQ column sums in the dQ kernel; k: 0 and v: column
+# sums of dO, exact softmax identities).  Measured neutral end to end (the dQ kernel's extra
+# LDS pass costs what the separate column-sum pass over dqkv did), so off by default.
+_FUSED_QKV_BIAS = os.environ.get("VITMI_FUSED_QKV_BIAS", "0") != "0"
 
 
 def bias_grad_(dy: Tensor, db: Tensor) -> None:
@@ -246,10 +250,23 @@ def attention_fwd(qkv: Tensor, B: int, N: int, H: int, scale: float):
 
 
 def attention_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, B: int, N: int, H: int,
-                  scale: float) -> Tensor:
+                  scale: float, bias_grad: Optional[Tensor] = None) -> Tensor:
+    """dqkv; ``bias_grad`` (fp32 [3D]) += its column sums (the q/k/v bias gradient), fused into
+    the backward kernels where they allow (vitmi_attention_bwd_bias)."""
     D = o.shape[-1]
     assert do.is_contiguous() and do.dtype == qkv.dtype
     dqkv = torch.empty_like(qkv)
+    if bias_grad is not None and not _FUSED_QKV_BIAS:
+        dqkv = attention_bwd(qkv, o, do, lse, B, N, H, scale)
+        bias_grad_(dqkv, bias_grad)
+        return dqkv
+    if bias_grad is not None:
+        assert bias_grad.dtype == torch.float32 and bias_grad.numel() == 3 * D and bias_grad.is_contiguous()
+        ws = _ws(lib().vitmi_attention_bwd_bias_workspace_size(B, N, H), qkv)
+        check(lib().vitmi_attention_bwd_bias(dt(qkv.dtype), B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(do),
+                                             _p(lse), _p(dqkv), _p(bias_grad), _p(ws), ws.numel(), _s()),
+              "attention_bwd_bias")
+        return dqkv
     ws = _ws(lib().vitmi_attention_bwd_workspace_size(B, N, H), qkv)
     check(lib().vitmi_attention_bwd(dt(qkv.dtype), B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(do),
                                     _p(lse), _p(dqkv), _p(ws), ws.numel(), _s()), "attention_bwd")
