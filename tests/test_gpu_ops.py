@@ -275,9 +275,10 @@ def test_attention_fwd_bwd(B, N, H, T, attn_path):
 
 @pytest.mark.parametrize("B,N,H,T", [(2, 197, 2, BF), (3, 17, 1, BF), (1, 256, 3, BF), (2, 1, 2, BF),
                                      (2, 300, 1, BF), (2, 33, 2, torch.float32)])
-def test_attention_bwd_fused_bias(B, N, H, T):
-    """the q/k/v bias gradient out of the attention backward kernels (padded keys of the
-    whole-sequence kernels excluded) == a column-sum pass over dqkv"""
+def test_attention_bwd_fused_bias(B, N, H, T, monkeypatch):
+    """the q/k/v bias gradient out of the attention backward kernels (q: dQ column sums;
+    k: 0, v: column sums of dO by the softmax identities) == a column-sum pass over dqkv"""
+    monkeypatch.setattr(ops, "_FUSED_QKV_BIAS", True)
     D = 64 * H
     qkv = rnd(B * N, 3 * D, dtype=T, seed=25).to(DEV)
     o, lse = ops.attention_fwd(qkv, B, N, H, 0.125)
