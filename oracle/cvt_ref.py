@@ -80,6 +80,7 @@ class CvTConfig:
     avg_count_pad: bool = False       # 'avg' divisor: False = TF 'same' in-bounds count; True = torch's 9
     proc_dim: int = 0                 # process parameters (5 in the reference, :392); 0 = image only
     proc_hidden: int = 256            # Proc_Dense_1/2 width (:343-344)
+    drop_rate: float = 0.0            # Dropout after proj (:141,189) and both MLP Dense (:255,257)
     dtype: str = "bf16"
 
     def replace(self, **kw) -> "CvTConfig":
@@ -191,8 +192,13 @@ def dw_bn(x: Tensor, w: Tensor, gamma: Tensor, beta: Tensor, eps: float) -> Tens
     return F.batch_norm(z, None, None, gamma, beta, training=True, eps=eps)
 
 
-def block(x: Tensor, hw: Tuple[int, int], p: Dict[str, Tensor], pre: str, cfg: CvTConfig, st: CvTStage) -> Tensor:
-    """ConvTransformerBlock.call (models/CvT(Par).py:261-289) on tokens [B, N, D]."""
+def block(x: Tensor, hw: Tuple[int, int], p: Dict[str, Tensor], pre: str, cfg: CvTConfig, st: CvTStage,
+          drop=None) -> Tensor:
+    """ConvTransformerBlock.call (models/CvT(Par).py:261-289) on tokens [B, N, D].  ``drop`` =
+    (seed, rate, site0): training-mode Dropout with the build's counter-hash masks
+    (oracle/vit_ref.py ``dropout``) at sites site0 (proj), +1 (GELU output), +2 (fc2)."""
+    from oracle.vit_ref import dropout as _dropout
+    dp = (lambda t, j: t) if drop is None else (lambda t, j: _dropout(t, drop[0], drop[2] + j, drop[1]))
     B, N, D = x.shape
     H, W = hw
     Hh = st.num_heads
@@ -219,18 +225,20 @@ def block(x: Tensor, hw: Tuple[int, int], p: Dict[str, Tensor], pre: str, cfg: C
     scale = dh ** -0.5 if cfg.attn_scale == "head" else D ** -0.5
     a = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * scale, dim=-1)
     o = torch.matmul(a, v).transpose(1, 2).reshape(B, N, D)
-    x = x + F.linear(o, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"])
+    x = x + dp(F.linear(o, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"]), 0)
     y = F.layer_norm(x, (D,), n2w, n2b, cfg.ln_eps)
-    y = F.linear(F.gelu(F.linear(y, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])),
-                 p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"])
+    y = dp(F.gelu(F.linear(y, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])), 1)
+    y = dp(F.linear(y, p[pre + "mlp.fc2.weight"], p[pre + "mlp.fc2.bias"]), 2)
     return x + y
 
 
-def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, capture: Optional[list] = None) -> Tensor:
+def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, capture: Optional[list] = None,
+                     drop_seed: Optional[int] = None) -> Tensor:
     """Stages 1..S; returns LN(final cls token) [B, D] (the token mean without cls, :337-340)."""
     x = img
     tok = None
     t = None
+    bi = 0
     for i, st in enumerate(cfg.stages):
         pre = f"stage{i}."
         x = conv_embed(x, p[pre + "embed.weight"], p[pre + "embed.bias"], st)
@@ -241,7 +249,9 @@ def forward_features(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, capture:
         if st.with_cls_token:
             t = torch.cat([p[pre + "cls_token"].expand(B, 1, D), t], dim=1)
         for j in range(st.depth):
-            t = block(t, (H, W), p, f"{pre}blocks.{j}.", cfg, st)
+            drop = None if (drop_seed is None or cfg.drop_rate <= 0) else (drop_seed, cfg.drop_rate, 3 * bi)
+            t = block(t, (H, W), p, f"{pre}blocks.{j}.", cfg, st, drop)
+            bi += 1
         if capture is not None:
             capture.append((t, H, st.with_cls_token))
         if st.with_cls_token:
@@ -259,9 +269,9 @@ def proc_features(proc: Tensor, p: Dict[str, Tensor]) -> Tensor:
 
 
 def forward(img: Tensor, p: Dict[str, Tensor], cfg: CvTConfig, proc: Optional[Tensor] = None,
-            capture: Optional[list] = None) -> Tensor:
+            capture: Optional[list] = None, drop_seed: Optional[int] = None) -> Tensor:
     """Image features (+ concatenated process features, :347) -> Final_Dense (:350)."""
-    f = forward_features(img, p, cfg, capture)
+    f = forward_features(img, p, cfg, capture, drop_seed)
     if cfg.proc_dim:
         f = torch.cat([f, proc_features(proc, p)], dim=1)
     return F.linear(f, p["head.weight"], p["head.bias"])
@@ -274,9 +284,9 @@ def loss_fn(logits: Tensor, target: Tensor, num_classes: int) -> Tensor:
 
 
 def forward_backward(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg: CvTConfig,
-                     proc: Optional[Tensor] = None):
+                     proc: Optional[Tensor] = None, drop_seed: Optional[int] = None):
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
-    logits = forward(img, leaves, cfg, proc)
+    logits = forward(img, leaves, cfg, proc, drop_seed=drop_seed)
     loss = loss_fn(logits, target, cfg.num_classes)
     loss.backward()
     return logits.detach(), loss.detach(), {k: v.grad.detach() for k, v in leaves.items()}

@@ -177,3 +177,37 @@ def test_dense_f32_kernels(M, N, K, act):
     assert rel(dx, xr.grad) < 1e-6
     assert rel(dw - 1, wr.grad) < 1e-6          # accumulates
     assert rel(db, br.grad) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cvt_dropout_matches_oracle(dtype):
+    """Keras Dropout(0.1) after the out-projection and both MLP Dense layers (models/CvT(Par).py
+    :141,189,255,257) in training mode: the build's counter-hash masks, fused into the GEMM
+    epilogues, regenerated in the backward -- identical masks in the oracle for a fixed seed."""
+    ocfg = cvt_ref.CvTConfig(img_size=64, num_classes=1, dtype="fp32", drop_rate=0.1, proc_dim=5)
+    params = cvt_ref.init_params(ocfg, seed=6)
+    img, tgt = cvt_ref.synthetic_batch(ocfg, 3, seed=8)
+    proc = cvt_ref.synthetic_proc(ocfg, 3)
+    logits_ref, loss_ref, gref = cvt_ref.forward_backward(img, tgt, params, ocfg, proc, drop_seed=4242)
+    no_drop, _, _ = cvt_ref.forward_backward(img, tgt, params, ocfg.replace(drop_rate=0.0), proc)
+    assert rel(no_drop, logits_ref) > 1e-3            # the masks change the output
+    model = cvt.CvT(product_cfg(ocfg, dtype)).to(DEV)
+    model.load_param_dict(params)
+    model.train()
+    model.drop_seed = 4242
+    logits = model(img.to(DEV), proc.to(DEV))
+    mse_loss(logits, tgt.to(DEV)).backward()
+    tl, tg = (1e-4, 1e-3) if dtype == "fp32" else (3e-2, 8e-2)
+    assert rel(logits, logits_ref) < tl
+    bad = {}
+    for k, p in model.named_parameters():
+        if k.endswith("attn.proj_k.bias") or (k.endswith("attn.conv_proj_k.bn.bias") and "stage2" not in k):
+            continue   # exact-zero gradients (softmax shift invariance), see test_cvt_keras_spec_vs_oracle
+        r = rel(p.grad, gref[k], 1e-4)
+        if r >= tg:
+            bad[k] = r
+    assert not bad, bad
+    model.eval()                                       # inference: no dropout
+    with torch.no_grad():
+        assert torch.equal(model(img.to(DEV), proc.to(DEV)), model(img.to(DEV), proc.to(DEV)))

@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .modules import F32, LayerNorm, Linear, _check_cuda, _grad, _lp, cross_entropy, mse_loss  # noqa: F401
+from .modules import F32, LayerNorm, Linear, _check_cuda, _drop_args, _grad, _lp, cross_entropy, mse_loss  # noqa: F401
 
 Tensor = torch.Tensor
 
@@ -76,6 +76,9 @@ class CvTConfig:
     avg_count_pad: bool = False    # 'avg' divisor: TF 'same' in-bounds count (False) or torch's 9
     proc_dim: int = 0              # process parameters (5 in the reference, :392); 0 = image only
     proc_hidden: int = 256         # Proc_Dense_1/2 width (:343-344)
+    # Dropout after the out-projection (:141,189) and after both MLP Dense layers (:255,257);
+    # Keras default 0.1 in training.  0 = the parity / benchmark configuration.
+    drop_rate: float = 0.0
     dtype: str = "bf16"
 
     def replace(self, **kw) -> "CvTConfig":
@@ -216,9 +219,9 @@ class CvTBlock(nn.Module):
     def _norm2(self) -> LayerNorm:
         return self.norm1 if self.tie_norms else self.norm2
 
-    def forward(self, x: Tensor, H: int, W: int, with_cls: bool) -> Tensor:
+    def forward(self, x: Tensor, H: int, W: int, with_cls: bool, drop=None) -> Tensor:
         _check_cuda(x)
-        return _CvTBlockFn.apply(x, self, H, W, with_cls, *self.parameters())
+        return _CvTBlockFn.apply(x, self, H, W, with_cls, drop, *self.parameters())
 
 
 class _CvTBlockFn(torch.autograd.Function):
@@ -227,7 +230,7 @@ class _CvTBlockFn(torch.autograd.Function):
     (models/CvT(Par).py:146-150,164-176)."""
 
     @staticmethod
-    def forward(ctx, x, blk, H, W, with_cls, *params):
+    def forward(ctx, x, blk, H, W, with_cls, drop, *params):
         cfg = blk.cfg
         T = ops.torch_dtype(cfg.dtype)
         B, N, D = x.shape
@@ -266,14 +269,17 @@ class _CvTBlockFn(torch.autograd.Function):
             ops.gemm(inp, wl, True, True, M, D, D, qkv[:, c_i * D:(c_i + 1) * D], ops.EPI_STORE, bias=lin.bias)
             saved_proj += [inp, z, mean, rstd, wl]
         o, lse = ops.attention_fwd(qkv, B, N, Hh, scale)
+        dr = [None, None, None]
+        if drop is not None:   # (seed, rate, site0): sites site0 (proj), +1 (GELU), +2 (fc2)
+            dr = [(drop[0], drop[2] + j, drop[1]) for j in range(3)]
         wo = _lp(blk, a_.proj.weight, T)
-        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2)
+        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
         h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, cfg.ln_eps, T)
         w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
-        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU)
-        out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
+        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1])
+        out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])
         ctx.save_for_backward(x2, h, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wo, w1, w2, *saved_proj)
-        ctx.blk, ctx.dims = blk, (B, N, D, H, W, with_cls, scale)
+        ctx.blk, ctx.dims, ctx.drop = blk, (B, N, D, H, W, with_cls, scale), drop
         return out.view(B, N, D)
 
     @staticmethod
@@ -289,7 +295,11 @@ class _CvTBlockFn(torch.autograd.Function):
         a_, mlp = blk.attn, blk.mlp
         n1, n2 = blk.norm1, blk._norm2
         g2 = dout.contiguous().view(M, D).float()
-        g2_lp = g2 if T == F32 else ops.cast_bf16(g2)
+        drop = ctx.drop
+        if drop is None:
+            g2_lp = g2 if T == F32 else ops.cast_bf16(g2)
+        else:   # the fc2 branch was dropped: its dgrad/wgrad/bias see g2 * mask / (1 - p)
+            g2_lp = ops.dropout_apply(g2, drop[0], drop[2] + 2, drop[1], T)
         # MLP
         du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias))
         ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
@@ -297,8 +307,10 @@ class _CvTBlockFn(torch.autograd.Function):
         dh2 = ops.linear_dgrad(du, w1, T)
         ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
         dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias), dres=g2,
-                                        lp_dtype=lpT)
-        if dx1_lp is None:
+                                        lp_dtype=lpT if drop is None else None)
+        if drop is not None:   # the out-projection branch was dropped
+            dx1_lp = ops.dropout_apply(dx1, drop[0], drop[2], drop[1], T)
+        elif dx1_lp is None:
             dx1_lp = dx1
         # attention + out-projection
         do = ops.linear_dgrad(dx1_lp, wo, T)
@@ -330,7 +342,7 @@ class _CvTBlockFn(torch.autograd.Function):
                               _grad(cp.bn.weight), _grad(cp.bn.bias), x_img=N, x_off=off, dy_img=N, dy_off=off)
             _grad(cp.weight).add_(dw9.t().reshape(D, 1, 3, 3))
         dx, _ = ops.layernorm_bwd(dh, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias), dres=dx1, lp_dtype=None)
-        return (dx.view(B, N, D), None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 5)
+        return (dx.view(B, N, D), None, None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 6)
 
 
 class ProcMlp(nn.Module):
@@ -407,6 +419,7 @@ class CvT(nn.Module):
     def __init__(self, cfg: CvTConfig):
         super().__init__()
         self.cfg = cfg
+        self.drop_seed: Optional[int] = None   # fixed dropout seed (tests); None = drawn per forward
         cin = cfg.in_chans
         for i, st in enumerate(cfg.stages):
             self.add_module(f"stage{i}", CvTStageModule(cin, st, cfg))
@@ -430,6 +443,8 @@ class CvT(nn.Module):
         t = None
         cap = getattr(self, "_capture_stage", None)
         stages = self.stages()
+        drop = _drop_args(self, self.cfg.drop_rate, 0)
+        bi = 0   # global block index: dropout sites 3*bi .. 3*bi+2
         for si, stg in enumerate(stages):
             st = stg.spec
             t, H = stg.embed(x, B, H, img_stride, row_off)          # [B, H*H, D] fp32
@@ -437,7 +452,9 @@ class CvT(nn.Module):
             if stg.cls_token is not None:
                 t = torch.cat([stg.cls_token.expand(B, 1, D), t], dim=1)
             for blk in stg.blocks:
-                t = blk(t, H, H, stg.cls_token is not None)
+                d = None if drop is None else (drop[0], drop[1], 3 * bi)
+                t = blk(t, H, H, stg.cls_token is not None, d)
+                bi += 1
             if cap is not None and si == cap % len(stages):     # Grad-CAM's activation (vitmi.gradcam)
                 if t.requires_grad:
                     t.retain_grad()
@@ -464,7 +481,7 @@ class CvT(nn.Module):
 
     def reset_parameters(self, seed: int = 0) -> None:
         """Keras initialisers: glorot_uniform kernels (Dense, Conv2D, DepthwiseConv2D), zero
-        biases / betas, unit gammas, cls token ~ N(0, 0.02)."""
+        biases / betas / cls token, unit gammas."""
         g = torch.Generator().manual_seed(seed)
         with torch.no_grad():
             for name, p in self.named_parameters():
@@ -473,8 +490,8 @@ class CvT(nn.Module):
                     t = torch.ones(p.shape) if leaf == "weight" else torch.zeros(p.shape)
                 elif leaf == "bias":
                     t = torch.zeros(p.shape)
-                elif leaf == "cls_token":
-                    t = 0.02 * torch.randn(p.shape, generator=g)
+                elif leaf == "cls_token":              # add_weight(initializer='zeros'), :245
+                    t = torch.zeros(p.shape)
                 else:
                     rf = p.shape[2] * p.shape[3] if p.dim() == 4 else 1
                     fan_in, fan_out = p.shape[1] * rf, p.shape[0] * rf
