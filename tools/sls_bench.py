@@ -5,8 +5,8 @@
   content written to a temp dir since the dataset is not on the GPU box) -> host decode
   (thread pool) -> pinned chunks -> H2D -> cv2-fixed-point resize + gray + /255 kernel ->
   HBM-resident fp32 dataset.  Reported: frames/s end to end, and the GPU conversion alone;
-  beside it the same preprocessing restated on the host (oracle/sls_ref.py numpy, 1 thread,
-  a bounded sample) as the CPU baseline.
+  beside it the reference's per-image host loop with PIL standing in for cv2 (1 thread, a
+  bounded sample) as the CPU baseline.
 * row 2, the reference's training objective: CvT (Keras spec, dw_bn, cls, process-parameter
   head) fwd + MSE + bwd + Keras Adam at batch 128 (models/CvT(Par).py:46,458-476) over
   batches gathered from the HBM-resident dataset: images/s of `vitmi.train.fit`.
@@ -77,11 +77,14 @@ def main():
         ev1.record()
         torch.cuda.synchronize()
         t_kern = ev0.elapsed_time(ev1) / 10 / 1e3
-        # host restatement (the reference's per-image cv2 work, numpy), bounded sample
-        from oracle import sls_ref
+        # the reference's per-image host work (imread -> resize -> gray -> /255, :419-423) with
+        # PIL standing in for cv2 (absent here), one thread, bounded sample
+        from PIL import Image
         t0 = time.perf_counter()
         for p in paths[:args.cpu_frames]:
-            sls_ref.sls_image(sls.decode_jpeg_rgb(p)[..., ::-1])
+            with Image.open(p) as im:
+                g8 = im.convert("RGB").resize((128, 128), Image.BILINEAR).convert("L")
+                np.asarray(g8, dtype=np.float32) / 255.0
         t_cpu = (time.perf_counter() - t0) / args.cpu_frames
     out["pipeline"] = {"frames": args.frames, "frame": "340x345 RGB JPEG -> 128x128 fp32",
                        "end_to_end_frames_per_sec": round(args.frames / t_load, 1),
@@ -89,7 +92,7 @@ def main():
                        "gpu_convert_frame_GBps_mall_resident": round(512 * (345 * 340 * 3 + 128 * 128 * 4) / t_kern / 1e9, 1),
                        "host_decode_workers": args.workers,
                        "cpu_baseline_frames_per_sec": round(1 / t_cpu, 1),
-                       "cpu_baseline": "oracle/sls_ref.py numpy restatement of cv2 resize+gray (+PIL decode), 1 thread"}
+                       "cpu_baseline": "PIL decode + bilinear resize + gray + /255 per image (cv2 absent), 1 thread"}
     # training objective on the resident dataset
     layers = 200 if images.shape[0] >= 2000 else max(1, images.shape[0] // 10)
     n_pieces = images.shape[0] // layers                 # 200 layers per piece, as the reference
