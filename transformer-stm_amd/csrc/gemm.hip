@@ -911,6 +911,35 @@ __global__ __launch_bounds__(256) void gemm_tail_fixup_kernel(GemmArgs g, int nt
   }
 }
 
+// Column-sum partial rows (GemmArgs::colsum) of the split tail tiles, which skip the fused
+// epilogue: block = (tail tile, 128-row half); thread = 4 columns x one of 4 row groups.
+template <typename TC>
+__global__ __launch_bounds__(256) void tail_colsum_kernel(GemmArgs g) {
+  __shared__ f32x4 red[4][64];
+  const int t = blockIdx.x >> 1, half = blockIdx.x & 1;
+  int tm, tn;
+  tile_rc(g, g.t_full + t, tm, tn);
+  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int64_t col = (int64_t)tn * 256 + cg * 4;
+  const int64_t r0 = (int64_t)tm * 256 + half * 128;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (col < g.N) {
+    for (int i = rg; i < 128; i += 4) {
+      const int64_t row = r0 + i;
+      if (row >= g.M) break;
+      const TC* p = (const TC*)g.C + row * g.ldc + col;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += (float)p[e];
+    }
+  }
+  red[rg][cg] = a;
+  __syncthreads();
+  if (rg == 0 && col < g.N) {
+    const f32x4 sum = red[0][cg] + red[1][cg] + red[2][cg] + red[3][cg];
+    *(f32x4*)(g.colsum + ((int64_t)tm * 2 + half) * g.N + col) = sum;
+  }
+}
+
 // ---------------------------------------------------------------- host launch
 // GEMM kernel policy: 0 = auto, 1 = always the 128x128 kernel, 2 = always gemm256 (bf16),
 // 3 = gemm256 on an 8-block persistent grid (every block walks many tiles; tests only)
@@ -1015,8 +1044,7 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       const char* tenv = getenv("VITMI_GEMM_TAIL");   // 0: no tail split (A/B timing)
       // measured: pays off for long reductions (>= 16 K-steps) and for the DGELU epilogue
       // (whose partial units skip its aux loads); a wash or a loss for K = 768 otherwise
-      // (no tail split with fused column sums: every tile must run the full epilogue)
-      const bool tail_ok = (g.k_per_split / 64 >= 16 || EPI == VITMI_EPI_DGELU) && g.colsum == nullptr;
+      const bool tail_ok = g.k_per_split / 64 >= 16 || EPI == VITMI_EPI_DGELU;
       if (splits == 1 && tail_ok && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM && g.tail_ws && !(tenv && atoi(tenv) == 0) &&
           tail_plan(nwg, gx, (int)(g.k_per_split / 64), S, ks, ntail) &&
           g.tail_ws_bytes >= (size_t)ntail * S * 256 * 256 * sizeof(float)) {
@@ -1031,6 +1059,10 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
         const int blocks = (ntail * 256 * 64 + 255) / 256;
         hipLaunchKernelGGL((gemm_tail_fixup_kernel<T, TC, EPI>), dim3(blocks), dim3(256), 0, s, g, ntail);
         VITMI_LAUNCH_CHECK("gemm_tail_fixup_kernel");
+        if (g.colsum) {   // the split tail tiles' column sums, from their finished output
+          hipLaunchKernelGGL((tail_colsum_kernel<TC>), dim3(ntail * 2), dim3(256), 0, s, g);
+          VITMI_LAUNCH_CHECK("tail_colsum_kernel");
+        }
       }
       return VITMI_OK;
     }
