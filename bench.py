@@ -29,7 +29,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from vitmi import dp, ops, optim  # noqa: E402
-from vitmi.config import config_c3  # noqa: E402
+from vitmi.config import config_c3, config_c5  # noqa: E402
 from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
 METRIC = "images/sec fwd+bwd ViT-B/16 224px bs=256/GPU at 1/2/4/8 MI355X; % MFMA roofline"
@@ -63,7 +63,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--config", choices=["c3", "c5"], default="c3",
+                    help="c3: ViT-B/16 224px bs 256/GPU (the headline metric); c5: ViT-L/16 384px bs 64/GPU "
+                         "(BASELINE config 5, N = 577 tokens: a secondary line, not the headline)")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=16)
@@ -76,8 +79,11 @@ def main():
     rank, world, local = dp.init_from_env("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cfg = config_c3()
-    B = args.batch
+    cfg = config_c3() if args.config == "c3" else config_c5()
+    B = args.batch or (256 if args.config == "c3" else 64)
+    model_name = "vit_base_16" if args.config == "c3" else "vit_large_16"
+    metric = METRIC if args.config == "c3" else \
+        "images/sec fwd+bwd ViT-L/16 384px bs=64/GPU MI355X; % MFMA roofline (BASELINE config 5)"
 
     torch.manual_seed(0)
     model = VisionTransformer(cfg).to(dev)
@@ -146,7 +152,7 @@ def main():
             traffic = None
     step_flops = cfg.flops_per_image_fwd_bwd() * B * world
     out = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(imgs, 2),
         "unit": "images/sec",
         "n_gpus": world,
@@ -158,9 +164,10 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (torch.rand images in [0,1), randint labels; random-init trunc_normal(.02) weights)",
-        "config": {"workload": "ViT-B/16 224x224x3 fwd + CE loss + bwd + RCCL grad all-reduce + Adam step",
+        "config": {"workload": f"{'ViT-B/16 224' if args.config == 'c3' else 'ViT-L/16 384'}x"
+                               f"{cfg.img_size}x3 fwd + CE loss + bwd + RCCL grad all-reduce + Adam step",
                    "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
-                   "model": "vit_base_16", "global_batch": B * world, "seq_len": cfg.seq_len,
+                   "model": model_name, "global_batch": B * world, "seq_len": cfg.seq_len,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd bf16 [{M}x{F_}x{D}] +bias+GELU",
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -169,7 +176,7 @@ def main():
         "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "loss": round(float(loss.item()), 5),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -169,46 +169,55 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(const bf16* __restrict__ qk
     }
     const char* kt = smem + buf * 16384;
     const char* vt = kt + 8192;
-    if (qw < N) {
-      f32x16 st[2];
+    // One key tile: U 32-key sub-tiles (U = 1 when the tile holds <= 32 valid keys: padded keys
+    // beyond the last 32-key group are never multiplied), the key mask only in the last tile,
+    // scale folded into the exp argument, O rescaled only when a lane's running max moved.
+    auto tile = [&](auto uc, auto mc) {
+      constexpr int U = decltype(uc)::value;
+      constexpr bool MASK = decltype(mc)::value;
+      f32x16 st[U];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         st[u] = zero16();
 #pragma unroll
         for (int s = 0; s < 4; ++s) st[u] = mfma32(frag_row(kt, 32 * u, s, lane), qf[s], st[u]);
       }
-      // scale, mask, tile max
+      if constexpr (MASK) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (t * 64 + 32 * u + acc_row(r, h) >= N) st[u][r] = -INFINITY;
+      }
       float tmax = -INFINITY;
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = t * 64 + 32 * u + acc_row(r, h);
-          const float v = key < N ? st[u][r] * c2 : -INFINITY;
-          st[u][r] = v;
-          tmax = fmaxf(tmax, v);
-        }
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[u][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m, tmax);
+      const float mn = fmaxf(m, tmax * c2);
       const float alpha = fexp2(m - mn);  // m=-inf on the first tile -> 0
+      const bool first = m == -INFINITY;
       m = mn;
       float rs = 0.f;
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(st[u][r] - mn);
+          const float p = fexp2(fmaf(st[u][r], c2, -mn));
           st[u][r] = p;
           rs += p;
         }
-      l = l * alpha + rs;
+      l = fmaf(l, alpha, rs);
+      if (!first && __builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
+        for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
+          for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
+      }
       // O^T[d][q] += V^T[d][key] P^T[key][q]
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const bf16x8 pb = pack8(st[u], s);
@@ -216,6 +225,11 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(const bf16* __restrict__ qk
           for (int dt = 0; dt < 2; ++dt)
             oacc[dt] = mfma32(frag_tr(vt, 32 * u + 16 * s, 32 * dt, lane), pb, oacc[dt]);
         }
+    };
+    if (qw < N) {
+      if (t * 64 + 64 <= N) tile(std::integral_constant<int, 2>{}, std::false_type{});
+      else if (t * 64 + 32 < N) tile(std::integral_constant<int, 2>{}, std::true_type{});
+      else tile(std::integral_constant<int, 1>{}, std::true_type{});
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -319,6 +333,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
     if (kw < N) {
 #pragma unroll 1
       for (int u = 0; u < 2; ++u) {  // 32-query sub-tile
+        if (t * 64 + 32 * u >= N) break;   // all 32 queries padding: P = 0, dS = 0 there
         f32x16 sa = zero16(), dp = zero16();
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -398,7 +413,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     df[s] = load_row16(rdo, (uint32_t)((int64_t)q * ldo + (16 * s + 8 * h) * 2));
   }
   const bool qok = q < N;
-  const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : 0.f;
+  const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
   // delta: this lane holds d = 16s + 8h + j of dO[q]; the xor-32 partner the other half
   float dl;
   {
@@ -431,18 +446,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     const char* kt = smem + buf * 16384;
     const char* vt = kt + 8192;
     if (qw < N) {
+      const bool last = t * 64 + 64 > N;   // the only tile with keys >= N
 #pragma unroll
       for (int u = 0; u < 2; ++u) {  // 32-key sub-tile
+        if (t * 64 + 32 * u >= N) break;   // all 32 keys padding: dS = 0 there
         f32x16 st = zero16(), dp = zero16();
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           st = mfma32(frag_row(kt, 32 * u, s, lane), qf[s], st);  // S^T[key][q]
           dp = mfma32(frag_row(vt, 32 * u, s, lane), df[s], dp);  // dP^T[key][q]
         }
+        if (last) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (t * 64 + 32 * u + acc_row(r, h) >= N) st[r] = -INFINITY;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int key = t * 64 + 32 * u + acc_row(r, h);
-          const float p = (key < N && qok) ? fexp2(st[r] * c2 - L2) : 0.f;
+          const float p = fexp2(fmaf(st[r], c2, -L2));   // q >= N: L2 = +inf -> p = 0
           dp[r] = p * (dp[r] - dl);
         }
         // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
