@@ -103,7 +103,9 @@ def main():
     img = torch.rand(B, cfg.in_chans, cfg.img_size, cfg.img_size, device=dev, generator=g)
     tgt = torch.randint(0, cfg.num_classes, (B,), device=dev, generator=g)
 
-    def step():
+    opt_events = []   # (start, end) around each timed optimizer step (reported separately)
+
+    def step(timed=False):
         arena.grad.zero_()
         red.start()
         logits = model(img)
@@ -111,7 +113,13 @@ def main():
         loss.backward()
         red.finish()
         if not args.no_optimizer:
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
             opt.step()
+            if timed:
+                e1.record()
+                opt_events.append((e0, e1))
         return loss
 
     for _ in range(args.warmup):
@@ -126,7 +134,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = step(timed=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -173,6 +181,8 @@ def main():
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                      "launches_timed": len(events), "avg_launch_ms": round(kern_ms, 4)},
+        "optimizer_ms": (round(sum(a.elapsed_time(b) for a, b in opt_events) / len(opt_events), 3)
+                         if opt_events else None),
         "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "loss": round(float(loss.item()), 5),
     }

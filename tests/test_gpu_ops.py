@@ -273,6 +273,34 @@ def test_attention_fwd_bwd(B, N, H, T, attn_path):
         assert rel(d[:, i], g[:, i]) < (2e-2 if T == BF else 1e-5), name
 
 
+@pytest.mark.parametrize("B,N,H", [(2, 197, 2), (1, 17, 3), (3, 1, 2), (1, 130, 1), (1, 256, 1),
+                                   (2, 255, 1), (1, 33, 2), (1, 96, 1), (4, 197, 12)])
+def test_attention_bwd_single_pass(B, N, H, monkeypatch):
+    """The single-pass backward (VITMI_ATTN_FUSED=1: S/P/dS formed once, dQ summed over the
+    key waves in a fixed order through LDS) vs the fp32 reference, vs the dQ + dK/dV kernel
+    pair, and bitwise equal across runs (deterministic: no atomics)."""
+    D = 64 * H
+    scale = 64 ** -0.5
+    qkv = rnd(B * N, 3 * D, dtype=BF, seed=31)
+    do = rnd(B * N, D, dtype=BF, seed=32)
+    o, lse = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
+    monkeypatch.setenv("VITMI_ATTN_FUSED", "0")
+    pair = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+    monkeypatch.setenv("VITMI_ATTN_FUSED", "1")
+    one = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+    again = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+    assert torch.equal(one, again)
+    qq = qkv.float().clone().requires_grad_()
+    o2, _ = attn_ref(qq, B, N, H, scale)
+    o2.backward(do.float())
+    g = qq.grad.view(B * N, 3, D)
+    d1 = one.float().cpu().view(B * N, 3, D)
+    d2 = pair.float().cpu().view(B * N, 3, D)
+    for i, name in enumerate("qkv"):
+        assert rel(d1[:, i], g[:, i]) < 2e-2, name
+        assert rel(d1[:, i], d2[:, i]) < 1e-2, name
+
+
 @pytest.mark.parametrize("B,N,H,T", [(2, 197, 2, BF), (3, 17, 1, BF), (1, 256, 3, BF), (2, 1, 2, BF),
                                      (2, 300, 1, BF), (2, 33, 2, torch.float32)])
 def test_attention_bwd_fused_bias(B, N, H, T, monkeypatch):

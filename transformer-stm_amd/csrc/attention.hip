@@ -857,6 +857,211 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
   (void)colsum;   // the k / v bias gradients come from the dQ kernel (see there)
 }
 
+// ---------------------------------------------- fused single-pass backward (N <= NPMAX)
+// One workgroup per (batch, head), NW = ceil(N/32) waves; wave w owns keys 32w..32w+31 exactly
+// as in attn_bwd_dkv_seq_bf16 (dK, dV accumulate in registers), and S, P, dP and dS of every
+// 32x32 block are formed ONCE (the two-kernel path forms them in both kernels: 28 MFMAs + two
+// exp passes per block, here 20 + one).  dQ needs a sum over keys, i.e. over waves:
+//   * the wave's dS block (accumulator: key on the lane) goes to a per-wave LDS scratch as
+//     dS^T[key][q] with 8-B writes, and comes back with ds_read_b64_tr_b16 as the B operand
+//     with q on the lane;
+//   * dQ^T[d][q] += K^T[d][key] dS^T[key][q], with the wave's K^T fragments in registers;
+//   * the partial goes into an fp32 dQ image in LDS by read-add-write.  At step t wave w works
+//     on query tile (w + t) mod NW and adds only after the tile's turn counter says step t-1's
+//     add is in, so every tile has one writer at a time and its sum order (w = tile, tile-1, ...)
+//     is fixed: deterministic, no atomics, no workgroup barrier inside the loop.
+// Delta = rowsum(dO * O) is formed in the prologue (each wave its own 32 query rows).
+// LDS (NPMAX = 256): Q | dO images 64 KiB + dQ fp32 [256][68] 68 KiB + L2 | delta 2 KiB +
+// scratch 8 x 2 KiB = 150 KiB: one workgroup per CU.
+__device__ __forceinline__ int scr_off(int key, int chunk) { return key * 64 + ((chunk ^ (key & 7)) << 3); }
+
+template <int NPMAX>
+__global__ __launch_bounds__(NPMAX * 2) void attn_bwd_fused_seq_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, bf16* __restrict__ dqkv, int N, int H, float scale) {
+  constexpr int DQP = 68;                                  // dQ image row pitch (floats)
+  constexpr int OFF_DQ = 2 * NPMAX * 128;
+  constexpr int OFF_ROW = OFF_DQ + NPMAX * DQP * 4;
+  constexpr int OFF_SCR = OFF_ROW + 2 * NPMAX * 4;
+  constexpr int OFF_TURN = OFF_SCR + (NPMAX / 32) * 2048;
+  __shared__ __attribute__((aligned(16))) char smem[OFF_TURN + (NPMAX / 32) * 4];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6, NP = nw * 32;
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  char* qt = smem;
+  char* dt_ = smem + NPMAX * 128;
+  float* dqs = (float*)(smem + OFF_DQ);
+  float* l2s = (float*)(smem + OFF_ROW);
+  float* dls = l2s + NPMAX;
+  char* scr = smem + OFF_SCR + wave * 2048;
+
+  // prologue: Q, dO images; the K image (128-B rows) parked in the dQ area for the K^T fragments
+  stage_seq(qt, rq, ldb, NP, nw, wave, lane);
+  stage_seq(dt_, rdo, ldo, NP, nw, wave, lane);
+  stage_seq(smem + OFF_DQ, rk, ldb, NP, nw, wave, lane);
+  const int r32 = wave * 32 + (lane & 31);   // this lane's key (dK/dV) and query (delta) row
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = load_row16(rk, (uint32_t)((int64_t)r32 * ldb + (16 * s + 8 * h) * 2));
+    vf[s] = load_row16(rv, (uint32_t)((int64_t)r32 * ldb + (16 * s + 8 * h) * 2));
+  }
+  float dl;
+  {
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t off = (uint32_t)((int64_t)r32 * ldo + (16 * s + 8 * h) * 2);
+      const bf16x8 dv = load_row16(rdo, off), ov = load_row16(ro, off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)ov[j] * (float)dv[j];
+    }
+    dl = part + __shfl_xor(part, 32, 64);
+  }
+  const bool rok = r32 < N;
+  const float l2v = rok ? lse[(int64_t)bh * N + r32] * LOG2E : INFINITY;   // q >= N -> P = 0
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (h == 0) {
+    l2s[r32] = l2v;
+    dls[r32] = rok ? dl : 0.f;
+  }
+  __syncthreads();
+  // K^T[d][key] fragments of this wave's keys (A operands of dQ^T = K^T dS^T)
+  bf16x8 ktf[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int d2 = 0; d2 < 2; ++d2) ktf[s][d2] = frag_tr(smem + OFF_DQ, wave * 32 + 16 * s, 32 * d2, lane);
+  __syncthreads();   // (the barrier's fence retires the reads before the area is zeroed)
+  for (int i = threadIdx.x; i < NP * DQP / 4; i += blockDim.x) ((f32x4*)dqs)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int* turn = (int*)(smem + OFF_TURN);   // turn[tile] = steps whose dQ add into the tile is done
+  if (threadIdx.x < nw) turn[threadIdx.x] = 0;
+  __syncthreads();
+
+  const float c2 = scale * LOG2E;
+  const int g16 = lane >> 4, tl = lane & 15, qq = tl >> 2, pp = tl & 3;
+  f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+#pragma unroll 1
+  for (int t = 0; t < nw; ++t) {
+    int qi = wave + t;
+    if (qi >= nw) qi -= nw;
+    const int q0 = qi * 32;
+    f32x16 sa = zero16(), dp = zero16();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
+      dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key]
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int q4 = q0 + 8 * g4 + 4 * h;
+      const f32x4 L2 = *(const f32x4*)(l2s + q4);
+      const f32x4 d4 = *(const f32x4*)(dls + q4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = fexp2(fmaf(sa[4 * g4 + i], c2, -L2[i]));
+        sa[4 * g4 + i] = p;
+        dp[4 * g4 + i] = p * (dp[4 * g4 + i] - d4[i]);
+      }
+    }
+    // dS^T[key][q] into the scratch: rows q = 8*g4 + 4h + 0..3 of this lane's key column
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)dp[4 * g4 + i];
+      *(bf16x4*)(scr + scr_off(lane & 31, 2 * g4 + h)) = v;
+    }
+    asm volatile("" ::: "memory");   // scratch writes stay ahead of the transposed reads
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
+#pragma unroll
+      for (int d2 = 0; d2 < 2; ++d2) {
+        dvt[d2] = mfma32(frag_tr(dt_, q0 + 16 * s, 32 * d2, lane), pb, dvt[d2]);
+        dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
+      }
+    }
+    // dQ^T[d][q] partial of this wave's 32 keys; B = dS^T with q on the lane (transposed read
+    // of the scratch: element j <-> key 16s + 8(j>>2) + 4h + (j&3), the frag_tr k order)
+    f32x16 dqp[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 sbt;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = 16 * s + 8 * i + 4 * (g16 >> 1) + qq;
+        s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scr + scr_off(row, 4 * (g16 & 1) + pp)));
+        bf16x4 bv = __builtin_bit_cast(bf16x4, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sbt[4 * i + j] = bv[j];
+      }
+#pragma unroll
+      for (int d2 = 0; d2 < 2; ++d2) dqp[d2] = mfma32(ktf[s][d2], sbt, dqp[d2]);
+    }
+    // this step's only writer of query tile qi: dQ[q][d] += partial (lane q, d = 32d2 + acc_row).
+    // Step t-1 of tile qi belonged to wave w+1; wait for its add (turn[qi] == t) instead of a
+    // workgroup barrier, so the waves drift apart and one wave's MFMAs overlap another's softmax.
+    // The waits form a chain (w waits on w+1 one step earlier), so they always resolve; the
+    // bound only guards against a logic error hanging the device.
+    {
+      volatile int* tp = turn + qi;
+      for (int spin = 0; *tp != t && spin < (1 << 22); ++spin) __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    float* dq_row = dqs + (q0 + (lane & 31)) * DQP;
+#pragma unroll
+    for (int d2 = 0; d2 < 2; ++d2)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        f32x4* pq = (f32x4*)(dq_row + 32 * d2 + 8 * g4 + 4 * h);
+        f32x4 a = *pq;
+        a[0] += dqp[d2][4 * g4];
+        a[1] += dqp[d2][4 * g4 + 1];
+        a[2] += dqp[d2][4 * g4 + 2];
+        a[3] += dqp[d2][4 * g4 + 3];
+        *pq = a;
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    *(volatile int*)(turn + qi) = t + 1;
+  }
+  __syncthreads();   // every tile's last add is in
+  // dK, dV of the wave's keys
+  if (rok) {
+    bf16* row = dqkv + ((int64_t)b * N + r32) * ld;
+#pragma unroll
+    for (int d2 = 0; d2 < 2; ++d2)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * d2 + 8 * g4 + 4 * h;
+        store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
+               dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
+        store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
+               dvt[d2][4 * g4 + 3]);
+      }
+    // dQ of query row r32 (all writers finished at the loop's last barrier): half h = d 32h..
+    bf16* qrow = row + hd * DH + 32 * h;
+    const float* src = dqs + r32 * DQP + 32 * h;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const f32x4 a = *(const f32x4*)(src + 4 * c);
+      store4(qrow + 4 * c, a[0] * scale, a[1] * scale, a[2] * scale, a[3] * scale);
+    }
+  }
+}
+
 // ============================================ persistent, pipelined whole-sequence kernels
 // The same math as the three kernels above, but ONE workgroup per CU walks (batch, head)
 // pairs p = blockIdx.x, +gridDim.x, ...  While pair p computes out of LDS buffer `cur`, the
@@ -1400,6 +1605,12 @@ static int pp_grid(int npairs) {
   return npairs < cus ? npairs : cus;
 }
 
+// single-pass fused backward for N <= SEQ_MAX (VITMI_ATTN_FUSED=0 selects the dQ + dK/dV pair)
+static bool fused_bwd() {
+  const char* e = getenv("VITMI_ATTN_FUSED");
+  return e ? atoi(e) != 0 : false;
+}
+
 static int attn_check(int dtype, int B, int N, int H, int dh) {
   VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "attention: bad dtype %d", dtype);
   VITMI_CHECK_ARG(dh == DH, "attention: head dim must be 64 (got %d)", dh);
@@ -1452,7 +1663,10 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
   if (dtype == VITMI_BF16 && seq_path(N)) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
     const dim3 block(64 * ((N + 31) / 32));
-    if (const int g = colsum ? 0 : pp_grid(B * H)) {
+    if (!colsum && fused_bwd()) {
+      hipLaunchKernelGGL(attn_bwd_fused_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
+                         (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, N, H, scale);
+    } else if (const int g = colsum ? 0 : pp_grid(B * H)) {
       hipLaunchKernelGGL(attn_bwd_dq_pp_bf16<SEQ_MAX>, dim3(g), block, 0, s, (const bf16*)qkv, (const bf16*)o,
                          (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, B * H);
       hipLaunchKernelGGL(attn_bwd_dkv_pp_bf16<SEQ_MAX>, dim3(g), block, 0, s, (const bf16*)qkv,
