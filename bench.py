@@ -3,22 +3,37 @@
 
 BASELINE.json metric: "images/sec fwd+bwd ViT-B/16 224px bs=256/GPU at 1/2/4/8 MI355X;
 % MFMA roofline".  One step = forward + CE loss + full backward (hand-written gfx950
-kernels) + RCCL gradient all-reduce (N>1) + Keras Adam update (one fused vitmi launch), on a synthetic
+kernels) + RCCL gradient all-reduce (N>1, the library's vitmi_comm_* leg on a side stream,
+overlapped with the backward) + Keras Adam update (one fused vitmi launch), on a synthetic
 batch of 256 images/GPU already resident in HBM, random-init ViT-B/16 weights.
 
 Launch:  python bench.py [--gpus 1 --steps 10 --warmup 3]
          python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
              --master-port P bench.py --gpus N ...
-Rank 0 prints ONE JSON line.  Extra fields: `roofline` (dominant kernel: the fc1 GEMM
-[M x 3072 x 768], timed live with HIP events on its stream inside the timed region) and
-`cpu_baseline` (the CPU oracle's fwd+bwd on the host cores, rank 0 at N=1 only).
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries, measured in this run:
+  roofline      the dominant kernel (fc1 GEMM [M x 3072 x 768] + bias + GELU) timed with HIP
+                events on its stream inside the timed region; `traffic` = its HBM bytes per
+                launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over the same
+                GEMM run as a child process;
+  per_kernel    a rocprofv3 --kernel-trace --stats child run of this bench (3 steps), joined
+                with the library's own per-kernel algorithmic work (vitmi_stats_*): ms/step,
+                TFLOP/s, GB/s and MFMA fraction per kernel;
+  cpu_baseline  the CPU oracle's fwd+bwd on the host cores (rank 0 at N=1 only), plus the
+                bf16 GPU logits' max-abs distance from the fp32 oracle on the same weights.
+The evidence legs run after the timed region (N=1, rank 0) and never change `value`.
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import signal
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -28,23 +43,39 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from vitmi import dp, ops, optim  # noqa: E402
+from vitmi import _lib, dp, ops, optim  # noqa: E402
 from vitmi.config import config_c3, config_c5  # noqa: E402
 from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
 METRIC = "images/sec fwd+bwd ViT-B/16 224px bs=256/GPU at 1/2/4/8 MI355X; % MFMA roofline"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level table)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_fc1_fwd.json")
+PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(cfg, batch: int, steps: int):
-    """The CPU oracle (oracle/vit_ref.py) timed on this host's cores: a bounded sample."""
+# ------------------------------------------------------------------ CPU baseline (oracle)
+def _lscpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, batch: int, steps: int, model=None, dev=None):
+    """The CPU oracle (oracle/vit_ref.py, fp32) timed on this host's cores: 1 warm-up step and
+    `steps` timed steps at `batch` images (BASELINE.md §2 protocol).  Threads: every core of the
+    affinity mask, capped by the pool's per-GPU CPU share (OMP_NUM_THREADS, set to 16 on the
+    GPU boxes, whose affinity mask spans the whole multi-tenant host)."""
     from oracle import vit_ref
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+        affinity = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", affinity) or affinity)
+    cores = max(1, min(affinity, share))
     torch.set_num_threads(cores)
     params = vit_ref.init_params(cfg, seed=0, randomize_all=False)
     img, tgt = vit_ref.synthetic_batch(cfg, batch)
@@ -53,11 +84,155 @@ def cpu_baseline(cfg, batch: int, steps: int):
     for _ in range(steps):
         vit_ref.forward_backward(img, tgt, params, cfg)
     dt_ = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt_, 3), "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": f"oracle/vit_ref.py fp32 fwd+bwd ViT-B/16 224px, bs={batch}, {steps} steps after 1 warm-up "
-                      f"({dt_:.1f} s), torch CPU threads={cores}"}
+    out = {"value": round(batch * steps / dt_, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+           "affinity_cores": affinity, "cpu_model": _lscpu_model(),
+           "sample": f"oracle/vit_ref.py fp32 fwd+bwd ViT-B/16 224px, bs={batch}, 1 warm-up + {steps} timed "
+                     f"steps ({dt_:.1f} s), torch CPU threads={cores} (affinity {affinity}, pool share "
+                     f"OMP_NUM_THREADS={share})"}
+    if model is not None:
+        # the same weights through the bf16 GPU path and the fp32 oracle: logits distance
+        with torch.no_grad():
+            p = {k: v.detach().float().cpu() for k, v in model.named_parameters()}
+            x, _ = vit_ref.synthetic_batch(cfg, 2, seed=99)
+            ref = vit_ref.forward(x, p, cfg)
+            got = model(x.to(dev)).float().cpu()
+        out["parity_bf16_logits_max_abs"] = float((got - ref).abs().max().item())
+        out["parity_sample"] = "2 images, the bench model's weights after the timed steps, fp32 CPU oracle"
+    return out
 
 
+# ------------------------------------------------------------------ evidence legs (child runs)
+def _run(cmd, timeout, cwd=ROOT, log=None):
+    """Run a child in its own process group; kill the group on timeout.  -> returncode or None."""
+    with open(log or os.devnull, "w") as f:
+        p = subprocess.Popen(cmd, cwd=cwd, stdout=f, stderr=subprocess.STDOUT, start_new_session=True,
+                             env=dict(os.environ, PYTHONUNBUFFERED="1"))
+        try:
+            return p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return None
+
+
+def _demangle(names):
+    """__cxa_demangle of mangled names (the demangler rocprofv3 applies to kernel names)."""
+    import ctypes
+    try:
+        cxx = ctypes.CDLL("libstdc++.so.6")
+        fn = cxx.__cxa_demangle
+        fn.restype = ctypes.c_void_p
+        free = ctypes.CDLL("libc.so.6").free
+    except OSError:
+        return {n: n for n in names}
+    out = {}
+    for n in names:
+        st = ctypes.c_int(0)
+        r = fn(n.encode(), None, None, ctypes.byref(st))
+        if r and st.value == 0:
+            out[n] = ctypes.string_at(r).decode()
+            free(ctypes.c_void_p(r))
+        else:
+            out[n] = n
+    return out
+
+
+def _short(name: str) -> str:
+    s = name[5:] if name.startswith("void ") else name
+    return s.split("(")[0]
+
+
+def per_kernel_evidence(args, tmp):
+    """rocprofv3 --kernel-trace --stats over a 3-step child run of this bench, joined per kernel
+    with the library's algorithmic work table of the same run."""
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return {"error": "rocprofv3 not found"}
+    steps = 3
+    stats_json = os.path.join(tmp, "stats.json")
+    cmd = [rp, "--kernel-trace", "--stats", "-d", os.path.join(tmp, "kt"), "-o", "run", "--output-format", "csv",
+           "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup", "2",
+           "--config", args.config, "--no-cpu-baseline", "--no-evidence", "--stats-out", stats_json]
+    if args.batch:
+        cmd += ["--batch", str(args.batch)]
+    rc = _run(cmd, 300, log=os.path.join(tmp, "kt.log"))
+    if rc != 0 or not os.path.exists(stats_json):
+        return {"error": f"rocprofv3 kernel-trace child failed (rc={rc})"}
+    work = json.load(open(stats_json))
+    lib_names = _demangle([w["name"] for w in work["kernels"]])
+    by_name = {}
+    for w in work["kernels"]:
+        for key in (w["name"], lib_names[w["name"]]):
+            by_name[_short(key)] = w
+    traces = glob.glob(os.path.join(tmp, "kt", "**", "run_kernel_trace.csv"), recursive=True)
+    if not traces:
+        return {"error": "no kernel trace"}
+    # the timed steps are the dispatches between the two marker kernels (torch.cuda._sleep ->
+    # spin_kernel) the child launches around its timed region
+    disp = sorted(csv.DictReader(open(traces[0])), key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(disp) if "spin_kernel" in r["Kernel_Name"]]
+    if len(marks) < 2:
+        return {"error": "timed-region markers not found in the kernel trace"}
+    agg = {}
+    for r in disp[marks[0] + 1:marks[-1]]:
+        k = _short(r["Kernel_Name"])
+        a = agg.setdefault(k, [0, 0.0])
+        a[0] += 1
+        a[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    tot = sum(a[1] for a in agg.values()) * 1e3 / steps
+    out = []
+    for k, (calls, sec) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        ms = sec * 1e3 / steps
+        if ms < 0.02:
+            continue
+        e = {"name": k[:120], "ms": round(ms, 3), "calls": round(calls / steps, 2),
+             "avg_us": round(sec / calls * 1e6, 1)}
+        w = by_name.get(k)
+        if w is not None and w["calls"] == calls:       # the same launches the work table counted
+            fl, by = w["flops"], w["bytes"]
+            e["tflops"] = round(fl / sec / 1e12, 1) if fl else None
+            e["mfma_util"] = round(fl / sec / 1e12 / PEAK_BF16_TFLOPS, 4) if fl else None
+            e["gbps"] = round(by / sec / 1e9, 1) if by else None
+        out.append(e)
+    return {"source": "rocprofv3 --kernel-trace of a child run of this bench (3 timed steps after 2 warm-up, "
+                      "bracketed by marker kernels); flops/bytes = the library's algorithmic work "
+                      "(vitmi_stats_*) of the same launches; mfma_util vs the 2.5 PF bf16 dense peak",
+            "kernel_ms_per_step": round(tot, 3), "kernels": out}
+
+
+def traffic_evidence(tmp, M):
+    """HBM bytes per launch of the fc1 GEMM (+bias+GELU) from two rocprofv3 --pmc passes, with the
+    gfx950 corrections of MI355X_MICROARCH.md §HBM (FETCH_SIZE KiB x2 for wide streaming reads;
+    WRITE_SIZE KiB exact for 16-B stores)."""
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(tmp, ctr)
+        cmd = [rp, "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.join(ROOT, "tools", "gemm_one.py"), "fc1_gelu", "5"]
+        rc = _run(cmd, 120, log=os.path.join(tmp, ctr + ".log"))
+        files = glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True)
+        if rc != 0 or not files:
+            return None, f"rocprofv3 --pmc {ctr} failed (rc={rc})"
+        per = {}
+        for r in csv.DictReader(open(files[0])):
+            name = r.get("Kernel_Name", "")
+            if "gemm256_kernel" not in name or r.get("Counter_Name") != ctr:
+                continue
+            per[r.get("Dispatch_Id")] = per.get(r.get("Dispatch_Id"), 0.0) + float(r["Counter_Value"])
+        v = list(per.values())
+        if not v:
+            return None, f"no gemm256 dispatch in the {ctr} pass"
+        v = v[1:] or v                                   # skip the cold first launch
+        vals[ctr] = sum(v) / len(v)
+    fetch = vals["FETCH_SIZE"] * 1024 * 2
+    write = vals["WRITE_SIZE"] * 1024
+    return {"fetch": fetch, "write": write, "total": fetch + write}, None
+
+
+# ------------------------------------------------------------------ the benchmark
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -68,15 +243,30 @@ def main():
                          "(BASELINE config 5, N = 577 tokens: a secondary line, not the headline)")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--comm", choices=["vitmi", "torch"], default="vitmi",
+                    help="vitmi: the library's RCCL communicator (vitmi_comm_*, side stream + hipEvent gating); "
+                         "torch: torch.distributed all_reduce (ProcessGroupNCCL)")
+    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="dtype of the gradient all-reduce (bf16 halves the bytes; vitmi comm only)")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="CUs the persistent GEMM leaves to RCCL while buckets are in flight (N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=16)
-    ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--no-evidence", action="store_true", help="skip the rocprofv3 per-kernel / traffic legs")
+    ap.add_argument("--cpu-batch", type=int, default=32)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-optimizer", action="store_true", help="diagnostic only: skip Adam")
     ap.add_argument("--optimizer", choices=["vitmi", "torch"], default="vitmi",
                     help="vitmi: Keras Adam, one fused launch over the arena (+ bf16 shadow); torch: fused torch Adam")
+    ap.add_argument("--stats-out", default=None, help=argparse.SUPPRESS)   # evidence child: work table
     args = ap.parse_args()
 
-    rank, world, local = dp.init_from_env("nccl")
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    # with the vitmi communicator the process group only bootstraps (rendezvous, TCPStore,
+    # barriers, the max-over-ranks time): gloo, so the job holds ONE RCCL communicator
+    backend = "gloo" if args.comm == "vitmi" else "nccl"
+    if world_env > 1:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    rank, world, local = dp.init_from_env(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = config_c3() if args.config == "c3" else config_c5()
@@ -88,8 +278,10 @@ def main():
     torch.manual_seed(0)
     model = VisionTransformer(cfg).to(dev)
     model.reset_parameters(seed=0)
-    red = dp.attach(model, bucket_mb=args.bucket_mb)
-    dp.broadcast_parameters(model)
+    comm = dp.VitmiComm.from_store(rank, world) if (world > 1 and args.comm == "vitmi") else None
+    red = dp.attach(model, bucket_mb=args.bucket_mb, comm=comm, grad_dtype=args.grad_dtype,
+                    reserve_cus=args.reserve_cus if world > 1 else 0)
+    dp.broadcast_parameters(model, comm=comm)
     if args.optimizer == "vitmi":
         opt = optim.Adam(model, learning_rate=1e-3)     # keras.optimizers.Adam(1e-3), models/CvT(Par).py:458
     else:
@@ -129,6 +321,9 @@ def main():
         dist.barrier()
     M, F_, D = B * cfg.seq_len, cfg.mlp_dim, cfg.embed_dim
     events = ops.set_probe((M, F_, D))        # fc1 forward GEMM launches
+    if args.stats_out:
+        _lib.lib().vitmi_stats_enable(1)
+        torch.cuda._sleep(1000)               # marker kernel: the timed region starts
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -139,8 +334,14 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.stats_out:
+        torch.cuda._sleep(1000)               # marker kernel: the timed region ended
     ops.set_probe(None)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if args.stats_out:
+        _dump_stats(args.stats_out)
+    if comm is not None:
+        comm.check()
+    t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
@@ -150,14 +351,6 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in events) / max(1, len(events))
     kflop = 2.0 * M * F_ * D
     achieved = kflop / (kern_ms * 1e-3) / 1e12
-    traffic = None
-    if os.path.exists(TRAFFIC_FILE):
-        try:
-            tr = json.load(open(TRAFFIC_FILE))
-            if tr.get("M") == M:
-                traffic = tr.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
     step_flops = cfg.flops_per_image_fwd_bwd() * B * world
     out = {
         "metric": metric,
@@ -173,26 +366,66 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (torch.rand images in [0,1), randint labels; random-init trunc_normal(.02) weights)",
         "config": {"workload": f"{'ViT-B/16 224' if args.config == 'c3' else 'ViT-L/16 384'}x"
-                               f"{cfg.img_size}x3 fwd + CE loss + bwd + RCCL grad all-reduce + Adam step",
+                               f"{cfg.img_size}x3 fwd + CE loss + bwd"
+                               + (f" + {args.grad_dtype} grad all-reduce ({args.comm} RCCL, "
+                                  f"{args.bucket_mb:g} MiB buckets)" if world > 1 else "")
+                               + " + Adam step",
                    "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
                    "model": model_name, "global_batch": B * world, "seq_len": cfg.seq_len,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd bf16 [{M}x{F_}x{D}] +bias+GELU",
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                     "launches_timed": len(events), "avg_launch_ms": round(kern_ms, 4)},
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "launches_timed": len(events), "avg_launch_ms": round(kern_ms, 4),
+                     "algorithmic_bytes": 2 * (M * D + F_ * D) + 2 * 2 * M * F_},
         "optimizer_ms": (round(sum(a.elapsed_time(b) for a, b in opt_events) / len(opt_events), 3)
                          if opt_events else None),
         "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
         "loss": round(float(loss.item()), 5),
+        "build_id": _lib.lib().vitmi_build_id().decode(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
-        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps, model, dev)
+    if rank == 0 and world == 1 and not args.no_evidence and args.config == "c3" and not args.stats_out:
+        del model, opt, arena, red
+        torch.cuda.empty_cache()
+        tmp = tempfile.mkdtemp(prefix="vitmi_bench_")
+        tr, err = traffic_evidence(tmp, M)
+        if tr is not None:
+            out["roofline"]["traffic"] = round(tr["total"])
+            out["roofline"]["traffic_detail"] = {
+                "fetch_bytes": round(tr["fetch"]), "write_bytes": round(tr["write"]),
+                "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/gemm_one.py fc1_gelu "
+                          "(this run); FETCH_SIZE KiB x2 (gfx950 wide-read half count), WRITE_SIZE KiB"}
+        else:
+            out["roofline"]["traffic_error"] = err
+        out["per_kernel"] = per_kernel_evidence(args, tmp)
+        keep = os.path.join(ROOT, "gpurun_out")
+        if os.path.isdir(keep):
+            shutil.copytree(tmp, os.path.join(keep, "bench_evidence"), dirs_exist_ok=True)
+        shutil.rmtree(tmp, ignore_errors=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.destroy()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _dump_stats(path):
+    lib = _lib.lib()
+    import ctypes
+    n = lib.vitmi_stats_count()
+    ks = []
+    for i in range(n):
+        name = ctypes.create_string_buffer(1024)
+        calls, fl, by = ctypes.c_int64(0), ctypes.c_double(0), ctypes.c_double(0)
+        lib.vitmi_stats_get(i, name, 1024, ctypes.byref(calls), ctypes.byref(fl), ctypes.byref(by))
+        ks.append({"name": name.value.decode(), "calls": calls.value, "flops": fl.value, "bytes": by.value})
+    lib.vitmi_stats_enable(0)
+    with open(path, "w") as f:
+        json.dump({"kernels": ks}, f)
 
 
 if __name__ == "__main__":

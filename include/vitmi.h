@@ -30,7 +30,7 @@ extern "C" {
 
 typedef void* vitmi_stream_t; /* hipStream_t */
 
-enum { VITMI_OK = 0, VITMI_ERR_INVALID = 1, VITMI_ERR_HIP = 2, VITMI_ERR_UNSUPPORTED = 3 };
+enum { VITMI_OK = 0, VITMI_ERR_INVALID = 1, VITMI_ERR_HIP = 2, VITMI_ERR_UNSUPPORTED = 3, VITMI_ERR_COMM = 4 };
 enum { VITMI_F32 = 0, VITMI_BF16 = 1 };
 
 /* GEMM epilogues (all apply `bias` (fp32, may be NULL) first where it applies) */
@@ -45,9 +45,19 @@ enum {
 enum { VITMI_LOSS_CE = 0, VITMI_LOSS_MSE = 1 };
 
 int vitmi_version(void);
+/* content hash of the sources the library was built from (csrc/ + this header), as 16 hex
+ * digits; __graft_entry__ compares it with the tree it runs in, so a stale .so is caught */
+const char* vitmi_build_id(void);
 const char* vitmi_last_error(void);
 /* number of hipDevice compute units seen by the library (0 on error) */
 int vitmi_device_cus(void);
+/* Per-kernel algorithmic work accounting (host side, off by default): while enabled every
+ * launch adds its 2 x MAC flops and minimum HBM bytes to its kernel's entry (keyed by the
+ * mangled device symbol).  Enabling clears the table.  bench.py joins these with a rocprofv3
+ * kernel trace of the same run (per-kernel TFLOP/s, GB/s). */
+int vitmi_stats_enable(int on);
+int vitmi_stats_count(void);
+int vitmi_stats_get(int i, char* name, int name_len, int64_t* calls, double* flops, double* bytes);
 
 /* ---------------------------------------------------------------------------
  * Generic MFMA GEMM:  C[M,N] (op)= sum_k A(m,k) * B(k,n)
@@ -137,6 +147,10 @@ int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, con
                         const void* o, const void* dout, const float* lse, void* dqkv,
                         void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_attention_bwd_workspace_size(int B, int N, int H);
+/* Kernel selection (process-wide; tests / A-B timing): 0 = auto, 1 = always the streamed
+ * (64-key LDS-tiled) kernels, 2 = auto with the single-pass fused backward for N <= 256.
+ * Returns the previous policy. */
+int vitmi_attention_set_policy(int policy);
 /* vitmi_attention_bwd plus the qkv bias gradient: dbias[3*H*dh] += column sums of dqkv (the
  * q/k/v Dense biases, models/CvT(Par).py:132-134).  On the whole-sequence bf16 path (N <= 256)
  * the sums come from the dQ and dK/dV kernels' registers (per (batch, head) block, then a
@@ -218,8 +232,9 @@ int vitmi_conv_col2im(int dtype, int B, int H, int W, int C, int kh, int kw, int
                       int Ho, int Wo, const void* dpatches, int Kp, float* dx, int64_t ldx, int64_t img_stride,
                       int64_t row_off, int accumulate, vitmi_stream_t stream);
 /* Projection(method='dw_bn') (:83-112): z = DepthwiseConv2D(3, 'same', no bias)(x) [3][3][C],
- * y = BatchNormalization: training != 0 -> batch statistics over B*H*W (biased variance) and the
- * moving statistics m <- momentum m + (1-momentum) stat (NULL to skip); training == 0 -> the
+ * y = BatchNormalization: training != 0 -> batch statistics over n = B*H*W (biased variance) and the
+ * moving statistics m <- momentum m + (1-momentum) stat (NULL to skip; the moving variance takes
+ * the unbiased n/(n-1) estimate, as Keras' fused BN and torch's BatchNorm2d do); training == 0 -> the
  * moving statistics normalise (Keras inference).  x/dx rows as above (cls row skipped via
  * x_off), y rows b*y_img + y_off + hw of y [..][ldy] (y_dtype).  z [B*H*W][C], mean/rstd [C]
  * are saved for the backward.  C % 4 == 0 and 1024 % C == 0. */
@@ -291,6 +306,38 @@ int vitmi_gather_rows(int64_t n, int64_t row_bytes, const void* src, int64_t n_s
 
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
+/* bf16 -> fp32 cast of n elements (the bf16 gradient all-reduce writes back into the fp32 arena) */
+int vitmi_cast_bf16_f32(int64_t n, const void* src, float* dst, vitmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Data-parallel gradient exchange over RCCL (xGMI within a node).  Replaces the cross-replica
+ * gradient reduction of tf.distribute.MirroredStrategy (old_codes/BayConvT(Par)(Muti).py:16-19,
+ * the reference's only parallel construct; TF runs it as an NCCL all-reduce on one host).
+ * One process per GPU, one communicator per process (bound to the HIP device current at
+ * vitmi_comm_init).  Rank 0 creates the 128-byte id; the caller distributes it (vitmi/dp.py
+ * uses torch.distributed's TCPStore).  RCCL is bound at run time (the copy already loaded by
+ * the process, else librccl.so); errors return VITMI_ERR_COMM.
+ */
+#define VITMI_COMM_UID_BYTES 128
+enum { VITMI_REDUCE_SUM = 0, VITMI_REDUCE_AVG = 1 };
+int vitmi_comm_get_unique_id(char* uid /* [VITMI_COMM_UID_BYTES] */);
+int vitmi_comm_init(int rank, int world, const char* uid /* [VITMI_COMM_UID_BYTES] */);
+int vitmi_comm_info(int* rank, int* world);
+/* In-place all-reduce of `count` elements (VITMI_F32 | VITMI_BF16) on the side stream `side`,
+ * after `ready_event` (a hipEvent_t recorded on the compute stream, may be NULL).  Returns once
+ * enqueued; the caller orders its consumers after `side` (record an event / stream wait). */
+int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, int op, vitmi_stream_t side, void* ready_event);
+/* in-place broadcast from `root` (parameter replication at start-up) */
+int vitmi_comm_broadcast(void* ptr, int64_t count, int dtype, int root, vitmi_stream_t stream);
+/* VITMI_ERR_COMM if the communicator reported an asynchronous error */
+int vitmi_comm_check(void);
+/* abort != 0: ncclCommAbort (tear down after a peer failure without waiting) */
+int vitmi_comm_destroy(int abort);
+
+/* Compute units the persistent GEMM leaves free (default 0): with data-parallel gradient
+ * all-reduces in flight, RCCL's kernels need CUs while a one-block-per-CU GEMM would hold all
+ * of them for its whole duration.  Returns the previous value. */
+int vitmi_gemm_set_reserved_cus(int n);
 
 #ifdef __cplusplus
 }

@@ -55,3 +55,30 @@ def test_workspace_queries_are_pure_host():
 def test_argtypes_declared(name):
     fn = getattr(_lib.lib(), name)
     assert fn.argtypes is not None and len(fn.argtypes) > 5
+
+
+def test_build_id_matches_sources():
+    """the .so was built from the csrc/ + include/ in this tree (a stale library is caught)"""
+    want = _lib.source_build_id()
+    assert want is not None
+    assert _lib.lib().vitmi_build_id().decode() == want
+
+
+def test_comm_entry_points_validate_without_a_communicator():
+    lib = _lib.lib()
+    assert lib.vitmi_comm_destroy(0) == 0                      # nothing to destroy
+    assert lib.vitmi_comm_check() == 0
+    rc = lib.vitmi_comm_allreduce_async(16, 4, 0, 1, None, None)
+    assert rc == 1 and b"vitmi_comm_init first" in lib.vitmi_last_error()
+    rc = lib.vitmi_comm_init(2, 2, b"\0" * 128)                # rank out of range: host check
+    assert rc == 1 and b"rank" in lib.vitmi_last_error()
+    assert lib.vitmi_comm_get_unique_id(None) == 1
+
+
+def test_policy_knobs_round_trip():
+    lib = _lib.lib()
+    prev = lib.vitmi_attention_set_policy(1)
+    assert lib.vitmi_attention_set_policy(prev) == 1
+    assert lib.vitmi_attention_set_policy(7) == 1              # out of range: rejected
+    prev = lib.vitmi_gemm_set_reserved_cus(8)
+    assert lib.vitmi_gemm_set_reserved_cus(prev) == 8

@@ -59,6 +59,8 @@ def _worker(rank, world, port, q):
         out["arena_order"] = [b for _, b in r2.launch_log]
         dp.broadcast_parameters(m)
         out["param0"] = arena.flat[:8].clone().numpy()
+        # 3) the RCCL id of the vitmi communicator travels through the job's TCPStore
+        out["uid"] = dp.exchange_unique_id(rank, world)
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -87,3 +89,4 @@ def test_grad_reducer_gloo_world2():
         assert torch.allclose(o["arena_mean"], torch.full_like(o["arena_mean"], 1.5))
         assert o["arena_order"] == sorted(o["arena_order"])    # front-to-back readiness
         assert (res[r]["param0"] == res[0]["param0"]).all()     # broadcast from rank 0
+        assert len(res[r]["uid"]) == dp.UID_BYTES and res[r]["uid"] == res[0]["uid"]

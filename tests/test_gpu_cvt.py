@@ -105,7 +105,7 @@ def test_dwconv_bn_fwd_bwd(B, H, C, cls):
     # moving statistics (Keras convention, biased batch variance)
     zr = F.conv2d(xs.detach().permute(0, 3, 1, 2), w, None, padding=1, groups=C)
     assert rel(rm, 0.01 * zr.mean(dim=(0, 2, 3))) < 1e-5
-    assert rel(rv, 0.99 + 0.01 * zr.var(dim=(0, 2, 3), unbiased=False)) < 1e-5
+    assert rel(rv, 0.99 + 0.01 * zr.var(dim=(0, 2, 3), unbiased=True)) < 1e-5
     # backward
     dyd = torch.zeros(B, N, C, device=DEV)
     dyd[:, off:] = dy.view(B, H * H, C).to(DEV)

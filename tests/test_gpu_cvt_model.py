@@ -146,7 +146,7 @@ def test_cvt_moving_stats_and_eval_mode():
                      params["stage0.blocks.0.norm1.bias"], ocfg.ln_eps).permute(0, 3, 1, 2)
     zq = F.conv2d(t, params["stage0.blocks.0.attn.conv_proj_q.weight"], None, padding=1, groups=D)
     assert rel(rm, 0.01 * zq.mean(dim=(0, 2, 3))) < 1e-4
-    assert rel(rv, 0.99 + 0.01 * zq.var(dim=(0, 2, 3), unbiased=False)) < 1e-4
+    assert rel(rv, 0.99 + 0.01 * zq.var(dim=(0, 2, 3), unbiased=True)) < 1e-4
     model.eval()
     with torch.no_grad():
         l1 = model(img.to(DEV))

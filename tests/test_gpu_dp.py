@@ -93,3 +93,132 @@ def test_dp_two_ranks_match_full_batch_oracle():
             assert vit_ref.rel_err(torch.from_numpy(o["grads"][k]), ref) <= 1e-4, (r, k)
     for k in g_ref:
         assert (res[0]["grads"][k] == res[1]["grads"][k]).all(), k
+
+
+# ------------------------------------------------------------------ the vitmi_comm_* RCCL leg
+def _comm_1rank():
+    from vitmi import dp
+    return dp.VitmiComm.from_store(0, 1)
+
+
+def test_rccl_one_rank_comm_side_stream_and_event_gating():
+    """A 1-rank RCCL communicator through the C ABI (vitmi_comm_init / allreduce_async /
+    broadcast / destroy): the all-reduce runs on the side stream only after the hipEvent
+    recorded behind a long compute-stream kernel, and the compute stream's consumer runs after
+    the side stream.  sum and mean over one rank are the identity, in fp32 and bf16."""
+    from vitmi import dp
+    comm = _comm_1rank()
+    try:
+        side = torch.cuda.Stream()
+        for dt in (torch.float32, torch.bfloat16):
+            x = torch.zeros(1 << 22, device="cuda", dtype=dt)
+            big = torch.randn(4096, 4096, device="cuda")
+            # a slow producer on the compute stream, then the value the all-reduce must see
+            for _ in range(4):
+                big = big @ big * 1e-3
+            x.fill_(3.0)
+            ready = torch.cuda.Event()
+            ready.record()
+            comm.allreduce_async(x, side, ready, dp.REDUCE_SUM)
+            torch.cuda.current_stream().wait_stream(side)
+            y = x * 2                                       # consumer on the compute stream
+            torch.cuda.synchronize()
+            assert torch.all(y == 6.0), dt
+            comm.allreduce_async(x, side, None, dp.REDUCE_AVG)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            assert torch.all(x == 3.0), dt
+        b = torch.arange(1000, device="cuda", dtype=torch.float32)
+        comm.broadcast(b, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(b, torch.arange(1000, device="cuda", dtype=torch.float32))
+        comm.check()
+    finally:
+        comm.destroy()
+
+
+@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
+def test_rccl_reducer_one_rank_matches_no_reducer(grad_dtype):
+    """GradReducer on the vitmi RCCL communicator (world 1): buckets launched from the fused
+    block backward's hooks on the side stream; the averaged gradients equal the plain ones
+    (bit for bit in fp32, bf16-rounded with grad_dtype='bf16'), and the CU reservation used
+    during the backward is restored afterwards."""
+    from oracle import vit_ref
+    from vitmi import _lib, dp
+    from vitmi.modules import VisionTransformer, cross_entropy
+    cfg = _cfg()
+    params = vit_ref.init_params(cfg, seed=3)
+    img, tgt = vit_ref.synthetic_batch(cfg, 8, seed=11)
+    ref = VisionTransformer(cfg).cuda()
+    ref.load_param_dict(params)
+    cross_entropy(ref(img.cuda()), tgt.cuda()).backward()
+    want = ref.arena().grad.clone()
+    comm = _comm_1rank()
+    try:
+        model = VisionTransformer(cfg).cuda()
+        model.load_param_dict(params)
+        red = dp.attach(model, bucket_mb=0.25, comm=comm, grad_dtype=grad_dtype, reserve_cus=16)
+        dp.broadcast_parameters(model, comm=comm)
+        for _ in range(2):                                  # the second step reuses every buffer
+            model.arena().grad.zero_()
+            red.start()
+            cross_entropy(model(img.cuda()), tgt.cuda()).backward()
+            early = sum(1 for r, _ in red.launch_log if r < model.arena().numel)
+            red.finish()
+            got = model.arena().grad.clone()
+            torch.cuda.synchronize()
+            assert len(red.bounds) > 2 and early >= 1
+            if grad_dtype == "fp32":
+                assert torch.equal(got, want)
+            else:
+                assert torch.equal(got, want.to(torch.bfloat16).float())
+        assert _lib.lib().vitmi_gemm_set_reserved_cus(0) == 0   # restored by finish()
+    finally:
+        comm.destroy()
+
+
+def _rccl_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vitmi import dp
+        try:
+            comm = dp.VitmiComm.from_store(rank, world)
+        except RuntimeError as e:                      # e.g. RCCL refuses two ranks on one GPU
+            q.put((rank, dict(skip=str(e))))
+            return
+        try:
+            side = torch.cuda.Stream()
+            x = torch.full((1 << 20,), float(rank + 1), device="cuda")
+            comm.allreduce_async(x, side, None, dp.REDUCE_AVG)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            q.put((rank, dict(val=float(x[0].item()), same=bool(torch.all(x == x[0]).item()))))
+        finally:
+            comm.destroy()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_rccl_two_ranks_on_one_gpu_or_skip():
+    """Two RCCL ranks sharing the test box's one GPU (real ncclAllReduce between processes),
+    if RCCL admits that topology; skipped with RCCL's own message otherwise."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rccl_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=120) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    skips = [o["skip"] for o in res.values() if "skip" in o]
+    if skips:
+        pytest.skip("RCCL: " + skips[0][:200])
+    for r in range(world):
+        assert res[r]["same"] and res[r]["val"] == 1.5

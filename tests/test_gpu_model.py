@@ -18,6 +18,12 @@ from vitmi.modules import VisionTransformer, cross_entropy, mse_loss  # noqa: E4
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
+# bf16 logits bounds: about 2x the max-abs error measured on MI355X ("Oracle and
+# parity"), so a numerics regression of a few x fails instead of hiding under a loose bound
+BF16_VITB_LOGITS = 7e-3      # measured 2.7e-3 (bs 2, default init) / 3.6e-3 (randomised, fwd+bwd)
+BF16_C1_LOGITS = 5e-3        # measured 2.2e-3
+BF16_VITL_LOGITS = 1e-2      # measured 4.9e-3 (ViT-L/16@384, depth 4)
+
 
 def gpu_step(cfg, params, img, tgt):
     model = VisionTransformer(cfg).cuda()
@@ -51,7 +57,8 @@ def test_c1_bf16_matches_oracle():
     cfg = config_c1(dtype="bf16")
     params = vit_ref.init_params(cfg, seed=0)
     img, tgt = vit_ref.synthetic_batch(cfg, 8)
-    compare(cfg, params, img, tgt, logit_tol=5e-2, grad_tol=2e-2, loss_tol=2e-2)
+    err, worst = compare(cfg, params, img, tgt, logit_tol=BF16_C1_LOGITS, grad_tol=2e-2, loss_tol=2e-2)
+    print(f"C1 bf16: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
 
 
 @pytest.mark.parametrize("variant", [dict(tie_norms=True), dict(qkv_bias=False, attn_scale="dim"),
@@ -102,7 +109,31 @@ def test_vit_b_bf16_logits_vs_oracle():
         out = model(img.cuda()).cpu()
     err = (out - ref).abs().max().item()
     print(f"ViT-B/16 bf16 logits max-abs vs fp32 oracle: {err:.3e}")
-    assert err < 2e-2
+    assert err < BF16_VITB_LOGITS
+
+
+def test_vit_b_bf16_full_depth_fwd_bwd_vs_oracle():
+    """BASELINE config 3 architecture at full depth (ViT-B/16 224^2: D = 768, H = 12, N = 197,
+    12 blocks) in bf16 at bs=2, forward AND backward against the fp32 CPU oracle on the same
+    weights (randomised gamma/beta/biases so every backward term is exercised): logits, loss
+    and every parameter gradient, ||d|| / ||g|| <= 2e-2 (SURVEY §8d bf16 bound)."""
+    cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype="bf16")
+    params = vit_ref.init_params(cfg, seed=0)
+    img, tgt = vit_ref.synthetic_batch(cfg, 2)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    err, worst = compare(cfg, params, img, tgt, logit_tol=BF16_VITB_LOGITS, grad_tol=2e-2, loss_tol=2e-2)
+    print(f"ViT-B/16 bf16 depth 12 bs 2: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
+
+
+def test_c2_fp32_fwd_bwd_vs_oracle():
+    """BASELINE config 2 architecture (ViT-S/16 224^2, fp32) forward AND backward at bs=4 vs the
+    CPU oracle: logits <= 1e-3 (north star), loss rel <= 1e-5, every grad rel <= 1e-3."""
+    cfg = config_c2()
+    params = vit_ref.init_params(cfg, seed=1)
+    img, tgt = vit_ref.synthetic_batch(cfg, 4, seed=3)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    err, worst = compare(cfg, params, img, tgt, logit_tol=1e-3, grad_tol=1e-3, loss_tol=1e-5)
+    print(f"ViT-S/16 fp32 bs 4: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
 
 
 def test_c2_fp32_logits_vs_oracle():
@@ -140,7 +171,7 @@ def test_c5_vit_l_bf16_vs_oracle():
     params = vit_ref.init_params(cfg, seed=0)
     img, tgt = vit_ref.synthetic_batch(cfg, 2)
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    err, worst = compare(cfg, params, img, tgt, logit_tol=5e-2, grad_tol=2e-2, loss_tol=2e-2)
+    err, worst = compare(cfg, params, img, tgt, logit_tol=BF16_VITL_LOGITS, grad_tol=2e-2, loss_tol=2e-2)
     print(f"ViT-L/16@384 depth 4 bf16: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
 
 
@@ -227,6 +258,7 @@ def test_dropout_training_matches_oracle(dtype, ltol, gtol):
     l_nodrop, _, _ = vit_ref.forward_backward(img, tgt, params, cfg)
     assert (l_ref - l_nodrop).abs().max().item() > 1e-3      # the masks do act
     l, loss, g = _drop_step(cfg, params, img, tgt, 4242)
+    print(f"dropout {dtype}: logits max-abs {(l - l_ref).abs().max().item():.3e}")
     assert (l - l_ref).abs().max().item() <= ltol
     worst = max((vit_ref.rel_err(g[k], g_ref[k]), k) for k in g_ref)
     assert worst[0] <= gtol, f"grad {worst[1]} rel {worst[0]:.3e}"
@@ -264,3 +296,21 @@ def test_dropout_vit_shape_rate_and_scale():
     gm = ops.dropout_apply(gsrc, 7, 1, 0.1, torch.float32)
     assert torch.equal(gm[~keep_t], torch.zeros_like(gm[~keep_t]))
     assert torch.allclose(gm[keep_t], gsrc[keep_t] / 0.9, rtol=1e-6, atol=0)
+
+
+# ------------------------------------------------------------------ determinism
+@pytest.mark.parametrize("dtype,batch", [("bf16", 64), ("fp32", 4)])
+def test_fwd_bwd_is_bitwise_deterministic(dtype, batch):
+    """The HIP race check of SURVEY §5: the same step run twice gives bitwise-identical logits,
+    loss and gradients.  No kernel of the path uses atomics; split-K, tail-split and column-sum
+    partials are folded in a fixed order, and LDS tiles are barrier-ordered.  ViT-B/16 width at
+    depth 2 and bs 64 puts every GEMM on the persistent kernel with its split-K / tail-split
+    units (M = 12,608 rows)."""
+    cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype=dtype, depth=2)
+    params = vit_ref.init_params(cfg, seed=5)
+    img, tgt = vit_ref.synthetic_batch(cfg, batch, seed=6)
+    runs = [gpu_step(cfg, params, img, tgt) for _ in range(2)]
+    (l0, s0, g0), (l1, s1, g1) = runs
+    assert torch.equal(l0, l1) and torch.equal(s0, s1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k

@@ -241,12 +241,12 @@ ATT = [(2, 197, 2), (1, 17, 3), (2, 64, 1), (1, 577, 2), (3, 1, 2), (1, 130, 1),
 
 
 @pytest.fixture(params=["seq", "stream"])
-def attn_path(request, monkeypatch):
-    """bf16 N <= 256 runs the whole-sequence kernels; VITMI_ATTN_STREAM=1 forces the streamed
-    ones (read by the library on every call), so both are checked at the same sizes."""
-    if request.param == "stream":
-        monkeypatch.setenv("VITMI_ATTN_STREAM", "1")
-    return request.param
+def attn_path(request):
+    """bf16 N <= 256 runs the whole-sequence kernels; attention policy 1 forces the streamed
+    ones, so both are checked at the same sizes."""
+    prev = ops.attention_set_policy(1 if request.param == "stream" else 0)
+    yield request.param
+    ops.attention_set_policy(prev)
 
 
 @pytest.mark.parametrize("B,N,H", ATT)
@@ -275,8 +275,8 @@ def test_attention_fwd_bwd(B, N, H, T, attn_path):
 
 @pytest.mark.parametrize("B,N,H", [(2, 197, 2), (1, 17, 3), (3, 1, 2), (1, 130, 1), (1, 256, 1),
                                    (2, 255, 1), (1, 33, 2), (1, 96, 1), (4, 197, 12)])
-def test_attention_bwd_single_pass(B, N, H, monkeypatch):
-    """The single-pass backward (VITMI_ATTN_FUSED=1: S/P/dS formed once, dQ summed over the
+def test_attention_bwd_single_pass(B, N, H):
+    """The single-pass backward (attention policy 2: S/P/dS formed once, dQ summed over the
     key waves in a fixed order through LDS) vs the fp32 reference, vs the dQ + dK/dV kernel
     pair, and bitwise equal across runs (deterministic: no atomics)."""
     D = 64 * H
@@ -284,11 +284,14 @@ def test_attention_bwd_single_pass(B, N, H, monkeypatch):
     qkv = rnd(B * N, 3 * D, dtype=BF, seed=31)
     do = rnd(B * N, D, dtype=BF, seed=32)
     o, lse = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
-    monkeypatch.setenv("VITMI_ATTN_FUSED", "0")
+    prev = ops.attention_set_policy(0)
     pair = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-    monkeypatch.setenv("VITMI_ATTN_FUSED", "1")
-    one = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-    again = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+    ops.attention_set_policy(2)
+    try:
+        one = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+        again = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+    finally:
+        ops.attention_set_policy(prev)
     assert torch.equal(one, again)
     qq = qkv.float().clone().requires_grad_()
     o2, _ = attn_ref(qq, B, N, H, scale)
@@ -303,10 +306,9 @@ def test_attention_bwd_single_pass(B, N, H, monkeypatch):
 
 @pytest.mark.parametrize("B,N,H,T", [(2, 197, 2, BF), (3, 17, 1, BF), (1, 256, 3, BF), (2, 1, 2, BF),
                                      (2, 300, 1, BF), (2, 33, 2, torch.float32)])
-def test_attention_bwd_fused_bias(B, N, H, T, monkeypatch):
+def test_attention_bwd_fused_bias(B, N, H, T):
     """the q/k/v bias gradient out of the attention backward kernels (q: dQ column sums;
     k: 0, v: column sums of dO by the softmax identities) == a column-sum pass over dqkv"""
-    monkeypatch.setattr(ops, "_FUSED_QKV_BIAS", True)
     D = 64 * H
     qkv = rnd(B * N, 3 * D, dtype=T, seed=25).to(DEV)
     o, lse = ops.attention_fwd(qkv, B, N, H, 0.125)
@@ -315,7 +317,7 @@ def test_attention_bwd_fused_bias(B, N, H, T, monkeypatch):
     db_ref = torch.full((3 * D,), 0.25, device=DEV)
     ops.bias_grad(ref, db_ref)
     db = torch.full((3 * D,), 0.25, device=DEV)
-    dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, H, 0.125, bias_grad=db)
+    dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, H, 0.125, bias_grad=db, fused_bias=True)
     assert torch.equal(dqkv, ref)
     # fused sums add fp32 values before dqkv's bf16 rounding
     assert rel(db, db_ref) < (3e-3 if T == BF else 1e-5)

@@ -75,3 +75,27 @@ def test_adam_arena_single_launch_and_bf16_shadow():
         model.head.weight.add_(1.0)
     arena.refresh_lp()
     assert torch.equal(arena.flat_lp, arena.flat.to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+def test_adam_per_tensor_on_arena_params_refreshes_bf16_shadow():
+    """Adam built from a parameter LIST of an arena-backed bf16 ViT (the per-tensor
+    path, raw-pointer writes) must still invalidate the arena's bf16 operand shadow, so the
+    next forward's GEMMs read the updated weights."""
+    from vitmi.config import ViTConfig
+    from vitmi.modules import VisionTransformer, cross_entropy
+    cfg = ViTConfig(img_size=32, patch_size=8, in_chans=3, num_classes=2, embed_dim=128, depth=1, num_heads=2,
+                    dtype="bf16")
+    model = VisionTransformer(cfg).to(DEV)
+    model.reset_parameters(seed=3)
+    g = torch.Generator().manual_seed(4)
+    img = torch.rand(4, 3, 32, 32, generator=g).to(DEV)
+    tgt = torch.randint(0, 2, (4,), generator=g).to(DEV)
+    cross_entropy(model(img), tgt).backward()          # builds the arena and its shadow
+    arena = model.arena()
+    opt = optim.Adam(list(model.parameters()), learning_rate=1e-2)
+    assert opt._arena is None                           # the per-tensor path
+    opt.step()
+    model(img)                                          # the forward refreshes the shadow if stale
+    torch.cuda.synchronize()
+    assert torch.equal(arena.flat_lp, arena.flat.to(torch.bfloat16))

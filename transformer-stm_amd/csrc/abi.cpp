@@ -2,6 +2,10 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
 #include "../../include/vitmi.h"
 
 namespace vitmi {
@@ -23,9 +27,73 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// ---- per-kernel algorithmic work (VITMI_STAT, common.h)
+bool g_stats_on = false;
+namespace {
+struct KStat {
+  std::string name;
+  int64_t calls = 0;
+  double flops = 0, bytes = 0;
+};
+std::mutex g_stats_mu;
+std::unordered_map<const void*, size_t> g_stats_idx;
+std::vector<KStat> g_stats;
+}  // namespace
+
+void stat_record(const void* kernel, double flops, double bytes) {
+  std::lock_guard<std::mutex> lk(g_stats_mu);
+  auto it = g_stats_idx.find(kernel);
+  size_t i;
+  if (it == g_stats_idx.end()) {
+    KStat k;
+    const char* n = hipKernelNameRefByPtr(kernel, nullptr);   // the mangled device symbol
+    k.name = n ? n : "?";
+    i = g_stats.size();
+    g_stats.push_back(k);
+    g_stats_idx[kernel] = i;
+  } else {
+    i = it->second;
+  }
+  g_stats[i].calls += 1;
+  g_stats[i].flops += flops;
+  g_stats[i].bytes += bytes;
+}
+
 }  // namespace vitmi
 
-extern "C" int vitmi_version(void) { return 100; /* 0.1.0 */ }
+extern "C" int vitmi_stats_enable(int on) {
+  std::lock_guard<std::mutex> lk(vitmi::g_stats_mu);
+  if (on) {
+    vitmi::g_stats.clear();
+    vitmi::g_stats_idx.clear();
+  }
+  vitmi::g_stats_on = on != 0;
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_stats_count(void) {
+  std::lock_guard<std::mutex> lk(vitmi::g_stats_mu);
+  return (int)vitmi::g_stats.size();
+}
+
+extern "C" int vitmi_stats_get(int i, char* name, int name_len, int64_t* calls, double* flops, double* bytes) {
+  std::lock_guard<std::mutex> lk(vitmi::g_stats_mu);
+  if (i < 0 || i >= (int)vitmi::g_stats.size()) return vitmi::fail(VITMI_ERR_INVALID, "stats_get: index %d", i);
+  const vitmi::KStat& k = vitmi::g_stats[i];
+  if (name && name_len > 0) snprintf(name, (size_t)name_len, "%s", k.name.c_str());
+  if (calls) *calls = k.calls;
+  if (flops) *flops = k.flops;
+  if (bytes) *bytes = k.bytes;
+  return VITMI_OK;
+}
+
+#ifndef VITMI_BUILD_ID
+#define VITMI_BUILD_ID "unknown"
+#endif
+
+extern "C" int vitmi_version(void) { return 200; /* 0.2.0: + RCCL comm, build id */ }
+
+extern "C" const char* vitmi_build_id(void) { return VITMI_BUILD_ID; }
 
 extern "C" const char* vitmi_last_error(void) { return vitmi::g_err; }
 

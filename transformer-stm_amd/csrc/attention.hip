@@ -1015,23 +1015,28 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_fused_seq_bf16(
     // Step t-1 of tile qi belonged to wave w+1; wait for its add (turn[qi] == t) instead of a
     // workgroup barrier, so the waves drift apart and one wave's MFMAs overlap another's softmax.
     // The waits form a chain (w waits on w+1 one step earlier), so they always resolve; the
-    // bound only guards against a logic error hanging the device.
+    // bound only guards against a logic error hanging the device.  Should it ever be hit, the
+    // tile's dQ is poisoned with NaN (the parity tests then fail loudly) instead of being
+    // summed out of order.
+    bool late;
     {
       volatile int* tp = turn + qi;
       for (int spin = 0; *tp != t && spin < (1 << 22); ++spin) __builtin_amdgcn_s_sleep(1);
+      late = *tp != t;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     float* dq_row = dqs + (q0 + (lane & 31)) * DQP;
+    const float poison = late ? __builtin_nanf("") : 0.f;
 #pragma unroll
     for (int d2 = 0; d2 < 2; ++d2)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         f32x4* pq = (f32x4*)(dq_row + 32 * d2 + 8 * g4 + 4 * h);
         f32x4 a = *pq;
-        a[0] += dqp[d2][4 * g4];
-        a[1] += dqp[d2][4 * g4 + 1];
-        a[2] += dqp[d2][4 * g4 + 2];
-        a[3] += dqp[d2][4 * g4 + 3];
+        a[0] += dqp[d2][4 * g4] + poison;
+        a[1] += dqp[d2][4 * g4 + 1] + poison;
+        a[2] += dqp[d2][4 * g4 + 2] + poison;
+        a[3] += dqp[d2][4 * g4 + 3] + poison;
         *pq = a;
       }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1059,359 +1064,6 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_fused_seq_bf16(
       const f32x4 a = *(const f32x4*)(src + 4 * c);
       store4(qrow + 4 * c, a[0] * scale, a[1] * scale, a[2] * scale, a[3] * scale);
     }
-  }
-}
-
-// ============================================ persistent, pipelined whole-sequence kernels
-// The same math as the three kernels above, but ONE workgroup per CU walks (batch, head)
-// pairs p = blockIdx.x, +gridDim.x, ...  While pair p computes out of LDS buffer `cur`, the
-// LDS-staged operands of the next pair are DMA'd into buffer cur^1 and its register operands
-// are loaded, so HBM streaming overlaps MFMA/softmax work (the one-shot kernels above load,
-// then compute, with both co-resident workgroups in lockstep).  One `s_waitcnt vmcnt(0)` +
-// barrier per pair retires the prefetch and frees `cur` for the pair after next; the output
-// stores of pair p drain during pair p+1.
-
-// rebased descriptor of head `hd`, matrix `which` (0 q, 1 k, 2 v) of batch b in qkv
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t qkv_rsrc(const bf16* qkv, int b, int hd, int which, int N,
-                                                           int D) {
-  const int64_t ld = 3 * (int64_t)D;
-  const uint32_t bytes = (uint32_t)((int64_t)N * ld * 2);
-  const int col = which * D + hd * DH;
-  return make_rsrc(qkv + (int64_t)b * N * ld + col, bytes - col * 2);
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t od_rsrc(const bf16* t, int b, int hd, int N, int D) {
-  const uint32_t bytes = (uint32_t)((int64_t)N * D * 2);
-  return make_rsrc(t + (int64_t)b * N * D + hd * DH, bytes - hd * DH * 2);
-}
-
-// grid min(B*H, CUs), block 64*NW.  LDS: 2 x (K | V).
-template <int NPMAX>
-__global__ __launch_bounds__(NPMAX * 2, 2) void attn_fwd_pp_bf16(const bf16* __restrict__ qkv,
-                                                              bf16* __restrict__ o, float* __restrict__ lse,
-                                                              int N, int H, float scale, int npairs) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * NPMAX * 128];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = blockDim.x >> 6, NP = nw * 32;
-  const int D = H * DH;
-  const int64_t ldb = 3 * (int64_t)D * 2;
-  const int h = lane >> 5;
-  const int q = wave * 32 + (lane & 31);
-  int p = blockIdx.x;
-  if (p >= npairs) return;
-  auto kbuf = [&](int c) { return smem + c * 2 * NPMAX * 128; };
-  auto prefetch = [&](int pp, int c, bf16x8* qdst) {
-    const int b = pp / H, hd = pp % H;
-    stage_seq(kbuf(c), qkv_rsrc(qkv, b, hd, 1, N, D), ldb, NP, nw, wave, lane);
-    stage_seq(kbuf(c) + NPMAX * 128, qkv_rsrc(qkv, b, hd, 2, N, D), ldb, NP, nw, wave, lane);
-    const __amdgpu_buffer_rsrc_t rq = qkv_rsrc(qkv, b, hd, 0, N, D);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qdst[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
-  };
-  bf16x8 qf[4], qn[4];
-  prefetch(p, 0, qf);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const float c2 = scale * LOG2E;
-  int cur = 0;
-  for (;;) {
-    const int pn = p + gridDim.x;
-    const bool hn = pn < npairs;
-    if (hn) prefetch(pn, cur ^ 1, qn);
-    const char* kt = kbuf(cur);
-    const char* vt = kt + NPMAX * 128;
-    float m = -INFINITY, l = 0.f;
-    f32x16 oacc[2] = {zero16(), zero16()};
-    auto tile = [&](auto uc, auto mc, int k0) {
-      constexpr int U = decltype(uc)::value;
-      constexpr bool MASK = decltype(mc)::value;
-      f32x16 st[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        st[u] = zero16();
-#pragma unroll
-        for (int s = 0; s < 4; ++s) st[u] = mfma32(frag_row(kt, k0 + 32 * u, s, lane), qf[s], st[u]);
-      }
-      if constexpr (MASK) {   // only the last tile holds keys >= N
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (k0 + 32 * u + acc_row(r, h) >= N) st[u][r] = -INFINITY;
-      }
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[u][r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m, tmax * c2);
-      const float alpha = fexp2(m - mn);
-      const bool first = m == -INFINITY;
-      m = mn;
-      float rs = 0.f;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = fexp2(fmaf(st[u][r], c2, -mn));
-          st[u][r] = pv;
-          rs += pv;
-        }
-      l = fmaf(l, alpha, rs);
-      if (!first && __builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 pb = pack8(st[u], s);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
-            oacc[dt] = mfma32(frag_tr(vt, k0 + 32 * u + 16 * s, 32 * dt, lane), pb, oacc[dt]);
-        }
-    };
-    int k0 = 0;
-    // full tiles of valid keys without the mask; padding keys (< 32 of them) sit in the last tile
-    for (; k0 + 64 <= N; k0 += 64) tile(std::integral_constant<int, 2>{}, std::false_type{}, k0);
-    if (k0 + 64 <= NP) {
-      tile(std::integral_constant<int, 2>{}, std::true_type{}, k0);
-      k0 += 64;
-    }
-    if (k0 < NP) tile(std::integral_constant<int, 1>{}, std::true_type{}, k0);
-    const float lt = l + __shfl_xor(l, 32, 64);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next pair staged / loaded
-    __syncthreads();                                     // ... by every wave; `cur` is free
-    if (q < N) {
-      const int b = p / H, hd = p % H;
-      const float inv = 1.f / lt;
-      bf16* orow = o + ((int64_t)b * N + q) * D + hd * DH;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d = 32 * dt + 8 * g4 + 4 * h;
-          store4(orow + d, oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv, oacc[dt][4 * g4 + 2] * inv,
-                 oacc[dt][4 * g4 + 3] * inv);
-        }
-      if (h == 0) lse[(int64_t)p * N + q] = (m + log2f(lt)) * LN2;
-    }
-    if (!hn) break;
-    p = pn;
-    cur ^= 1;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = qn[s];
-  }
-}
-
-// dQ (+ delta): LDS 2 x (K | V); Q, dO, O rows and lse of the next pair prefetched to registers.
-template <int NPMAX>
-__global__ __launch_bounds__(NPMAX * 2, 2) void attn_bwd_dq_pp_bf16(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
-    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
-    float scale, int npairs) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * NPMAX * 128];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = blockDim.x >> 6, NP = nw * 32;
-  const int D = H * DH;
-  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
-  const int h = lane >> 5;
-  const int q = wave * 32 + (lane & 31);
-  const bool qok = q < N;
-  int p = blockIdx.x;
-  if (p >= npairs) return;
-  auto kbuf = [&](int c) { return smem + c * 2 * NPMAX * 128; };
-  auto prefetch = [&](int pp, int c, bf16x8* qd, bf16x8* dd, bf16x8* od, float& l2) {
-    const int b = pp / H, hd = pp % H;
-    stage_seq(kbuf(c), qkv_rsrc(qkv, b, hd, 1, N, D), ldb, NP, nw, wave, lane);
-    stage_seq(kbuf(c) + NPMAX * 128, qkv_rsrc(qkv, b, hd, 2, N, D), ldb, NP, nw, wave, lane);
-    const __amdgpu_buffer_rsrc_t rq = qkv_rsrc(qkv, b, hd, 0, N, D);
-    const __amdgpu_buffer_rsrc_t rdo = od_rsrc(dout, b, hd, N, D), ro = od_rsrc(o, b, hd, N, D);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const uint32_t off = (uint32_t)((int64_t)q * ldo + (16 * s + 8 * h) * 2);
-      dd[s] = load_row16(rdo, off);
-      od[s] = load_row16(ro, off);
-      qd[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
-    }
-    l2 = qok ? lse[(int64_t)pp * N + q] * LOG2E : INFINITY;   // q >= N -> p = 0
-  };
-  bf16x8 qf[4], df[4], of[4], qn[4], dn[4], on[4];
-  float L2, L2n;
-  prefetch(p, 0, qf, df, of, L2);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const float c2 = scale * LOG2E;
-  int cur = 0;
-  for (;;) {
-    const int pn = p + gridDim.x;
-    const bool hn = pn < npairs;
-    float dl;
-    {
-      float part = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) part += (float)of[s][j] * (float)df[s][j];
-      dl = part + __shfl_xor(part, 32, 64);
-    }
-    if (qok && h == 0) delta[(int64_t)p * N + q] = dl;
-    if (hn) prefetch(pn, cur ^ 1, qn, dn, on, L2n);
-    const char* kt = kbuf(cur);
-    const char* vt = kt + NPMAX * 128;
-    f32x16 dqt[2] = {zero16(), zero16()};
-#pragma unroll 1
-    for (int k0 = 0; k0 < NP; k0 += 32) {
-      f32x16 st = zero16(), dp = zero16();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        st = mfma32(frag_row(kt, k0, s, lane), qf[s], st);
-        dp = mfma32(frag_row(vt, k0, s, lane), df[s], dp);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = fexp2(fmaf(st[r], c2, -L2));
-        dp[r] = pv * (dp[r] - dl);
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 sb = pack8(dp, s);
-#pragma unroll
-        for (int d2 = 0; d2 < 2; ++d2) dqt[d2] = mfma32(frag_tr(kt, k0 + 16 * s, 32 * d2, lane), sb, dqt[d2]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (qok) {
-      const int b = p / H, hd = p % H;
-      bf16* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
-#pragma unroll
-      for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d = 32 * d2 + 8 * g4 + 4 * h;
-          store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale, dqt[d2][4 * g4 + 2] * scale,
-                 dqt[d2][4 * g4 + 3] * scale);
-        }
-    }
-    if (!hn) break;
-    p = pn;
-    cur ^= 1;
-    L2 = L2n;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) { qf[s] = qn[s]; df[s] = dn[s]; of[s] = on[s]; }
-  }
-}
-
-// dK/dV: LDS 2 x (Q | dO | lse | delta), the lse/delta rows by one LDS-DMA each (queries >= N
-// read as 0: harmless, their Q and dO rows are zero, so P.dO, dS.Q and dS vanish for them);
-// K and V rows of the next pair prefetched to registers.
-template <int NPMAX>
-__global__ __launch_bounds__(NPMAX * 2, 2) void attn_bwd_dkv_pp_bf16(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale, int npairs) {
-  constexpr int BUF = 2 * NPMAX * 128 + 2 * 1024;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
-  static_assert(NPMAX * 4 <= 1024, "lse/delta rows must fit one LDS-DMA instruction");
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = blockDim.x >> 6, NP = nw * 32;
-  const int D = H * DH;
-  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
-  const int h = lane >> 5;
-  const int key = wave * 32 + (lane & 31);
-  int p = blockIdx.x;
-  if (p >= npairs) return;
-  auto qbuf = [&](int c) { return smem + c * BUF; };
-  auto prefetch = [&](int pp, int c, bf16x8* kd, bf16x8* vd) {
-    const int b = pp / H, hd = pp % H;
-    stage_seq(qbuf(c), qkv_rsrc(qkv, b, hd, 0, N, D), ldb, NP, nw, wave, lane);
-    stage_seq(qbuf(c) + NPMAX * 128, od_rsrc(dout, b, hd, N, D), ldo, NP, nw, wave, lane);
-    if (wave == 0) {
-      char* rows = qbuf(c) + 2 * NPMAX * 128;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(lse + (int64_t)pp * N, N * 4), LDS_PTR(void, rows), 16,
-                                               lane * 16, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(delta + (int64_t)pp * N, N * 4),
-                                               LDS_PTR(void, rows + 1024), 16, lane * 16, 0, 0, 0);
-    }
-    const __amdgpu_buffer_rsrc_t rk = qkv_rsrc(qkv, b, hd, 1, N, D), rv = qkv_rsrc(qkv, b, hd, 2, N, D);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kd[s] = load_row16(rk, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
-      vd[s] = load_row16(rv, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
-    }
-  };
-  bf16x8 kf[4], vf[4], kn[4], vn[4];
-  prefetch(p, 0, kf, vf);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const float c2 = scale * LOG2E;
-  int cur = 0;
-  for (;;) {
-    const int pn = p + gridDim.x;
-    const bool hn = pn < npairs;
-    if (hn) prefetch(pn, cur ^ 1, kn, vn);
-    const char* qt = qbuf(cur);
-    const char* dt_ = qt + NPMAX * 128;
-    const float* lsr = (const float*)(qt + 2 * NPMAX * 128);
-    const float* dls = lsr + 256;
-    f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
-#pragma unroll 1
-    for (int q0 = 0; q0 < NP; q0 += 32) {
-      f32x16 sa = zero16(), dp = zero16();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);
-        dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);
-      }
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int q4 = q0 + 8 * g4 + 4 * h;
-        const f32x4 ls = *(const f32x4*)(lsr + q4);
-        const f32x4 dl = *(const f32x4*)(dls + q4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float pv = fexp2(fmaf(sa[4 * g4 + i], c2, -ls[i] * LOG2E));
-          sa[4 * g4 + i] = pv;
-          dp[4 * g4 + i] = pv * (dp[4 * g4 + i] - dl[i]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
-#pragma unroll
-        for (int d2 = 0; d2 < 2; ++d2) {
-          dvt[d2] = mfma32(frag_tr(dt_, q0 + 16 * s, 32 * d2, lane), pb, dvt[d2]);
-          dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (key < N) {
-      const int b = p / H, hd = p % H;
-      bf16* row = dqkv + ((int64_t)b * N + key) * ld;
-#pragma unroll
-      for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d = 32 * d2 + 8 * g4 + 4 * h;
-          store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
-                 dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
-          store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
-                 dvt[d2][4 * g4 + 3]);
-        }
-    }
-    if (!hn) break;
-    p = pn;
-    cur ^= 1;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) { kf[s] = kn[s]; vf[s] = vn[s]; }
   }
 }
 
@@ -1580,35 +1232,19 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_f32(const float* __restrict__
 
 using namespace vitmi;
 
-// whole-sequence kernels for N <= SEQ_MAX (8 waves, 2 workgroups of <= 64 KiB LDS per CU);
-// VITMI_ATTN_STREAM=1 forces the streamed kernels (A/B timing, tests)
+// whole-sequence kernels for N <= SEQ_MAX (8 waves, 2 workgroups of <= 64 KiB LDS per CU).
+// Kernel policy (vitmi_attention_set_policy; tests / A-B timing): 0 = auto, 1 = always the
+// streamed kernels, 2 = auto with the single-pass fused backward for N <= SEQ_MAX.
 static constexpr int SEQ_MAX = 256;
-static bool seq_path(int N) {
-  const char* e = getenv("VITMI_ATTN_STREAM");
-  return N <= SEQ_MAX && !(e && atoi(e));
-}
+static int g_attn_policy = 0;
+static bool seq_path(int N) { return N <= SEQ_MAX && g_attn_policy != 1; }
+static bool fused_bwd() { return g_attn_policy == 2; }
 
-// persistent pipelined variants of the whole-sequence kernels (VITMI_ATTN_PP=1; default off:
-// at 7 resident waves per CU their compute is slower than the overlap they buy)
-static int pp_grid(int npairs) {
-  static int cus = 0;
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("VITMI_ATTN_PP");
-    on = e && atoi(e) == 1;   // measured slower than the one-shot kernels: opt-in
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
-  if (!on) return 0;
-  return npairs < cus ? npairs : cus;
-}
-
-// single-pass fused backward for N <= SEQ_MAX (VITMI_ATTN_FUSED=0 selects the dQ + dK/dV pair)
-static bool fused_bwd() {
-  const char* e = getenv("VITMI_ATTN_FUSED");
-  return e ? atoi(e) != 0 : false;
+extern "C" int vitmi_attention_set_policy(int policy) {
+  VITMI_CHECK_ARG(policy >= 0 && policy <= 2, "attention_set_policy: policy must be 0..2");
+  const int prev = g_attn_policy;
+  g_attn_policy = policy;
+  return prev;
 }
 
 static int attn_check(int dtype, int B, int N, int H, int dh) {
@@ -1627,12 +1263,8 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
   hipStream_t s = (hipStream_t)stream;
   if (dtype == VITMI_BF16 && seq_path(N)) {
     const dim3 block(64 * ((N + 31) / 32));
-    if (const int g = pp_grid(B * H))
-      hipLaunchKernelGGL(attn_fwd_pp_bf16<SEQ_MAX>, dim3(g), block, 0, s, (const bf16*)qkv, (bf16*)o, lse, N, H,
-                         scale, B * H);
-    else
-      hipLaunchKernelGGL(attn_fwd_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv, (bf16*)o, lse, N,
-                         H, scale);
+    hipLaunchKernelGGL(attn_fwd_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv, (bf16*)o, lse, N,
+                       H, scale);
   } else if (dtype == VITMI_BF16) {
     dim3 grid((N + 127) / 128, B * H);
     hipLaunchKernelGGL(attn_fwd_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (bf16*)o, lse, N, H, scale);
@@ -1641,6 +1273,14 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
     hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(64), 0, s, (const float*)qkv, (float*)o, lse, N, H, scale);
   }
   VITMI_LAUNCH_CHECK("attention_fwd");
+  {
+    // QK^T and PV: 4 N^2 dh flops per (batch, head); q/k/v read, o + lse written
+    const double es = dtype == VITMI_BF16 ? 2 : 4, bh = (double)B * H;
+    const double fl = 4.0 * bh * N * N * DH, by = bh * N * DH * 4 * es + bh * N * 4;
+    if (dtype == VITMI_BF16 && seq_path(N)) VITMI_STAT(attn_fwd_seq_bf16<SEQ_MAX>, fl, by);
+    else if (dtype == VITMI_BF16) VITMI_STAT(attn_fwd_bf16, fl, by);
+    else VITMI_STAT(attn_fwd_f32, fl, by);
+  }
   return VITMI_OK;
 }
 
@@ -1666,11 +1306,6 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     if (!colsum && fused_bwd()) {
       hipLaunchKernelGGL(attn_bwd_fused_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
                          (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, N, H, scale);
-    } else if (const int g = colsum ? 0 : pp_grid(B * H)) {
-      hipLaunchKernelGGL(attn_bwd_dq_pp_bf16<SEQ_MAX>, dim3(g), block, 0, s, (const bf16*)qkv, (const bf16*)o,
-                         (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, B * H);
-      hipLaunchKernelGGL(attn_bwd_dkv_pp_bf16<SEQ_MAX>, dim3(g), block, 0, s, (const bf16*)qkv,
-                         (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, B * H);
     } else {
       hipLaunchKernelGGL(attn_bwd_dq_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
                          (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
@@ -1695,6 +1330,23 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
                        lse, (const float*)delta, (float*)dqkv, N, H, scale);
   }
   VITMI_LAUNCH_CHECK("attention_bwd");
+  {
+    // algorithmic backward = dP, dQ (dQ kernel) + dV, dK (dK/dV kernel): 8 N^2 dh flops per head
+    // (recomputing S is not counted); bytes: q/k/v/o/dO read, dq/dk/dv written, lse/delta
+    const double es = dtype == VITMI_BF16 ? 2 : 4, bh = (double)B * H, t = bh * N * DH;
+    const double fl = 4.0 * bh * N * N * DH;
+    if (dtype == VITMI_BF16 && seq_path(N)) {
+      if (!colsum && fused_bwd()) {
+        VITMI_STAT(attn_bwd_fused_seq_bf16<SEQ_MAX>, 2 * fl, t * 8 * es + bh * N * 4);
+      } else {
+        VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+        VITMI_STAT(attn_bwd_dkv_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+      }
+    } else if (dtype == VITMI_BF16) {
+      VITMI_STAT(attn_bwd_dq_bf16, fl, t * 6 * es + bh * N * 8);
+      VITMI_STAT(attn_bwd_dkv_bf16, fl, t * 6 * es + bh * N * 8);
+    }
+  }
   return VITMI_OK;
 }
 

@@ -1,0 +1,161 @@
+// comm.cpp — RCCL gradient exchange of the data-parallel path.
+//
+// The reference's only parallel construct is tf.distribute.MirroredStrategy()
+// (old_codes/BayConvT(Par)(Muti).py:16-19): synchronous data parallelism whose
+// cross-replica gradient reduction TF runs as an NCCL all-reduce on one host.  Here it is
+// one process per GPU and one RCCL communicator per process; buckets of the flat gradient
+// buffer are all-reduced on a caller-owned side stream, gated by a hipEvent recorded on
+// the compute stream, so the exchange overlaps the rest of the backward (vitmi/dp.py).
+//
+// RCCL is bound at run time (dlopen/dlsym), preferring the copy already mapped into the
+// process: PyTorch-ROCm loads its own librccl.so, and two RCCL instances in one process
+// would each start their own proxy threads and IPC state.  No RCCL symbol is linked, so
+// the library still loads (and every other entry point works) where RCCL is absent.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+#include "common.h"
+
+namespace vitmi {
+namespace {
+
+struct Rccl {
+  void* handle = nullptr;
+  decltype(&::ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&::ncclCommInitRank) init_rank = nullptr;
+  decltype(&::ncclAllReduce) all_reduce = nullptr;
+  decltype(&::ncclBroadcast) broadcast = nullptr;
+  decltype(&::ncclCommDestroy) destroy = nullptr;
+  decltype(&::ncclCommAbort) abort = nullptr;
+  decltype(&::ncclGetErrorString) err = nullptr;
+  decltype(&::ncclCommGetAsyncError) async_err = nullptr;
+};
+
+Rccl g_rccl;
+ncclComm_t g_comm = nullptr;
+int g_rank = -1, g_world = 0;
+
+template <typename F>
+bool sym(void* h, const char* name, F& out) {
+  out = reinterpret_cast<F>(dlsym(h, name));
+  return out != nullptr;
+}
+
+int load_rccl() {
+  if (g_rccl.handle) return VITMI_OK;
+  // already mapped (torch's bundled copy is loaded by its file name, it has no SONAME)?
+  const char* names[] = {"librccl.so", "librccl.so.1"};
+  void* h = nullptr;
+  for (const char* n : names)
+    if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD)) != nullptr) break;
+  if (!h)
+    for (const char* n : names)
+      if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+  if (!h) return fail(VITMI_ERR_COMM, "comm: cannot load librccl.so (%s)", dlerror());
+  Rccl r;
+  r.handle = h;
+  if (!sym(h, "ncclGetUniqueId", r.get_unique_id) || !sym(h, "ncclCommInitRank", r.init_rank) ||
+      !sym(h, "ncclAllReduce", r.all_reduce) || !sym(h, "ncclBroadcast", r.broadcast) ||
+      !sym(h, "ncclCommDestroy", r.destroy) || !sym(h, "ncclCommAbort", r.abort) ||
+      !sym(h, "ncclGetErrorString", r.err) || !sym(h, "ncclCommGetAsyncError", r.async_err))
+    return fail(VITMI_ERR_COMM, "comm: librccl.so lacks an NCCL 2.x entry point");
+  g_rccl = r;
+  return VITMI_OK;
+}
+
+int nccl_fail(const char* what, ncclResult_t r) {
+  return fail(VITMI_ERR_COMM, "comm: %s: %s (%d)", what, g_rccl.err ? g_rccl.err(r) : "?", (int)r);
+}
+
+bool dtype_of(int dtype, ncclDataType_t& t) {
+  if (dtype == VITMI_F32) t = ncclFloat32;
+  else if (dtype == VITMI_BF16) t = ncclBfloat16;
+  else return false;
+  return true;
+}
+
+}  // namespace
+}  // namespace vitmi
+
+using namespace vitmi;
+
+extern "C" int vitmi_comm_get_unique_id(char* uid) {
+  VITMI_CHECK_ARG(uid != nullptr, "comm_get_unique_id: uid is null");
+  if (int rc = load_rccl()) return rc;
+  ncclUniqueId id;
+  if (ncclResult_t r = g_rccl.get_unique_id(&id)) return nccl_fail("ncclGetUniqueId", r);
+  static_assert(sizeof(id.internal) == VITMI_COMM_UID_BYTES, "ncclUniqueId size");
+  memcpy(uid, id.internal, VITMI_COMM_UID_BYTES);
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
+  VITMI_CHECK_ARG(world >= 1 && rank >= 0 && rank < world, "comm_init: rank %d / world %d", rank, world);
+  VITMI_CHECK_ARG(uid != nullptr, "comm_init: uid is null");
+  VITMI_CHECK_ARG(g_comm == nullptr, "comm_init: a communicator already exists (vitmi_comm_destroy first)");
+  if (int rc = load_rccl()) return rc;
+  ncclUniqueId id;
+  memcpy(id.internal, uid, VITMI_COMM_UID_BYTES);
+  ncclComm_t c = nullptr;
+  // the communicator binds to the calling thread's current HIP device
+  if (ncclResult_t r = g_rccl.init_rank(&c, world, id, rank)) return nccl_fail("ncclCommInitRank", r);
+  g_comm = c;
+  g_rank = rank;
+  g_world = world;
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_comm_info(int* rank, int* world) {
+  if (rank) *rank = g_rank;
+  if (world) *world = g_world;
+  return g_comm ? VITMI_OK : fail(VITMI_ERR_INVALID, "comm_info: no communicator");
+}
+
+extern "C" int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, int op, vitmi_stream_t side,
+                                          void* ready_event) {
+  VITMI_CHECK_ARG(g_comm != nullptr, "comm_allreduce_async: vitmi_comm_init first");
+  VITMI_CHECK_ARG(count >= 0, "comm_allreduce_async: negative count");
+  VITMI_CHECK_ARG(op == VITMI_REDUCE_SUM || op == VITMI_REDUCE_AVG, "comm_allreduce_async: bad op %d", op);
+  ncclDataType_t t;
+  VITMI_CHECK_ARG(dtype_of(dtype, t), "comm_allreduce_async: bad dtype %d", dtype);
+  if (count == 0) return VITMI_OK;
+  VITMI_CHECK_ARG(ptr != nullptr, "comm_allreduce_async: null buffer");
+  hipStream_t s = (hipStream_t)side;
+  if (ready_event) {
+    hipError_t e = hipStreamWaitEvent(s, (hipEvent_t)ready_event, 0);
+    if (e != hipSuccess) return fail(VITMI_ERR_HIP, "comm_allreduce_async: hipStreamWaitEvent: %s", hipGetErrorString(e));
+  }
+  const ncclRedOp_t rop = op == VITMI_REDUCE_AVG ? ncclAvg : ncclSum;
+  if (ncclResult_t r = g_rccl.all_reduce(ptr, ptr, (size_t)count, t, rop, g_comm, s)) return nccl_fail("ncclAllReduce", r);
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_comm_broadcast(void* ptr, int64_t count, int dtype, int root, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(g_comm != nullptr, "comm_broadcast: vitmi_comm_init first");
+  VITMI_CHECK_ARG(root >= 0 && root < g_world, "comm_broadcast: bad root %d", root);
+  ncclDataType_t t;
+  VITMI_CHECK_ARG(dtype_of(dtype, t), "comm_broadcast: bad dtype %d", dtype);
+  if (count == 0) return VITMI_OK;
+  if (ncclResult_t r = g_rccl.broadcast(ptr, ptr, (size_t)count, t, root, g_comm, (hipStream_t)stream))
+    return nccl_fail("ncclBroadcast", r);
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_comm_check(void) {
+  if (!g_comm) return VITMI_OK;
+  ncclResult_t a = ncclSuccess;
+  if (ncclResult_t r = g_rccl.async_err(g_comm, &a)) return nccl_fail("ncclCommGetAsyncError", r);
+  if (a != ncclSuccess && a != ncclInProgress) return nccl_fail("asynchronous error", a);
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_comm_destroy(int abort) {
+  if (!g_comm) return VITMI_OK;
+  ncclComm_t c = g_comm;
+  g_comm = nullptr;
+  g_rank = -1;
+  g_world = 0;
+  ncclResult_t r = abort ? g_rccl.abort(c) : g_rccl.destroy(c);
+  return r ? nccl_fail(abort ? "ncclCommAbort" : "ncclCommDestroy", r) : VITMI_OK;
+}

@@ -96,6 +96,17 @@ __device__ __forceinline__ uint32_t clamp_bytes(int64_t b) {
   return b <= 0 ? 0u : (b > 0x7fffffff ? 0x7fffffffu : (uint32_t)b);
 }
 
+// Algorithmic work of one kernel launch (flops = 2 x MACs of its dense contractions, bytes =
+// the HBM bytes its operands must move at least once), accumulated per kernel while
+// vitmi_stats_enable(1) is on (abi.cpp): bench.py joins it with a rocprofv3 kernel trace of
+// the same run to report per-kernel TFLOP/s and GB/s.  Off (one branch) otherwise.
+extern bool g_stats_on;
+void stat_record(const void* kernel, double flops, double bytes);
+#define VITMI_STAT(kernel, flops, bytes)                                                     \
+  do {                                                                                      \
+    if (::vitmi::g_stats_on) ::vitmi::stat_record((const void*)(kernel), (double)(flops), (double)(bytes)); \
+  } while (0)
+
 // db[n] += sum_z part[z][n] in a fixed order (elementwise.hip)
 int launch_colsum_finish(int64_t N, int Z, const float* part, float* db, hipStream_t s);
 

@@ -212,7 +212,10 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
   mean[c] = (float)mu;
   rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (run_mean) run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * (float)mu;
-  if (run_var) run_var[c] = momentum * run_var[c] + (1.f - momentum) * (float)var;
+  // the moving variance takes the unbiased batch variance (Bessel's n/(n-1)), as Keras'
+  // fused BatchNormalization on NHWC tensors and torch's BatchNorm2d (MS_CvT) both do
+  const double var_u = n > 1 ? var * (double)n / (double)(n - 1) : var;
+  if (run_var) run_var[c] = momentum * run_var[c] + (1.f - momentum) * (float)var_u;
 }
 
 // y = (z - mean) * rstd * gamma + beta  -> rows b*y_img + y_off + hw of y (out dtype)

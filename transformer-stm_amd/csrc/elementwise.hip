@@ -269,6 +269,24 @@ __global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16* __re
   if (t < n) dst[t] = (bf16)src[t];
 }
 
+__global__ void cast_up_kernel(int64_t n, const bf16* __restrict__ src, float* __restrict__ dst) {
+  const int64_t n8 = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bf16x8 v = *(const bf16x8*)(src + i * 8);
+    f32x4 a, b;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] = (float)v[j];
+      b[j] = (float)v[4 + j];
+    }
+    *(f32x4*)(dst + i * 8) = a;
+    *(f32x4*)(dst + i * 8 + 4) = b;
+  }
+  const int64_t t = n8 * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) dst[t] = (float)src[t];
+}
+
 // y[r][c] = x[r][c] * keep(seed, site, r, c) / (1 - p): the dropout mask applied to a
 // gradient in the backward (the forward fuses it into the GEMM epilogues).  4 columns per
 // thread; N % 4 == 0.
@@ -364,12 +382,15 @@ extern "C" int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, 
   const bool vec = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)dy % 16 == 0);
   if (vec) {
     dim3 grid((unsigned)((N + 511) / 512), Z);
-    if (dtype == VITMI_BF16)
+    if (dtype == VITMI_BF16) {
       hipLaunchKernelGGL(colsum8_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)dy, ldy,
                          (float*)workspace, rows_per);
-    else
+      VITMI_STAT(colsum8_kernel<bf16>, 0, (double)M * N * 2);
+    } else {
       hipLaunchKernelGGL(colsum8_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)dy, ldy,
                          (float*)workspace, rows_per);
+      VITMI_STAT(colsum8_kernel<float>, 0, (double)M * N * 4);
+    }
   } else {
     dim3 grid((unsigned)((N + 255) / 256), Z);
     if (dtype == VITMI_BF16)
@@ -424,7 +445,19 @@ extern "C" int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi
   if (n == 0) return VITMI_OK;
   hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n / 8 + 1)), dim3(256), 0, (hipStream_t)stream, n, src,
                      (bf16*)dst);
+  VITMI_STAT(cast_kernel, 0, 6.0 * n);
   VITMI_LAUNCH_CHECK("cast");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_cast_bf16_f32(int64_t n, const void* src, float* dst, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(src && dst, "cast_bf16_f32: null pointer");
+  VITMI_CHECK_ARG(((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % 16) == 0,
+                  "cast_bf16_f32: 16-byte alignment required");
+  if (n == 0) return VITMI_OK;
+  hipLaunchKernelGGL(cast_up_kernel, dim3(grid_for(n / 8 + 1)), dim3(256), 0, (hipStream_t)stream, n,
+                     (const bf16*)src, dst);
+  VITMI_LAUNCH_CHECK("cast_bf16_f32");
   return VITMI_OK;
 }
 

@@ -55,29 +55,17 @@ struct GemmArgs {
   // dropout of the *_DROP epilogues (see drop_hash in common.h)
   uint32_t drop_seed, drop_site, drop_thresh;
   float drop_scale;
-  // gemm256 tile order: groups of group_m tile-rows, column-major inside a group, so the 32
-  // tiles an XCD runs concurrently span ~group_m A panels x 32/group_m B panels (L2 reuse);
-  // 1 = plain row-major order
-  int group_m;
   // gemm256 DGELU epilogue: column sums of the output (the bias gradient of the layer whose
   // input gradient this is), one fp32 row per 128-row half tile: colsum[(2*tm + wm)*N + col]
   float* colsum;
 };
 
-// (tile-row, tile-col) of tile index tl in the grouped order (a bijection on [0, tm*tn))
+// (tile-row, tile-col) of tile index tl: row-major over the tiles_n tile columns (a persistent
+// block walks consecutive tiles, so an XCD's concurrent tiles share A row panels in its L2;
+// grouped column-major orders measured 0.5-1 % slower end to end)
 __device__ __forceinline__ void tile_rc(const GemmArgs& g, int tl, int& tm, int& tn) {
-  const int G = g.group_m;
-  if (G <= 1) {
-    tm = tl / g.tiles_n;
-    tn = tl - tm * g.tiles_n;
-    return;
-  }
-  const int tiles_m = (int)((g.M + 255) / 256);
-  const int per = G * g.tiles_n;
-  const int grp = tl / per, r = tl - grp * per;
-  const int gm = min(G, tiles_m - grp * G);
-  tn = r / gm;
-  tm = grp * G + (r - tn * gm);
+  tm = tl / g.tiles_n;
+  tn = tl - tm * g.tiles_n;
 }
 
 // internal epilogues: split-K partial slab, and GELU / residual with a fused dropout
@@ -946,18 +934,11 @@ __global__ __launch_bounds__(256) void tail_colsum_kernel(GemmArgs g) {
 static int g_policy = 0;
 static int g_cus = 256;   // compute units of the current device (set on first use)
 
-static int g_grid_override = 0;   // VITMI_GEMM_GRID: 0 = persistent (one block per CU), -1 = one block per tile
-static int g_fold = 1;            // VITMI_GEMM_FOLD: 1 = split-K folded into persistent units, 0 = gridDim.z
-static int g_split256 = 1;        // VITMI_GEMM_SPLIT256: 1 = few-tile split-K GEMMs on gemm256
-static int g_group_m = 1;         // VITMI_GEMM_GROUP: gemm256 tile-row group (1 = row-major order)
+static int g_reserved = 0;        // CUs the persistent grid leaves free (vitmi_gemm_set_reserved_cus)
 
 static void init_cus() {
   static bool done = false;
   if (done) return;
-  if (const char* e = getenv("VITMI_GEMM_GRID")) g_grid_override = atoi(e);
-  if (const char* e = getenv("VITMI_GEMM_FOLD")) g_fold = atoi(e);
-  if (const char* e = getenv("VITMI_GEMM_SPLIT256")) g_split256 = atoi(e);
-  if (const char* e = getenv("VITMI_GEMM_GROUP")) g_group_m = atoi(e);
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
@@ -982,15 +963,13 @@ static bool use256(int dtype, int64_t M, int64_t N, int64_t K = 0, bool split = 
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   if (tiles >= 16) return true;
   init_cus();
-  return split && g_split256 && tiles * splits_for(tiles, (K + 63) / 64, 256) >= 128;
+  return split && tiles * splits_for(tiles, (K + 63) / 64, 256) >= 128;
 }
 
 // persistent grid of the gemm256 launch for nwg tiles and `splits` K-slabs
 static int grid256(int nwg, int splits) {
-  int gx = g_cus / splits;
+  int gx = (g_cus - g_reserved) / splits;
   if (gx < 8 || g_policy == 3) gx = 8;   // policy 3: force many tiles per block (tests)
-  if (g_grid_override < 0) gx = nwg;
-  else if (g_grid_override > 0) gx = g_grid_override;
   return gx > nwg ? nwg : gx;
 }
 
@@ -1019,16 +998,30 @@ static size_t tail_ws_bytes(int64_t M, int64_t N, int64_t K) {
   return (size_t)ntail * S * 256 * 256 * sizeof(float);
 }
 
+// Algorithmic work of one GEMM launch: 2MNK flops; bytes = A and B once, C written once
+// (read too for ACCUM: the += of a weight gradient), plus the epilogue's aux / residual.
+// Split-K partial slabs and tail partials are implementation traffic, not counted here.
+template <typename T, int EPI, typename TC>
+static void gemm_stat(const void* kernel, const GemmArgs& g) {
+  constexpr int EB = EpiOf<EPI>::base;
+  const double M = (double)g.M, N = (double)g.N, K = (double)g.K, es = sizeof(T);
+  double bytes = (M * K + N * K) * es;
+  if (EPI == EPI_PARTIAL || EB == VITMI_EPI_ACCUM) bytes += 2.0 * M * N * 4;   // dW += (read + write, fp32)
+  else bytes += M * N * sizeof(TC);
+  if (EB == VITMI_EPI_BIAS_GELU || EB == VITMI_EPI_DGELU) bytes += M * N * es;   // gelu' written / read
+  if (EB == VITMI_EPI_RESIDUAL) bytes += M * N * 4;                               // residual read
+  VITMI_STAT(kernel, 2.0 * M * N * K, bytes);
+}
+
 template <typename T, bool AK, bool BKM, int EPI, typename TC>
 static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (big) {
       g.tiles_n = (int)((g.N + 255) / 256);
-      g.group_m = g_group_m;
       int nwg = (int)((g.M + 255) / 256) * g.tiles_n;
       g.kz = 1;
       g.ntiles = nwg;
-      if (splits > 1 && g_fold) {
+      if (splits > 1) {
         // fold the K-slabs into the persistent unit space (see GemmArgs::kz)
         g.kz = splits;
         g.kz_steps = (int)(g.k_per_split / 64);
@@ -1041,11 +1034,10 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       g.t_full = nwg;
       g.nsplit = 1;
       g.ksplit = 0;
-      const char* tenv = getenv("VITMI_GEMM_TAIL");   // 0: no tail split (A/B timing)
       // measured: pays off for long reductions (>= 16 K-steps) and for the DGELU epilogue
       // (whose partial units skip its aux loads); a wash or a loss for K = 768 otherwise
       const bool tail_ok = g.k_per_split / 64 >= 16 || EPI == VITMI_EPI_DGELU;
-      if (splits == 1 && tail_ok && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM && g.tail_ws && !(tenv && atoi(tenv) == 0) &&
+      if (splits == 1 && tail_ok && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM && g.tail_ws &&
           tail_plan(nwg, gx, (int)(g.k_per_split / 64), S, ks, ntail) &&
           g.tail_ws_bytes >= (size_t)ntail * S * 256 * 256 * sizeof(float)) {
         g.t_full = nwg - ntail;
@@ -1055,10 +1047,13 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       }
       hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
+      gemm_stat<T, EPI, TC>((const void*)gemm256_kernel<AK, BKM, EPI, TC>, g);
       if (units != nwg) {
         const int blocks = (ntail * 256 * 64 + 255) / 256;
         hipLaunchKernelGGL((gemm_tail_fixup_kernel<T, TC, EPI>), dim3(blocks), dim3(256), 0, s, g, ntail);
         VITMI_LAUNCH_CHECK("gemm_tail_fixup_kernel");
+        // partials read, outputs (+ gelu') written
+        VITMI_STAT((gemm_tail_fixup_kernel<T, TC, EPI>), 0, (double)ntail * 65536 * (4.0 * S + 2 * sizeof(TC)));
         if (g.colsum) {   // the split tail tiles' column sums, from their finished output
           hipLaunchKernelGGL((tail_colsum_kernel<TC>), dim3(ntail * 2), dim3(256), 0, s, g);
           VITMI_LAUNCH_CHECK("tail_colsum_kernel");
@@ -1073,6 +1068,7 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
   dim3 grid(tiles_m * g.tiles_n, 1, splits);
   hipLaunchKernelGGL((gemm_kernel<T, AK, BKM, EPI, TC, BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, s, g);
   VITMI_LAUNCH_CHECK("gemm_kernel");
+  gemm_stat<T, EPI, TC>((const void*)gemm_kernel<T, AK, BKM, EPI, TC, BM, BN, WM, WN>, g);
   return VITMI_OK;
 }
 
@@ -1223,12 +1219,20 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)ws,
                      (float*)C, n, splits, M * N);
   VITMI_LAUNCH_CHECK("splitk_reduce_kernel");
+  VITMI_STAT(splitk_reduce_kernel, 0, (double)n * 4 * (splits + 2));
   return VITMI_OK;
 }
 
 }  // namespace vitmi
 
 using namespace vitmi;
+
+extern "C" int vitmi_gemm_set_reserved_cus(int n) {
+  init_cus();
+  const int prev = g_reserved;
+  g_reserved = n < 0 ? 0 : (n > g_cus - 8 ? g_cus - 8 : n);
+  return prev;
+}
 
 extern "C" int vitmi_gemm_set_policy(int policy) {
   VITMI_CHECK_ARG(policy >= 0 && policy <= 3, "gemm_set_policy: policy must be 0..3");

@@ -204,6 +204,10 @@ static void ln_fwd_launch(hipStream_t s, int64_t M, int D, const float* x, int64
   else
     hipLaunchKernelGGL((ln_fwd_kernel<NV, float>), grid, dim3(256), 0, s, M, D, x, ldx, gamma, beta,
                        eps, (float*)y, ldy, mean, rstd);
+  // x (fp32) read, y written, mean/rstd written
+  const double ysz = ydt == VITMI_BF16 ? 2 : 4;
+  if (ydt == VITMI_BF16) VITMI_STAT((ln_fwd_kernel<NV, bf16>), 0, (double)M * D * (4 + ysz) + 8.0 * M);
+  else VITMI_STAT((ln_fwd_kernel<NV, float>), 0, (double)M * D * (4 + ysz) + 8.0 * M);
 }
 
 template <int NV, typename TDY>
@@ -219,6 +223,10 @@ static void ln_bwd_launch(hipStream_t s, int G, int64_t M, int D, const void* dy
     hipLaunchKernelGGL((ln_bwd_kernel<NV, TDY, false>), dim3(G), dim3(256), 0, s, M, D,
                        (const TDY*)dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx,
                        (bf16*)nullptr, 0, part);
+  // dy + x (+ dres) read, dx (+ bf16 copy) written
+  const double b = (double)M * D * (sizeof(TDY) + 4 + (dres ? 4 : 0) + 4 + (dx_lp ? 2 : 0)) + 8.0 * M;
+  if (dx_lp) VITMI_STAT((ln_bwd_kernel<NV, TDY, true>), 0, b);
+  else VITMI_STAT((ln_bwd_kernel<NV, TDY, false>), 0, b);
 }
 
 }  // namespace vitmi

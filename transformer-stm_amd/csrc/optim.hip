@@ -96,5 +96,8 @@ extern "C" int vitmi_adam_step(int64_t n, float* p, const float* g, float* m, fl
     hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v,
                        (bf16*)nullptr, a);
   VITMI_LAUNCH_CHECK("adam_step");
+  // p, g, m, v read; p, m, v (+ the bf16 shadow) written
+  if (p_lp) VITMI_STAT(adam_kernel<true>, 0, (double)n * 30);
+  else VITMI_STAT(adam_kernel<false>, 0, (double)n * 28);
   return VITMI_OK;
 }

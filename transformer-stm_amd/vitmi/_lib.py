@@ -28,6 +28,7 @@ U = ctypes.c_uint32
 # name -> (restype, argtypes); mirrors include/vitmi.h one to one
 SIGNATURES = {
     "vitmi_version": (I, []),
+    "vitmi_build_id": (ctypes.c_char_p, []),
     "vitmi_last_error": (ctypes.c_char_p, []),
     "vitmi_device_cus": (I, []),
     "vitmi_gemm": (I, [I, I, I, L, L, L, P, L, P, L, P, L, I, I, P, P, L, P, L, P, S, P]),
@@ -75,6 +76,19 @@ SIGNATURES = {
     "vitmi_dense_f32_bwd": (I, [I, I, I, P, L, P, L, P, L, P, P, L, P, P, I, P]),
     "vitmi_avgpool3_fwd": (I, [I, I, I, I, P, L, L, L, P, I, L, L, L, I, P]),
     "vitmi_avgpool3_bwd": (I, [I, I, I, I, P, I, L, L, L, P, L, L, L, I, P]),
+    "vitmi_cast_bf16_f32": (I, [L, P, P, P]),
+    "vitmi_stats_enable": (I, [I]),
+    "vitmi_stats_count": (I, []),
+    "vitmi_stats_get": (I, [I, P, I, P, P, P]),
+    "vitmi_attention_set_policy": (I, [I]),
+    "vitmi_gemm_set_reserved_cus": (I, [I]),
+    "vitmi_comm_get_unique_id": (I, [P]),
+    "vitmi_comm_init": (I, [I, I, P]),
+    "vitmi_comm_info": (I, [P, P]),
+    "vitmi_comm_allreduce_async": (I, [P, L, I, I, P, P]),
+    "vitmi_comm_broadcast": (I, [P, L, I, I, P]),
+    "vitmi_comm_check": (I, []),
+    "vitmi_comm_destroy": (I, [I]),
 }
 
 _lib = None
@@ -104,3 +118,24 @@ def check(rc: int, what: str = "") -> None:
 
 def exported_symbols():
     return list(SIGNATURES)
+
+
+def source_build_id():
+    """The build id the Makefile stamps into the library (vitmi_build_id): sha256 over the bytes
+    of csrc/*.{cpp,h,hip} (sorted by path) followed by include/vitmi.h, first 16 hex digits.
+    None when the sources are not present next to the package."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    hdr = os.path.join(os.path.dirname(pkg), "include", "vitmi.h")
+    names = sorted(os.path.relpath(f, pkg) for ext in ("hip", "cpp", "h")
+                   for f in glob.glob(os.path.join(pkg, "csrc", "*." + ext)))
+    if not names or not os.path.exists(hdr):
+        return None
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(pkg, n), "rb") as f:
+            h.update(f.read())
+    with open(hdr, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]

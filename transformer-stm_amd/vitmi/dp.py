@@ -4,81 +4,203 @@ Replaces the reference's only parallel construct, ``tf.distribute.MirroredStrate
 (``old_codes/BayConvT(Par)(Muti).py:16-19``): synchronous data parallelism with a
 cross-replica mean of every gradient once per step.  MI355X design:
 
-* one process per GPU (torchrun), ``torch.distributed`` with backend ``nccl`` = RCCL
-  over xGMI (``gloo`` on CPU for the tests);
+* one process per GPU (torchrun); ``torch.distributed`` bootstraps the job (rendezvous,
+  TCPStore, barriers) and, with ``comm="vitmi"`` (the default on GPUs), the gradient
+  exchange itself goes through the library's own RCCL communicator
+  (``vitmi_comm_*`` in include/vitmi.h): the 128-byte RCCL id travels through the
+  TCPStore, every bucket is all-reduced on a dedicated side HIP stream after a hipEvent
+  recorded on the compute stream, and the compute stream waits on the side stream once,
+  before the optimizer.  ``comm="torch"`` runs the same buckets through
+  ``torch.distributed.all_reduce`` (RCCL via ProcessGroupNCCL on GPUs, gloo on CPU);
 * all gradients live in ONE flat fp32 buffer (``ParamArena``) laid out in the order
   the backward finishes them (head, norm, block L-1 ... block 0, patch-embed), so
   fixed-size buckets (default 64 MiB: few, large collectives suit per-link-bound
   xGMI rings) become ready front to back;
 * each block's backward calls its ``_grad_ready_hook`` when its grads are final;
-  every bucket wholly inside the finished prefix is all-reduced at once with
-  ``async_op=True``: RCCL runs it on the process group's own HIP stream, ordered
-  after the compute stream's work so far, so it overlaps the rest of the backward;
-* ``finish()`` launches the tail buckets and makes the compute stream wait for them,
-  so the optimizer sees averaged gradients.
+  every bucket wholly inside the finished prefix is all-reduced at once, overlapping the
+  rest of the backward;
+* ``grad_dtype="bf16"`` halves the bytes on the wire (ViT-L: 1.2 GB -> 607 MB per step):
+  each bucket is cast to bf16 on the side stream, averaged, and cast back into the fp32
+  arena (rounding each gradient to bf16 once, plus RCCL's bf16 partial sums);
+* ``reserve_cus``: the persistent GEMM (one 512-thread block per CU, the whole register
+  file) leaves that many CUs free while the backward runs, so RCCL's kernels find CUs
+  instead of waiting for a GEMM to drain (``vitmi_gemm_set_reserved_cus``).
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
+UID_BYTES = 128
+_F32, _BF16 = 0, 1
+REDUCE_SUM, REDUCE_AVG = 0, 1
+
+
+class VitmiComm:
+    """The library's RCCL communicator (one per process, bound to the current HIP device)."""
+
+    def __init__(self, rank: int, world: int, uid: bytes):
+        from ._lib import check, lib
+        if len(uid) != UID_BYTES:
+            raise ValueError(f"vitmi comm: the RCCL id must be {UID_BYTES} bytes")
+        self.rank, self.world = rank, world
+        self._uid = ctypes.create_string_buffer(uid, UID_BYTES)
+        check(lib().vitmi_comm_init(rank, world, self._uid), "comm_init")
+        self._live = True
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from ._lib import check, lib
+        buf = ctypes.create_string_buffer(UID_BYTES)
+        check(lib().vitmi_comm_get_unique_id(buf), "comm_get_unique_id")
+        return buf.raw
+
+    @classmethod
+    def from_store(cls, rank: int, world: int, store=None, key: str = "vitmi_comm_uid") -> "VitmiComm":
+        """Rank 0 creates the id and publishes it in the job's TCPStore; the others wait for it."""
+        return cls(rank, world, exchange_unique_id(rank, world, store, key))
+
+    def allreduce_async(self, buf: torch.Tensor, side: "torch.cuda.Stream", ready=None, op: int = REDUCE_AVG) -> None:
+        from ._lib import check, lib
+        assert buf.is_cuda and buf.is_contiguous() and buf.dtype in (torch.float32, torch.bfloat16)
+        dt = _F32 if buf.dtype == torch.float32 else _BF16
+        check(lib().vitmi_comm_allreduce_async(buf.data_ptr(), buf.numel(), dt, op, side.cuda_stream,
+                                               ready.cuda_event if ready is not None else None),
+              "comm_allreduce_async")
+
+    def broadcast(self, buf: torch.Tensor, root: int = 0) -> None:
+        from ._lib import check, lib
+        dt = _F32 if buf.dtype == torch.float32 else _BF16
+        check(lib().vitmi_comm_broadcast(buf.data_ptr(), buf.numel(), dt, root,
+                                         torch.cuda.current_stream().cuda_stream), "comm_broadcast")
+
+    def check(self) -> None:
+        from ._lib import check, lib
+        check(lib().vitmi_comm_check(), "comm_check")
+
+    def destroy(self, abort: bool = False) -> None:
+        if self._live:
+            from ._lib import check, lib
+            self._live = False
+            check(lib().vitmi_comm_destroy(int(abort)), "comm_destroy")
+
+
+def exchange_unique_id(rank: int, world: int, store=None, key: str = "vitmi_comm_uid") -> bytes:
+    """The RCCL id of a new communicator: created by rank 0 (vitmi_comm_get_unique_id) and passed
+    to the other ranks through the job's TCPStore (the torch.distributed rendezvous)."""
+    if world <= 1:
+        return VitmiComm.unique_id()
+    store = store if store is not None else dist.distributed_c10d._get_default_store()
+    if rank == 0:
+        uid = VitmiComm.unique_id()
+        store.set(key, uid)
+        return uid
+    uid = bytes(store.get(key))
+    if len(uid) != UID_BYTES:
+        raise RuntimeError(f"vitmi comm: id from the store has {len(uid)} bytes, not {UID_BYTES}")
+    return uid
+
 
 class GradReducer:
-    """Bucketed, overlapped all-reduce over one flat gradient buffer."""
+    """Bucketed, overlapped all-reduce (mean) over one flat gradient buffer."""
 
-    def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 64.0, group=None):
+    def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 64.0, group=None,
+                 comm: Optional[VitmiComm] = None, grad_dtype: str = "fp32", reserve_cus: int = 0):
         self.flat = flat_grad
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.backend = dist.get_backend(group) if dist.is_initialized() else None
+        self.comm = comm
+        if comm is not None:
+            self.world = comm.world
+            self.backend = "vitmi"
+        else:
+            self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+            self.backend = dist.get_backend(group) if dist.is_initialized() else None
+        if grad_dtype not in ("fp32", "bf16"):
+            raise ValueError("grad_dtype must be 'fp32' or 'bf16'")
+        if grad_dtype == "bf16" and comm is None:
+            raise ValueError("grad_dtype='bf16' needs the vitmi RCCL communicator")
+        self.grad_dtype = grad_dtype
+        self.reserve_cus = int(reserve_cus)
         n = flat_grad.numel()
         per = max(64, int(bucket_mb * (1 << 20) / flat_grad.element_size()) // 64 * 64)
         self.bounds: List[Tuple[int, int]] = [(s, min(n, s + per)) for s in range(0, n, per)]
         self._next = 0
         self._ready = 0
         self._handles: list = []
+        self._active = comm is not None or self.world > 1
+        self._side = torch.cuda.Stream(device=flat_grad.device) if comm is not None else None
+        self._lp = (torch.empty(n, dtype=torch.bfloat16, device=flat_grad.device)
+                    if comm is not None and grad_dtype == "bf16" else None)
+        self._prev_reserve: Optional[int] = None
         self.launch_log: List[Tuple[int, int]] = []   # (ready prefix, bucket index) for tests
 
     def start(self) -> None:
         """Call before the backward of every step."""
         self._next, self._ready, self._handles = 0, 0, []
         self.launch_log = []
+        if self._active and self.reserve_cus > 0 and self._prev_reserve is None:
+            from ._lib import lib
+            self._prev_reserve = lib().vitmi_gemm_set_reserved_cus(self.reserve_cus)
 
     def _launch(self) -> None:
         s, e = self.bounds[self._next]
         buf = self.flat[s:e]
-        op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
-        h = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
-        self._handles.append((h, buf))
+        if self.comm is not None:
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(buf.device))
+            if self._lp is None:
+                self.comm.allreduce_async(buf, self._side, ready, REDUCE_AVG)
+            else:
+                from . import ops
+                lp = self._lp[s:e]
+                self._side.wait_event(ready)
+                with torch.cuda.stream(self._side):
+                    ops.cast_bf16(buf, lp)
+                    self.comm.allreduce_async(lp, self._side, None, REDUCE_AVG)
+                    ops.cast_f32(lp, buf)
+        else:
+            op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+            h = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
+            self._handles.append((h, buf))
         self.launch_log.append((self._ready, self._next))
         self._next += 1
 
     def mark_ready(self, end: int) -> None:
         """Gradients in flat[0:end] are final: launch every bucket inside that prefix."""
-        if self.world <= 1:
+        if not self._active:
             return
         self._ready = max(self._ready, end)
         while self._next < len(self.bounds) and self.bounds[self._next][1] <= self._ready:
             self._launch()
 
     def finish(self) -> None:
-        if self.world <= 1:
+        if not self._active:
             return
         while self._next < len(self.bounds):
             self._launch()
+        if self.comm is not None:
+            # the optimizer (on the compute stream) runs after every bucket's exchange
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
         for h, buf in self._handles:
             h.wait()   # nccl: the current (compute) stream waits on the RCCL stream
             if self.backend != "nccl":
                 buf.div_(self.world)
         self._handles = []
+        if self._prev_reserve is not None:
+            from ._lib import lib
+            lib().vitmi_gemm_set_reserved_cus(self._prev_reserve)
+            self._prev_reserve = None
 
 
-def attach(model, bucket_mb: float = 64.0, group=None) -> GradReducer:
+def attach(model, bucket_mb: float = 64.0, group=None, comm: Optional[VitmiComm] = None,
+           grad_dtype: str = "fp32", reserve_cus: int = 0) -> GradReducer:
     """Wire a GradReducer to a vitmi VisionTransformer's arena and backward hooks."""
     arena = model.arena()
-    red = GradReducer(arena.grad, bucket_mb, group)
+    red = GradReducer(arena.grad, bucket_mb, group, comm=comm, grad_dtype=grad_dtype, reserve_cus=reserve_cus)
 
     def end_of(params: Sequence[torch.nn.Parameter]) -> int:
         return max(arena.offsets[id(p)] + p.numel() for p in params)
@@ -96,14 +218,17 @@ def _hook(red: GradReducer, end: int) -> Callable:
     return lambda _mod: red.mark_ready(end)
 
 
-def broadcast_parameters(model, src: int = 0, group=None) -> None:
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.broadcast(model.arena().flat, src, group=group)
+def broadcast_parameters(model, src: int = 0, group=None, comm: Optional[VitmiComm] = None) -> None:
+    flat = model.arena().flat
+    if comm is not None:
+        if comm.world > 1:
+            comm.broadcast(flat, src)
+    elif dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.broadcast(flat, src, group=group)
 
 
 def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:
     """torchrun-style bootstrap: returns (rank, world, local_rank)."""
-    import os
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

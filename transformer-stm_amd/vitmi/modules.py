@@ -24,7 +24,6 @@ product is exact fp32 (f32-input MFMA).
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -39,77 +38,6 @@ F32 = torch.float32
 # bf16 copies of dx produced by a backward, keyed by the fp32 tensor's address, so
 # the next backward up the chain does not re-cast its incoming gradient.
 _LP_STASH: Dict[int, Tensor] = {}
-
-
-# Weight-gradient GEMMs and bias column sums have no consumer inside the backward; with
-# VITMI_WGRAD_STREAM=1 they run on a side HIP stream, ordered after their inputs by stream
-# waits, so their launches could fill the CUs that the dgrad chain's under-filled last tile
-# rounds leave idle (ViT N = 768 GEMMs: 591 tiles on 256 CUs).  Measured on MI355X: 1-1.5 %
-# SLOWER (two persistent one-block-per-CU launches delay each other's late blocks), so the
-# default keeps them in line on the compute stream.
-_SIDE: Dict[int, "torch.cuda.Stream"] = {}
-_SIDE_ON = os.environ.get("VITMI_WGRAD_STREAM", "0") == "1"
-
-
-def _side_stream(dev: torch.device):
-    if not _SIDE_ON or dev.type != "cuda":
-        return None
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    s = _SIDE.get(idx)
-    if s is None:
-        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
-    return s
-
-
-class _OnSide:
-    """``with _OnSide(dev, *tensors):`` the kernels launched inside run on the side stream,
-    after everything queued on the current stream so far; the tensors' memory is held until
-    the side stream has consumed it (``record_stream``)."""
-
-    def __init__(self, dev: torch.device, *tensors: Tensor):
-        self.side = _side_stream(dev)
-        self.tensors = tensors
-        self.ctx = None
-
-    def __enter__(self):
-        if self.side is not None:
-            _queue_join(self.side)
-            self.side.wait_stream(torch.cuda.current_stream(self.side.device))
-            self.ctx = torch.cuda.stream(self.side)
-            self.ctx.__enter__()
-        return self
-
-    def __exit__(self, *exc):
-        if self.ctx is not None:
-            self.ctx.__exit__(*exc)
-            for t in self.tensors:
-                t.record_stream(self.side)
-        return False
-
-
-_JOIN_QUEUED: Dict[int, bool] = {}
-
-
-def _queue_join(side) -> None:
-    """Once per backward pass: when autograd finishes, the current stream waits for the side
-    stream, so any graph (not only a whole model) hands back complete parameter grads."""
-    key = id(side)
-    if _JOIN_QUEUED.get(key):
-        return
-    _JOIN_QUEUED[key] = True
-
-    def _cb():
-        _JOIN_QUEUED[key] = False
-        torch.cuda.current_stream(side.device).wait_stream(side)
-
-    torch.autograd.Variable._execution_engine.queue_callback(_cb)
-
-
-def _join_side(dev: torch.device) -> None:
-    """The current stream waits for every side-stream kernel queued so far."""
-    side = _side_stream(dev)
-    if side is not None:
-        torch.cuda.current_stream(side.device).wait_stream(side)
 
 
 def _drop_args(mod: nn.Module, rate: float, site0: int):
@@ -407,14 +335,12 @@ class _BlockFn(torch.autograd.Function):
             seed, rate, site0 = drop
             g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
         # MLP branch
-        dev = g2.device
         # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
         du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias))
-        with _OnSide(dev, g2_lp, act, du, h2):
-            ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
-            if not ctx.bias_done:
-                ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
-            ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
+        ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
+        if not ctx.bias_done:
+            ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
+        ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
         dh2 = ops.linear_dgrad(du, w1, T)
         # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
         if drop is None:
@@ -429,13 +355,11 @@ class _BlockFn(torch.autograd.Function):
             ops.bias_grad(dx1_lp, _grad(a_.proj.bias))
         # attention branch
         do = ops.linear_dgrad(dx1_lp, wo, T)
-        with _OnSide(dev, dx1_lp, o):
-            ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
+        ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
         # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale,
                                  bias_grad=_grad(a_.qkv.bias) if a_.qkv.bias is not None else None)
-        with _OnSide(dev, dqkv, h1):
-            ops.linear_wgrad(dqkv, h1, _grad(a_.qkv.weight))
+        ops.linear_wgrad(dqkv, h1, _grad(a_.qkv.weight))
         dh1 = ops.linear_dgrad(dqkv, wq, T)
         prev = ctx.prev_bias
         dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
@@ -444,8 +368,7 @@ class _BlockFn(torch.autograd.Function):
         _stash(dx, dx_lp)
         hook = getattr(blk, "_grad_ready_hook", None)
         if hook is not None:
-            with _OnSide(dev):   # the bucket all-reduce orders after BOTH streams' grads
-                hook(blk)
+            hook(blk)
         return (dx.view(B, N, D), None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
 
 
@@ -514,14 +437,11 @@ class _EmbedFn(torch.autograd.Function):
         else:
             dtok, dtok_lp = ops.tokens_assemble_bwd(dx, B, np_, T == F32, lpT, dcls, dpos)
             g = dtok_lp if dtok_lp is not None else dtok
-        with _OnSide(dx.device, g, patches):
-            ops.linear_wgrad(g, patches, _grad(emb.proj.weight).view(D, -1))
-            ops.bias_grad(g, _grad(emb.proj.bias))
-            hook = getattr(emb, "_grad_ready_hook", None)
-            if hook is not None:
-                hook(emb)
-        # last backward of the model: the optimizer and the next step see every side grad
-        _join_side(dx.device)
+        ops.linear_wgrad(g, patches, _grad(emb.proj.weight).view(D, -1))
+        ops.bias_grad(g, _grad(emb.proj.bias))
+        hook = getattr(emb, "_grad_ready_hook", None)
+        if hook is not None:
+            hook(emb)
         n_params = len(ctx.needs_input_grad) - 4
         return (None, None, None, None) + (None,) * n_params
 

@@ -7,7 +7,6 @@ fallback — a missing library or a bad shape raises.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -133,10 +132,6 @@ def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = 
     M, N = dy.numel() // dy.shape[-1], dy.shape[-1]
     K = w.shape[1]
     dx = torch.empty(*dy.shape[:-1], K, dtype=out_dtype, device=dy.device)
-    if bias_grad is not None and not _FUSED_BIAS:       # A/B switch: separate column-sum pass
-        dx = linear_dgrad(dy, w, out_dtype, epilogue, aux)
-        bias_grad_(dx, bias_grad)
-        return dx
     if bias_grad is not None:
         assert bias_grad.dtype == torch.float32 and bias_grad.is_contiguous() and bias_grad.numel() == K
         nws = lib().vitmi_linear_dgrad_bias_workspace_size(dt(dy.dtype), M, N, K)
@@ -151,11 +146,6 @@ def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = 
     return dx
 
 
-_FUSED_BIAS = os.environ.get("VITMI_FUSED_BIAS", "1") != "0"          # fc1 bias in the DGELU dgrad
-# qkv bias from the attention backward (q: dQ column sums in the dQ kernel; k: 0 and v: column
-# sums of dO, exact softmax identities).  Measured neutral end to end (the dQ kernel's extra
-# LDS pass costs what the separate column-sum pass over dqkv did), so off by default.
-_FUSED_QKV_BIAS = os.environ.get("VITMI_FUSED_QKV_BIAS", "0") != "0"
 
 
 def bias_grad_(dy: Tensor, db: Tensor) -> None:
@@ -237,6 +227,12 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
 
 
 # ---------------------------------------------------------------- attention
+def attention_set_policy(policy: int) -> int:
+    """0 = auto, 1 = always the streamed kernels, 2 = single-pass fused backward for N <= 256
+    (tests / A-B timing).  Returns the previous policy."""
+    return lib().vitmi_attention_set_policy(int(policy))
+
+
 def attention_fwd(qkv: Tensor, B: int, N: int, H: int, scale: float):
     """qkv [B*N, 3*H*64] -> (o [B*N, H*64], lse fp32 [B*H, N])."""
     D3 = qkv.shape[-1]
@@ -250,13 +246,17 @@ def attention_fwd(qkv: Tensor, B: int, N: int, H: int, scale: float):
 
 
 def attention_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, B: int, N: int, H: int,
-                  scale: float, bias_grad: Optional[Tensor] = None) -> Tensor:
-    """dqkv; ``bias_grad`` (fp32 [3D]) += its column sums (the q/k/v bias gradient), fused into
-    the backward kernels where they allow (vitmi_attention_bwd_bias)."""
+                  scale: float, bias_grad: Optional[Tensor] = None, fused_bias: bool = False) -> Tensor:
+    """dqkv; ``bias_grad`` (fp32 [3D]) += its column sums (the q/k/v bias gradient).
+
+    ``fused_bias=True`` takes the sums out of the backward kernels' registers
+    (vitmi_attention_bwd_bias: q from the dQ kernel, k = 0 and v = column sums of dO by softmax
+    identities); measured neutral end to end against the separate column-sum pass, which is the
+    default."""
     D = o.shape[-1]
     assert do.is_contiguous() and do.dtype == qkv.dtype
     dqkv = torch.empty_like(qkv)
-    if bias_grad is not None and not _FUSED_QKV_BIAS:
+    if bias_grad is not None and not fused_bias:
         dqkv = attention_bwd(qkv, o, do, lse, B, N, H, scale)
         bias_grad_(dqkv, bias_grad)
         return dqkv
@@ -338,6 +338,15 @@ def cast_bf16(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
     if dst is None:
         dst = torch.empty(src.shape, dtype=torch.bfloat16, device=src.device)
     check(lib().vitmi_cast_f32_bf16(src.numel(), _p(src), _p(dst), _s()), "cast")
+    return dst
+
+
+def cast_f32(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
+    """bf16 -> fp32 (vitmi_cast_bf16_f32)."""
+    assert src.dtype == torch.bfloat16 and src.is_contiguous()
+    if dst is None:
+        dst = torch.empty(src.shape, dtype=torch.float32, device=src.device)
+    check(lib().vitmi_cast_bf16_f32(src.numel(), _p(src), _p(dst), _s()), "cast_bf16_f32")
     return dst
 
 

@@ -98,6 +98,9 @@ class Adam:
             check(lib().vitmi_adam_step(p.numel(), ops._p(p), ops._p(p.grad), ops._p(m), ops._p(v), None, alpha,
                                         self.beta_1, self.beta_2, self.epsilon, self.grad_scale, ops._s()),
                   "adam_step")
+            # the kernel wrote through a raw pointer: bump the version counter, so a ParamArena
+            # that owns p (its bf16 operand shadow is keyed on these counters) re-casts it
+            torch.autograd.graph.increment_version(p)
 
     # -- checkpointing (Keras saves the optimizer variables with the model weights)
     def state_dict(self) -> Dict:

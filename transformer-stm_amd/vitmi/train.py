@@ -56,7 +56,9 @@ def fit(model, ds: SLSDataset, epochs: int, batch_size: int = 128, optimizer: Op
         log: Optional[Callable[[str], None]] = None) -> Dict[str, List[float]]:
     """models/CvT(Par).py:458-476.  Returns the Keras-style history (one entry per epoch)."""
     dev = ds.images.device
-    opt = optimizer if optimizer is not None else Adam(list(model.parameters()), learning_rate=learning_rate)
+    # a model with a parameter arena gets the single fused launch (which also refreshes its bf16 shadow)
+    target = model if hasattr(model, "arena") else list(model.parameters())
+    opt = optimizer if optimizer is not None else Adam(target, learning_rate=learning_rate)
     gen = torch.Generator(device=dev).manual_seed(seed)
     hist: Dict[str, List[float]] = {"epoch": [], "loss": [], "mae": [], "lr": [], "seconds": []}
     if validate:
