@@ -58,6 +58,8 @@ struct GemmArgs {
   // gemm256 DGELU epilogue: column sums of the output (the bias gradient of the layer whose
   // input gradient this is), one fp32 row per 128-row half tile: colsum[(2*tm + wm)*N + col]
   float* colsum;
+  int stagger_iters, stagger_mode;   // EXPERIMENT (A/B timing only)
+  unsigned long long* stamps;        // DIAGNOSTIC build only (VITMI_GEMM_STAMPS)
 };
 
 // (tile-row, tile-col) of tile index tl: row-major over the tiles_n tile columns (a persistent
@@ -373,6 +375,10 @@ __device__ __forceinline__ void barrier() {
 constexpr int BM = 256, BN = 256, BK = 64, NWAVES = 8;
 constexpr int HALF = 16384;                 // bytes per half sub-image
 constexpr int STAGE = 4 * HALF;             // A0 A1 B0 B1
+// epilogue staging image per wave: 16 rows x 64 bf16 at a 144-B pitch (36 dwords: the 16 rows
+// of a ds_write_b64 lane group start on distinct even banks, conflict free)
+constexpr int EPI_PITCH = 144;
+constexpr int EPI_SCR = 16 * EPI_PITCH;
 
 // tile line of sub-image line i in half h: A (blocks of 64 per wave-row), B (blocks of 32)
 template <bool IS_A>
@@ -444,8 +450,10 @@ __device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf)
 template <bool AK, bool BKM, int EPI, typename TC>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   using namespace g256;
-  // two DMA stages + the bias of the current and the next tile (fp32, double-buffered)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048];
+  // two DMA stages + the bias of the current and the next tile (fp32, double-buffered) + one
+  // per-wave image of a 16-row group of the output, through which bf16 epilogue stores leave
+  // as whole 128-B lines
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048 + NWAVES * EPI_SCR];
   constexpr int EB = EpiOf<EPI>::base;         // public epilogue (the *_DROP ones extend one)
   constexpr bool DROP = EpiOf<EPI>::drop;
   constexpr bool HAS_BIAS = EB == VITMI_EPI_STORE || EB == VITMI_EPI_BIAS_GELU || EB == VITMI_EPI_RESIDUAL;
@@ -583,6 +591,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 
   int it = jx;
   if (it >= nseq) return;
+  if (g.stagger_iters) {   // EXPERIMENT: desynchronise the blocks' epilogue bursts
+    int d = 0;
+    if (g.stagger_mode == 0) d = (jx & 1) ? g.stagger_iters : 0;
+    else if (g.stagger_mode == 1) d = (jx & 3) * g.stagger_iters / 4;
+    else d = (jx >= nbx / 2) ? g.stagger_iters : 0;
+    for (int i = 0; i < d; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   int tile = unit_at(it);   // work unit (a whole tile, or a K-range of a tail tile)
   int64_t m0, n0;
   int ks0, nku, zs;
@@ -602,7 +617,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   // vector-memory ops the previous unit's epilogue issued (0: none yet).  Those are younger
   // than the half-tiles the first K-step waits for, so its counts may grow by that many.
   int ep_ops = 0;
+#ifdef VITMI_GEMM_STAMPS
+  // [block][iter][wave-half][3]: K-loop start, epilogue start, epilogue end (s_memtime)
+  int st_it = 0;
+  auto stamp = [&](int k) {
+    if (g.stamps && lane == 0 && (wave == 0 || wave == 4) && st_it < 16)
+      g.stamps[((blockIdx.x * 16 + st_it) * 2 + (wave >> 2)) * 4 + k] = __builtin_amdgcn_s_memtime();
+  };
+#else
+  auto stamp = [&](int) {};
+#endif
   for (;;) {
+    stamp(0);
     if constexpr (HAS_BIAS) {
       // bias[n0 .. n0+256) -> LDS by ONE LDS-DMA instruction of wave 0 (64 lanes x 16 B; the
       // range check zero-fills columns >= N and a null bias).  It is older than every DMA the
@@ -625,9 +651,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
       // vmcnt counts of the first step after an epilogue that issued S vector-memory ops:
-      // 8 + S (capped at the counter's 63): S = 32 for store-only and split-partial epilogues,
-      // 64 for GELU (two stores per fragment) and the loading epilogues (loads + stores)
+      // 8 + S (capped at the counter's 63): S = 16 (bf16 store), 32 (GELU, fp32 store, split
+      // partials), 48 (DGELU), 64 (residual / accumulate).  An op issued after the awaited DMA
+      // stays outstanding while it does (in-order completion), so 8 + S is the loosest exact wait.
 #define WAITV(N) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory")
+#define WAITF() do { if (fst >= 55) WAITV(63); else if (fst == 48) WAITV(56); else if (fst == 32) WAITV(40); \
+                     else if (fst == 16) WAITV(24); else WAITV(8); } while (0)
 #define COMPUTE(MH, NH, AS, BS)                                                                 \
       do {                                                                                      \
         barrier();                                                                              \
@@ -648,7 +677,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         RD_B(b0, buf, 0);
         if (h1) {
           issue(a1, b1r, t1, buf ^ 1, 3);
-          if (fst >= 64) WAITV(63); else if (fst) WAITV(40); else WAITV(8);
+          WAITF();
         } else {
           WAITV(0);
         }
@@ -657,7 +686,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         RD_B(b1, buf, 1);
         if (h1) {
           issue(a1, b1r, t1, buf ^ 1, 2);
-          if (fst >= 64) WAITV(63); else if (fst) WAITV(40); else WAITV(8);
+          WAITF();
         } else {
           WAITV(0);
         }
@@ -669,7 +698,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         // P3 (A1,B0): DMA B0(t+2); retire A0(t+1), B0(t+1)
         if (h2) {
           issue(a2, b2r, t2, buf, 1);
-          if (fst >= 64) WAITV(63); else if (fst) WAITV(40); else WAITV(8);
+          WAITF();
         } else {
           WAITV(0);
         }
@@ -677,9 +706,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         buf ^= 1;
       }
 #undef COMPUTE
+#undef WAITF
 #undef WAITV
 #undef MMA4
 
+    stamp(1);
     if ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) {
       // K-range of a tail tile: raw fp32 partial into its [256][256] slab
       const __amdgpu_buffer_rsrc_t rw = make_rsrc(g.tail_ws + (int64_t)(tile - g.t_full) * BM * BN, BM * BN * 4);
@@ -728,8 +759,33 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
                                         f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
       if constexpr (EB == VITMI_EPI_BIAS_GELU)
         ru = make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
-      // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand
-      auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) {
+      // bf16 outputs leave through the wave's LDS image of one 16-row group: each lane holds 4
+      // columns of ONE row per fragment (16 rows x 32 B per store instruction: every store would
+      // touch 16 lines with a quarter of each), so a row group is written to LDS and read back as
+      // row-major 16-B chunks: 2 stores of 8 rows x 128 B, whole lines (epilogue 8.8k -> ~3k
+      // cycles per tile measured with s_memtime stamps on the fc1 shape)
+      [[maybe_unused]] char* scr = smem + 2 * STAGE + 2048 + wave * EPI_SCR;
+      [[maybe_unused]] const int rr = lane >> 3, cc = lane & 7;
+      [[maybe_unused]] const bool ccok = n0 + wn * 64 + cc * 8 < g.N;
+      auto lds_put = [&](int ni, bf16x4 o) { *(bf16x4*)(scr + lr * EPI_PITCH + (ni * 16 + lc4) * 2) = o; };
+      // the image of row group mi -> rows m0 + wm*128 + 16 mi + (0..15) of the buffer `r` (bf16, ld)
+      auto flush = [&](__amdgpu_buffer_rsrc_t r, int64_t ld, int mi) {
+        bf16x8 d[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) d[j] = *(const bf16x8*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint32_t vo = ccok ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr) * ld + wn * 64 + cc * 8) * 2)
+                                   : 0x80000000u;
+          asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
+                       :: "v"(__builtin_bit_cast(u32x4, d[j])), "v"(vo), "s"(r), "s"((int)(mi * 16 * ld * 2))
+                       : "memory");
+        }
+      };
+      // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand.
+      // Returns the fragment of the second output (gelu') for BIAS_GELU.
+      auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) -> bf16x4 {
+        [[maybe_unused]] bf16x4 u;
         f32x4 v = acc[mi][ni] + bv[ni];
         const int soff = mi * rstride;
         [[maybe_unused]] f32x4 df;   // dropout factors of the 4 columns
@@ -742,7 +798,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         if constexpr (EPI == EPI_RESIDUAL_DROP) v = v * df + ldv;
         if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM) v += ldv;
         if constexpr (EB == VITMI_EPI_BIAS_GELU) {
-          bf16x4 u;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float cdf, pdf;
@@ -755,12 +810,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             }
             u[e] = (bf16)gp;
           }
-          const uint32_t uoff = cok[ni] ? (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldaux + wn * 64 + lc4) * 2)
-                                        : 0x80000000u;
-          const int usoff = (int)(mi * 16 * g.ldaux * 2);
-          asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
-                       :: "v"(__builtin_bit_cast(unsigned long long, u)), "v"(uoff), "s"(ru),
-                          "s"(usoff), "i"(ni * 32) : "memory");
         } else if constexpr (EPI == VITMI_EPI_DGELU) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= (float)ldb[e];   // aux = gelu'(u) from the forward
@@ -773,9 +822,22 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           bf16x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-          asm volatile("buffer_store_dwordx2 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
-                       :: "v"(__builtin_bit_cast(unsigned long long, o)), "v"(vb[ni]), "s"(rc),
-                          "s"(soff), "i"(ni * 32) : "memory");
+          lds_put(ni, o);
+        }
+        return u;
+      };
+      // all four column groups of row group mi: C (and gelu') through the LDS image
+      auto emit_row = [&](int mi, const f32x4 (&ldv)[4], const bf16x4 (&ldb)[4]) {
+        [[maybe_unused]] bf16x4 us[4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) us[ni] = emit(mi, ni, ldv[ni], ldb[ni]);
+        if constexpr (CES == 2) {
+          flush(rc, g.ldc, mi);
+          if constexpr (EB == VITMI_EPI_BIAS_GELU) {
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) lds_put(ni, us[ni]);
+            flush(ru, g.ldaux, mi);
+          }
         }
       };
       if constexpr (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM || EPI == VITMI_EPI_DGELU) {
@@ -798,9 +860,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             }
           }
 #pragma unroll
-          for (int h = 0; h < RB; ++h)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) emit(RB * mp + h, ni, ld4[h][ni], ldu[h][ni]);
+          for (int h = 0; h < RB; ++h) emit_row(RB * mp + h, ld4[h], ldu[h]);
         }
         if constexpr (EPI == VITMI_EPI_DGELU) {
           if (g.colsum) {
@@ -829,17 +889,28 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       } else {
         // store-only epilogues go row by row: the 4 column groups of a row (one 128-B line
         // for bf16) leave back to back, so the L2 sees whole lines
+        const f32x4 z4[4] = {};
+        const bf16x4 zb[4] = {};
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) emit(mi, ni, f32x4{0.f, 0.f, 0.f, 0.f}, bf16x4{});
+        for (int mi = 0; mi < 8; ++mi) emit_row(mi, z4, zb);
       }
     }
+    stamp(2);
+#ifdef VITMI_GEMM_STAMPS
+    ++st_it;
+#endif
     tpar ^= 1;
     // the epilogue just issued: 32 stores (store-only, split partials) or 64 ops
-    ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32
-             : (EB == VITMI_EPI_BIAS_GELU || EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ||
-                EPI == VITMI_EPI_DGELU) ? 64 : 32;
+    {
+      // bf16 outputs: 2 stores per row group (+2 for gelu'), DGELU + 32 aux loads; fp32 outputs:
+      // 32 direct stores, + 32 loads for residual / accumulate.  (DGELU's 4 column-sum stores
+      // only make the waits below stricter.)
+      constexpr int CES2 = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EB != VITMI_EPI_ACCUM &&
+                           EB != VITMI_EPI_RESIDUAL;
+      constexpr int EP = CES2 ? (EB == VITMI_EPI_BIAS_GELU ? 32 : EPI == VITMI_EPI_DGELU ? 48 : 16)
+                              : (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ? 64 : 32);
+      ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : EP;
+    }
     if (!has_next) break;
     it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
   }
@@ -935,6 +1006,10 @@ static int g_policy = 0;
 static int g_cus = 256;   // compute units of the current device (set on first use)
 
 static int g_reserved = 0;        // CUs the persistent grid leaves free (vitmi_gemm_set_reserved_cus)
+static int g_stag_iters = 0, g_stag_mode = 0;   // EXPERIMENT
+#ifdef VITMI_GEMM_STAMPS
+static unsigned long long* g_stamps = nullptr;
+#endif
 
 static void init_cus() {
   static bool done = false;
@@ -1045,6 +1120,11 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
         g.ksplit = ks;
         units = g.t_full + ntail * S;
       }
+#ifdef VITMI_GEMM_STAMPS
+      g.stamps = g_stamps;
+#endif
+      g.stagger_iters = g_stag_iters;
+      g.stagger_mode = g_stag_mode;
       hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
       gemm_stat<T, EPI, TC>((const void*)gemm256_kernel<AK, BKM, EPI, TC>, g);
@@ -1226,6 +1306,19 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
 }  // namespace vitmi
 
 using namespace vitmi;
+
+#ifdef VITMI_GEMM_STAMPS
+extern "C" int vitmi_gemm_set_stamps(void* buf) {
+  g_stamps = (unsigned long long*)buf;
+  return 0;
+}
+#endif
+
+extern "C" int vitmi_gemm_experiment(int iters, int mode) {
+  g_stag_iters = iters;
+  g_stag_mode = mode;
+  return 0;
+}
 
 extern "C" int vitmi_gemm_set_reserved_cus(int n) {
   init_cus();
