@@ -357,7 +357,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
 // "Pipelining across barriers", 8-phase template T3/T4/T5).
 // Block ids are remapped so consecutive tiles of one XCD share an A row panel.
 // =============================================================================
-// row groups per load batch of the loading epilogues (bf16 gelu' / fp32 residual+accum)
+// row groups per load batch of the loading epilogues (fp32 residual+accum; DGELU loads all 8)
 #ifndef VITMI_EPI_RB_BF16
 #define VITMI_EPI_RB_BF16 8
 #endif
@@ -845,6 +845,34 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         // loaded operand per wait -- the fragment registers are free here), stored row by row
         // like the store-only epilogues below
         constexpr int RB = EPI == VITMI_EPI_DGELU ? VITMI_EPI_RB_BF16 : VITMI_EPI_RB_F32;
+        if constexpr (EPI == VITMI_EPI_DGELU) {
+          // gelu'(u) arrives as whole 128-B lines too: each lane loads 16 B of one row (8 rows x
+          // 128 B per instruction; a C^T-layout load would take 16 rows x 32 B), the wave writes
+          // the 16-row group to its LDS image and reads it back in the accumulator's layout.
+          // All 16 loads of the tile are issued first (64 VGPRs), the range check zero-fills
+          // rows >= M.
+          const __amdgpu_buffer_rsrc_t rx =
+              make_rsrc((const char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
+          u32x4 al[8][2];
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const uint32_t vo = ccok ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr) * g.ldaux + wn * 64 + cc * 8) * 2)
+                                       : 0x80000000u;
+              al[mi][j] = __builtin_amdgcn_raw_buffer_load_b128(rx, vo, (int)(mi * 16 * g.ldaux * 2), 0);
+            }
+          const f32x4 z4[4] = {};
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) *(u32x4*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16) = al[mi][j];
+            bf16x4 lb[4];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) lb[ni] = *(const bf16x4*)(scr + lr * EPI_PITCH + (ni * 16 + lc4) * 2);
+            emit_row(mi, z4, lb);
+          }
+        } else
 #pragma unroll
         for (int mp = 0; mp < 8 / RB; ++mp) {
           f32x4 ld4[RB][4];
@@ -856,7 +884,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             for (int ni = 0; ni < 4; ++ni) {
               if constexpr (EB == VITMI_EPI_RESIDUAL) ld4[h][ni] = *(const f32x4*)(g.residual + row * g.ldr + colc[ni]);
               if constexpr (EPI == VITMI_EPI_ACCUM) ld4[h][ni] = *(const f32x4*)((const float*)g.C + row * g.ldc + colc[ni]);
-              if constexpr (EPI == VITMI_EPI_DGELU) ldu[h][ni] = *(const bf16x4*)((const bf16*)g.aux + row * g.ldaux + colc[ni]);
             }
           }
 #pragma unroll
@@ -902,13 +929,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     tpar ^= 1;
     // the epilogue just issued: 32 stores (store-only, split partials) or 64 ops
     {
-      // bf16 outputs: 2 stores per row group (+2 for gelu'), DGELU + 32 aux loads; fp32 outputs:
-      // 32 direct stores, + 32 loads for residual / accumulate.  (DGELU's 4 column-sum stores
-      // only make the waits below stricter.)
+      // bf16 outputs: 2 stores per row group (+2 for gelu'); fp32 outputs: 32 direct stores;
+      // + 16 aux loads for DGELU, + 32 loads for residual / accumulate.  (DGELU's 4 column-sum
+      // stores only make the waits below stricter.)
       constexpr int CES2 = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EB != VITMI_EPI_ACCUM &&
                            EB != VITMI_EPI_RESIDUAL;
-      constexpr int EP = CES2 ? (EB == VITMI_EPI_BIAS_GELU ? 32 : EPI == VITMI_EPI_DGELU ? 48 : 16)
-                              : (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ? 64 : 32);
+      constexpr int EP = CES2 ? (EB == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU ? 32 : 16)
+                              : (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ? 64
+                                 : EPI == VITMI_EPI_DGELU ? 48 : 32);
       ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : EP;
     }
     if (!has_next) break;
