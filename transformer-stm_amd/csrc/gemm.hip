@@ -768,8 +768,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       [[maybe_unused]] const int rr = lane >> 3, cc = lane & 7;
       [[maybe_unused]] const bool ccok = n0 + wn * 64 + cc * 8 < g.N;
       auto lds_put = [&](int ni, bf16x4 o) { *(bf16x4*)(scr + lr * EPI_PITCH + (ni * 16 + lc4) * 2) = o; };
+      // Lanes exchange data through the image: a compiler barrier between one lane's LDS write
+      // and another lane's read of it (no store-to-load forwarding or reordering across it; the
+      // LDS executes one wave's accesses in order)
+      auto lane_xchg = [] { asm volatile("" ::: "memory"); };
       // the image of row group mi -> rows m0 + wm*128 + 16 mi + (0..15) of the buffer `r` (bf16, ld)
       auto flush = [&](__amdgpu_buffer_rsrc_t r, int64_t ld, int mi) {
+        lane_xchg();
         bf16x8 d[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) d[j] = *(const bf16x8*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16);
@@ -867,10 +872,72 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) *(u32x4*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16) = al[mi][j];
+            lane_xchg();
             bf16x4 lb[4];
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) lb[ni] = *(const bf16x4*)(scr + lr * EPI_PITCH + (ni * 16 + lc4) * 2);
+            lane_xchg();   // (the image is rewritten by emit_row after every lane's read)
             emit_row(mi, z4, lb);
+          }
+        } else if constexpr (EB == VITMI_EPI_RESIDUAL) {
+          // fp32 residual in, fp32 out, both as whole lines through the LDS image, half a row
+          // group (8 rows x 256 B) at a time: lane (rq, cq) moves 16 B of row 4j + rq, the lanes
+          // holding those rows in the accumulator layout (lr / 8 == half) read, update and write
+          // them back in between.  RB row groups of loads in flight (64 VGPRs).
+          constexpr int P32 = 272;   // 68 dwords: 8 rows fit the 2304-B image
+          const int rq = lane >> 4, cq = lane & 15;
+          const bool cqok = n0 + wn * 64 + cq * 4 < g.N;
+          const __amdgpu_buffer_rsrc_t rres =
+              make_rsrc((const char*)(g.residual + m0 * g.ldr + n0), clamp_bytes(((g.M - m0) * g.ldr - n0) * 4));
+          auto vo32 = [&](int hh, int j, int64_t ld) -> uint32_t {
+            return cqok ? (uint32_t)(((int64_t)(wm * 128 + 8 * hh + 4 * j + rq) * ld + wn * 64 + cq * 4) * 4)
+                        : 0x80000000u;
+          };
+#pragma unroll
+          for (int mp = 0; mp < 8 / RB; ++mp) {
+            u32x4 rl[RB][2][2];
+#pragma unroll
+            for (int h = 0; h < RB; ++h)
+#pragma unroll
+              for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                  rl[h][hh][j] = __builtin_amdgcn_raw_buffer_load_b128(rres, vo32(hh, j, g.ldr),
+                                                                       (int)((RB * mp + h) * 16 * g.ldr * 4), 0);
+#pragma unroll
+            for (int h = 0; h < RB; ++h) {
+              const int mi = RB * mp + h;
+#pragma unroll
+              for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) *(u32x4*)(scr + (4 * j + rq) * P32 + cq * 16) = rl[h][hh][j];
+                lane_xchg();
+                if ((lr >> 3) == hh) {
+#pragma unroll
+                  for (int ni = 0; ni < 4; ++ni) {
+                    f32x4* pr = (f32x4*)(scr + (lr & 7) * P32 + (ni * 16 + lc4) * 4);
+                    f32x4 v = acc[mi][ni] + bv[ni];
+                    if constexpr (DROP) {
+                      const uint32_t rk = drop_row_key(g.drop_seed, g.drop_site, (uint32_t)(m0 + wm * 128 + mi * 16 + lr));
+#pragma unroll
+                      for (int e = 0; e < 4; ++e)
+                        v[e] *= drop_hash(rk, (uint32_t)(colc[ni] + e)) >= g.drop_thresh ? g.drop_scale : 0.f;
+                    }
+                    *pr = v + *pr;
+                  }
+                }
+                lane_xchg();
+                u32x4 d[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) d[j] = *(const u32x4*)(scr + (4 * j + rq) * P32 + cq * 16);
+                lane_xchg();   // every lane's read before the next half rewrites the image
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
+                               :: "v"(d[j]), "v"(vo32(hh, j, g.ldc)), "s"(rc), "s"((int)(mi * 16 * g.ldc * 4))
+                               : "memory");
+              }
+            }
           }
         } else
 #pragma unroll
