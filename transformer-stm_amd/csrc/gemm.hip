@@ -58,7 +58,6 @@ struct GemmArgs {
   // gemm256 DGELU epilogue: column sums of the output (the bias gradient of the layer whose
   // input gradient this is), one fp32 row per 128-row half tile: colsum[(2*tm + wm)*N + col]
   float* colsum;
-  int stagger_iters, stagger_mode;   // EXPERIMENT (A/B timing only)
   unsigned long long* stamps;        // DIAGNOSTIC build only (VITMI_GEMM_STAMPS)
 };
 
@@ -591,13 +590,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 
   int it = jx;
   if (it >= nseq) return;
-  if (g.stagger_iters) {   // EXPERIMENT: desynchronise the blocks' epilogue bursts
-    int d = 0;
-    if (g.stagger_mode == 0) d = (jx & 1) ? g.stagger_iters : 0;
-    else if (g.stagger_mode == 1) d = (jx & 3) * g.stagger_iters / 4;
-    else d = (jx >= nbx / 2) ? g.stagger_iters : 0;
-    for (int i = 0; i < d; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   int tile = unit_at(it);   // work unit (a whole tile, or a K-range of a tail tile)
   int64_t m0, n0;
   int ks0, nku, zs;
@@ -1101,7 +1093,6 @@ static int g_policy = 0;
 static int g_cus = 256;   // compute units of the current device (set on first use)
 
 static int g_reserved = 0;        // CUs the persistent grid leaves free (vitmi_gemm_set_reserved_cus)
-static int g_stag_iters = 0, g_stag_mode = 0;   // EXPERIMENT
 #ifdef VITMI_GEMM_STAMPS
 static unsigned long long* g_stamps = nullptr;
 #endif
@@ -1218,8 +1209,6 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
 #ifdef VITMI_GEMM_STAMPS
       g.stamps = g_stamps;
 #endif
-      g.stagger_iters = g_stag_iters;
-      g.stagger_mode = g_stag_mode;
       hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
       gemm_stat<T, EPI, TC>((const void*)gemm256_kernel<AK, BKM, EPI, TC>, g);
@@ -1408,12 +1397,6 @@ extern "C" int vitmi_gemm_set_stamps(void* buf) {
   return 0;
 }
 #endif
-
-extern "C" int vitmi_gemm_experiment(int iters, int mode) {
-  g_stag_iters = iters;
-  g_stag_mode = mode;
-  return 0;
-}
 
 extern "C" int vitmi_gemm_set_reserved_cus(int n) {
   init_cus();
