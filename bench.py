@@ -128,10 +128,13 @@ def _demangle(names):
     out = {}
     for n in names:
         st = ctypes.c_int(0)
-        r = fn(n.encode(), None, None, ctypes.byref(st))
-        if r and st.value == 0:
-            out[n] = ctypes.string_at(r).decode()
-            free(ctypes.c_void_p(r))
+        # libstdc++'s demangler predates the DF16b (__bf16) mangling: retry it as a vendor type
+        for m in (n, n.replace("DF16b", "u6__bf16")):
+            r = fn(m.encode(), None, None, ctypes.byref(st))
+            if r and st.value == 0:
+                out[n] = ctypes.string_at(r).decode()
+                free(ctypes.c_void_p(r))
+                break
         else:
             out[n] = n
     return out
@@ -181,11 +184,12 @@ def per_kernel_evidence(args, tmp):
         a[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     tot = sum(a[1] for a in agg.values()) * 1e3 / steps
     out = []
+    pretty = _demangle([k for k in agg if k.startswith("_Z")])   # names rocprofv3 left mangled
     for k, (calls, sec) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         ms = sec * 1e3 / steps
         if ms < 0.02:
             continue
-        e = {"name": k[:120], "ms": round(ms, 3), "calls": round(calls / steps, 2),
+        e = {"name": _short(pretty.get(k, k))[:120], "ms": round(ms, 3), "calls": round(calls / steps, 2),
              "avg_us": round(sec / calls * 1e6, 1)}
         w = by_name.get(k)
         if w is not None and w["calls"] == calls:       # the same launches the work table counted

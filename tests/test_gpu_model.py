@@ -23,6 +23,7 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 BF16_VITB_LOGITS = 7e-3      # measured 2.7e-3 (bs 2, default init) / 3.6e-3 (randomised, fwd+bwd)
 BF16_C1_LOGITS = 5e-3        # measured 2.2e-3
 BF16_VITL_LOGITS = 1e-2      # measured 4.9e-3 (ViT-L/16@384, depth 4)
+BF16_GRADS = 1.5e-2          # worst relative grad error measured 6.9e-3 (C1) / 7.5e-3 (ViT-B depth 12)
 
 
 def gpu_step(cfg, params, img, tgt):
@@ -57,7 +58,7 @@ def test_c1_bf16_matches_oracle():
     cfg = config_c1(dtype="bf16")
     params = vit_ref.init_params(cfg, seed=0)
     img, tgt = vit_ref.synthetic_batch(cfg, 8)
-    err, worst = compare(cfg, params, img, tgt, logit_tol=BF16_C1_LOGITS, grad_tol=2e-2, loss_tol=2e-2)
+    err, worst = compare(cfg, params, img, tgt, logit_tol=BF16_C1_LOGITS, grad_tol=BF16_GRADS, loss_tol=2e-2)
     print(f"C1 bf16: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
 
 
@@ -121,7 +122,7 @@ def test_vit_b_bf16_full_depth_fwd_bwd_vs_oracle():
     params = vit_ref.init_params(cfg, seed=0)
     img, tgt = vit_ref.synthetic_batch(cfg, 2)
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    err, worst = compare(cfg, params, img, tgt, logit_tol=BF16_VITB_LOGITS, grad_tol=2e-2, loss_tol=2e-2)
+    err, worst = compare(cfg, params, img, tgt, logit_tol=BF16_VITB_LOGITS, grad_tol=BF16_GRADS, loss_tol=2e-2)
     print(f"ViT-B/16 bf16 depth 12 bs 2: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
 
 
@@ -132,7 +133,7 @@ def test_c2_fp32_fwd_bwd_vs_oracle():
     params = vit_ref.init_params(cfg, seed=1)
     img, tgt = vit_ref.synthetic_batch(cfg, 4, seed=3)
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    err, worst = compare(cfg, params, img, tgt, logit_tol=1e-3, grad_tol=1e-3, loss_tol=1e-5)
+    err, worst = compare(cfg, params, img, tgt, logit_tol=1e-5, grad_tol=1e-4, loss_tol=1e-5)  # measured 5.7e-7 / 6.2e-6
     print(f"ViT-S/16 fp32 bs 4: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
 
 

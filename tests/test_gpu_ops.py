@@ -240,20 +240,22 @@ ATT = [(2, 197, 2), (1, 17, 3), (2, 64, 1), (1, 577, 2), (3, 1, 2), (1, 130, 1),
        (1, 33, 2), (1, 96, 1), (1, 300, 1)]
 
 
-@pytest.fixture(params=["seq", "stream"])
-def attn_path(request):
-    """bf16 N <= 256 runs the whole-sequence kernels; attention policy 1 forces the streamed
-    ones, so both are checked at the same sizes."""
-    prev = ops.attention_set_policy(1 if request.param == "stream" else 0)
-    yield request.param
+# bf16 N <= 256 runs the whole-sequence kernels; attention policy 1 forces the streamed ones, so
+# both are checked at the same sizes (other cases run the streamed / fp32 kernels either way)
+ATT_CASES = [(B, N, H, T, "seq") for T in (BF, torch.float32) for (B, N, H) in ATT] + \
+            [(B, N, H, BF, "stream") for (B, N, H) in ATT if N <= 256]
+
+
+@pytest.fixture
+def attn_policy():
+    prev = ops.attention_set_policy(0)
+    yield lambda path: ops.attention_set_policy(1 if path == "stream" else 0)
     ops.attention_set_policy(prev)
 
 
-@pytest.mark.parametrize("B,N,H", ATT)
-@pytest.mark.parametrize("T", [BF, torch.float32])
-def test_attention_fwd_bwd(B, N, H, T, attn_path):
-    if attn_path == "stream" and (T != BF or N > 256):
-        pytest.skip("same kernels as the default path")
+@pytest.mark.parametrize("B,N,H,T,path", ATT_CASES)
+def test_attention_fwd_bwd(B, N, H, T, path, attn_policy):
+    attn_policy(path)
     D = 64 * H
     scale = 64 ** -0.5
     qkv = rnd(B * N, 3 * D, dtype=T, seed=22)
@@ -324,8 +326,10 @@ def test_attention_bwd_fused_bias(B, N, H, T):
     assert rel(db - 0.25, ref.float().sum(0)) < (3e-3 if T == BF else 1e-5)
 
 
-def test_attention_softmax_spike(attn_path):
+@pytest.mark.parametrize("path", ["seq", "stream"])
+def test_attention_softmax_spike(path, attn_policy):
     """A key row that dominates one query forces the online-softmax rescale branch."""
+    attn_policy(path)
     B, N, H = 1, 197, 1
     qkv = rnd(B * N, 192, seed=24) * 0.5
     qkv[150, 64:128] = qkv[3, 0:64] * 40   # k_150 aligned with q_3 -> huge score at tile 2

@@ -3,14 +3,18 @@
 usage: python tools/prof_summary.py <kernel_stats.csv> [steps]
 """
 import csv
-import re
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import _demangle  # noqa: E402
 
 
 def short(name: str) -> str:
-    m = re.match(r"_ZN5vitmi\d+(\w+?)I", name)
-    if name.startswith("_ZN5vitmi"):
-        return name[:110]
+    if name.startswith("_Z"):       # rocprofv3's demangler gives up on __bf16 (DF16b) templates
+        name = _demangle([name])[name]
+    if name.startswith("void "):
+        name = name[5:]
     return name.split("(")[0][:110]
 
 
