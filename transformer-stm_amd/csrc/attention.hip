@@ -510,6 +510,38 @@ __device__ __forceinline__ void stage_seq(char* lds, __amdgpu_buffer_rsrc_t rs, 
   }
 }
 
+// A wave's 32-row x 64-column output tile in the 32x32 accumulator layout (lane: row =
+// lane & 31; acc[c2][r] = column 32*c2 + acc_row(r, lane >> 5)) leaves as whole 128-B lines:
+// written as bf16 into a per-wave [32][144 B] LDS image, read back 16 B per lane and stored as
+// 8 rows x 128 B per instruction.  Stored straight from the accumulator, every line would be
+// written in eight 16-B pieces by eight instructions (store-issue bound).  Row r goes to byte
+// offset (row0 + r) * ld_bytes of rs; rows past rs's range (>= N) are dropped by the buffer
+// range check.  The compiler barriers keep the cross-lane exchange ordered (each lane reads
+// what other lanes wrote).
+static constexpr int ST_PITCH = 144;
+static constexpr int ST_BYTES = 32 * ST_PITCH;
+__device__ __forceinline__ void store_tile32(char* scr, const f32x16 (&acc)[2], float mul,
+                                             __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int row0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)(acc[c2][4 * g4 + i] * mul);
+      *(bf16x4*)(scr + r * ST_PITCH + (32 * c2 + 8 * g4 + 4 * h) * 2) = v;
+    }
+  asm volatile("" ::: "memory");
+  const int rr = lane >> 3, cc = lane & 7;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32x4 v = *(const u32x4*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)((int64_t)(row0 + 8 * j + rr) * ld_bytes + cc * 16), 0, 0);
+  }
+  asm volatile("" ::: "memory");
+}
+
 // grid B*H, block 64*NW.  Online softmax over key tiles of 64 (a final tile of 32 when NP is
 // an odd multiple of 32); keys >= N exist only in the last tile and are masked there.
 template <int NPMAX>
@@ -607,19 +639,12 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   if (k0 < NP) tile(std::integral_constant<int, 1>{}, std::true_type{}, k0);
 
   const float lt = l + __shfl_xor(l, 32, 64);
-  if (q < N) {
-    const float inv = 1.f / lt;
-    bf16* orow = o + ((int64_t)b * N + q) * D + hd * DH;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * dt + 8 * g4 + 4 * h;
-        store4(orow + d, oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv, oacc[dt][4 * g4 + 2] * inv,
-               oacc[dt][4 * g4 + 3] * inv);
-      }
-    if (h == 0) lse[(int64_t)bh * N + q] = (m + log2f(lt)) * LN2;
-  }
+  if (q < N && h == 0) lse[(int64_t)bh * N + q] = (m + log2f(lt)) * LN2;
+  // O through the (now free) K/V image: every wave must be done reading it
+  __syncthreads();
+  const int64_t ldo = (int64_t)D * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
+  store_tile32(smem + wave * ST_BYTES, oacc, 1.f / lt, ro, ldo, wave * 32, lane);
 }
 
 // Column sums of a [rows][64] fp32 LDS image (row pitch 65 floats: conflict-free row writes and
@@ -647,7 +672,7 @@ __device__ __forceinline__ void lds_colsum64(const float* img, int nw, float* __
 // of the whole sequence in LDS.  Keys >= N need no mask: their K rows are zero in LDS, so
 // their dS (whatever it is) meets a zero row of K in dQ = dS K.
 template <int NPMAX>
-__global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dq_seq_bf16(
+__global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
     float scale, float* __restrict__ colsum) {
@@ -723,16 +748,11 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dq_seq_bf16(
       for (int d2 = 0; d2 < 2; ++d2) dqt[d2] = mfma32(frag_tr(kt, k0 + 16 * s, 32 * d2, lane), sb, dqt[d2]);
     }
   }
-  if (qok) {
-    bf16* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
-#pragma unroll
-    for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * d2 + 8 * g4 + 4 * h;
-        store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale, dqt[d2][4 * g4 + 2] * scale,
-               dqt[d2][4 * g4 + 3] * scale);
-      }
+  // dQ through the (now free) K/V image: every wave must be done reading it
+  __syncthreads();
+  {
+    const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv + (int64_t)b * N * ld + hd * DH, bytes - hd * DH * 2);
+    store_tile32(smem + wave * ST_BYTES, dqt, scale, rdq, ldb, wave * 32, lane);
   }
   if (colsum) {
     // Bias gradients of this (batch, head), from exact identities of softmax attention:
@@ -841,18 +861,15 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
       }
     }
   }
-  if (key < N) {
-    bf16* row = dqkv + ((int64_t)b * N + key) * ld;
-#pragma unroll
-    for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * d2 + 8 * g4 + 4 * h;
-        store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
-               dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
-        store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
-               dvt[d2][4 * g4 + 3]);
-      }
+  // dK, dV through the (now free) Q/dO image: every wave must be done reading it
+  __syncthreads();
+  {
+    const bf16* db = dqkv + (int64_t)b * N * ld;
+    const __amdgpu_buffer_rsrc_t rdk = make_rsrc(db + D + hd * DH, bytes - (D + hd * DH) * 2);
+    const __amdgpu_buffer_rsrc_t rdv = make_rsrc(db + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+    char* scr = smem + wave * ST_BYTES;
+    store_tile32(scr, dkt, scale, rdk, ldb, wave * 32, lane);
+    store_tile32(scr, dvt, 1.f, rdv, ldb, wave * 32, lane);
   }
   (void)colsum;   // the k / v bias gradients come from the dQ kernel (see there)
 }
