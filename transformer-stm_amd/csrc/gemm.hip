@@ -17,6 +17,14 @@
 #include "common.h"
 #include <stdlib.h>
 
+// Opens every inline-asm buffer store that takes SGPR operands (descriptor, soffset): under SGPR
+// pressure hipcc rematerialises such operands with v_readlane right before the statement, and a
+// VALU write of an SGPR needs 5 wait states before a VMEM instruction reads it.  hipcc pads that
+// hazard for its own instructions only, not for the text of an asm statement; without the pad the
+// store reads the stale soffset and lands on another row group (seen on the GELU-dropout and
+// residual epilogues).
+#define VMEM_SGPR_GUARD "s_nop 4\n\t"
+
 namespace vitmi {
 
 template <typename T> struct TT;
@@ -407,17 +415,34 @@ __device__ __forceinline__ void stage_half(char* sub, __amdgpu_buffer_rsrc_t rs,
 }
 }  // namespace g256
 
-// erf with |error| <= 1.5e-7 (Abramowitz-Stegun 7.1.26): one exp, one rcp, 6 FMAs.  Used
-// only where the result is rounded to bf16; the fp32 path keeps erff.
-__device__ __forceinline__ void gelu_fast_parts(float x, float& cdf, float& pdf) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
-  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
-  const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
-                      0.254829592f) * t;
-  const float erfz = 1.0f - poly * e;
-  cdf = 0.5f * (1.0f + (x < 0.f ? -erfz : erfz));
-  pdf = 0.39894228040143268f * e;   // e == exp(-x^2/2)
+// GELU and gelu' of a fragment's four columns, erf by Abramowitz-Stegun 7.1.26 (|error| <=
+// 1.5e-7: one exp, one rcp, 5 FMAs; used only where the result is rounded to bf16, the fp32
+// path keeps erff).  Written on f32x4 so that everything but the rcp / exp / |x| / sign steps
+// issues as packed v_pk_* pairs, the two independent halves of every step alternating (a packed
+// result consumed by the very next instruction costs an s_nop): 14 VALU per element instead of
+// 16 (the fc1 epilogue is VALU-bound; fc1 + GELU 334 -> 328 us).  0.5*erf comes directly from
+// coefficients pre-scaled by 0.5 (exact), the sign by copysign (v_bfi).
+__device__ __forceinline__ void gelu4(f32x4 x, f32x4& a, f32x4& gp) {
+  f32x4 ax, t, e;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ax[i] = fabsf(x[i]);
+  const f32x4 d = ax * (0.3275911f * 0.70710678118654752f) + 1.0f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t[i] = __builtin_amdgcn_rcpf(d[i]);
+  const f32x4 earg = (x * x) * (-0.5f * 1.4426950408889634f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_exp2f(earg[i]);   // exp(-x^2/2)
+  f32x4 p = t * (0.5f * 1.061405429f) + (0.5f * -1.453152027f);
+  p = p * t + (0.5f * 1.421413741f);
+  p = p * t + (0.5f * -0.284496736f);
+  p = p * t + (0.5f * 0.254829592f);
+  p = p * t;
+  f32x4 h = 0.5f - p * e;                                  // 0.5 erf(|x| / sqrt 2)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h[i] = __builtin_copysignf(h[i], x[i]);
+  const f32x4 cdf = h + 0.5f;
+  a = x * cdf;
+  gp = (x * 0.39894228040143268f) * e + cdf;               // Phi(x) + x phi(x)
 }
 
 // Persistent variant: gridDim.x blocks (<= one per CU) walk the tiles; blocks with equal
@@ -711,7 +736,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+          asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
                        :: "v"(acc[mi][ni]), "v"(wbase), "s"(rw), "s"(mi * 16 * BN * 4), "i"(ni * 64) : "memory");
     } else
     // ---- epilogue straight from registers: acc[mi][ni] = C^T tile; lane owns row
@@ -768,16 +793,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       auto flush = [&](__amdgpu_buffer_rsrc_t r, int64_t ld, int mi) {
         lane_xchg();
         bf16x8 d[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) d[j] = *(const bf16x8*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16);
+        uint32_t vo[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const uint32_t vo = ccok ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr) * ld + wn * 64 + cc * 8) * 2)
-                                   : 0x80000000u;
-          asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
-                       :: "v"(__builtin_bit_cast(u32x4, d[j])), "v"(vo), "s"(r), "s"((int)(mi * 16 * ld * 2))
-                       : "memory");
+          d[j] = *(const bf16x8*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16);
+          vo[j] = ccok ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr) * ld + wn * 64 + cc * 8) * 2) : 0x80000000u;
         }
+        asm volatile(VMEM_SGPR_GUARD
+                     "buffer_store_dwordx4 %0, %2, %4, %5 offen\n\t"
+                     "buffer_store_dwordx4 %1, %3, %4, %5 offen\n\ts_nop 1"
+                     :: "v"(__builtin_bit_cast(u32x4, d[0])), "v"(__builtin_bit_cast(u32x4, d[1])), "v"(vo[0]),
+                        "v"(vo[1]), "s"(r), "s"((int)(mi * 16 * ld * 2))
+                     : "memory");
+        lane_xchg();   // and the next writes of the image stay after these reads
       };
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand.
       // Returns the fragment of the second output (gelu') for BIAS_GELU.
@@ -795,25 +823,22 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         if constexpr (EPI == EPI_RESIDUAL_DROP) v = v * df + ldv;
         if constexpr (EPI == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM) v += ldv;
         if constexpr (EB == VITMI_EPI_BIAS_GELU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float cdf, pdf;
-            gelu_fast_parts(v[e], cdf, pdf);
-            float gp = cdf + v[e] * pdf;       // gelu'(x) = Phi(x) + x phi(x), kept for DGELU
-            v[e] = v[e] * cdf;
-            if constexpr (DROP) {              // dropped: a = gelu(u) m/(1-p), aux = gelu'(u) m/(1-p)
-              gp *= df[e];
-              v[e] *= df[e];
-            }
-            u[e] = (bf16)gp;
+          f32x4 a4, g4;                        // gelu(u), gelu'(u) (kept for DGELU)
+          gelu4(v, a4, g4);
+          v = a4;
+          if constexpr (DROP) {                // dropped: a = gelu(u) m/(1-p), aux = gelu'(u) m/(1-p)
+            v *= df;
+            g4 *= df;
           }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[e] = (bf16)g4[e];
         } else if constexpr (EPI == VITMI_EPI_DGELU) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= (float)ldb[e];   // aux = gelu'(u) from the forward
           csum[ni] += v;                                       // rows >= M hold 0 (zero A rows)
         }
         if constexpr (CES == 4) {
-          asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+          asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
                        :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
         } else {
           bf16x4 o;
@@ -925,7 +950,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
                 lane_xchg();   // every lane's read before the next half rewrites the image
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
+                  asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
                                :: "v"(d[j]), "v"(vo32(hh, j, g.ldc)), "s"(rc), "s"((int)(mi * 16 * g.ldc * 4))
                                : "memory");
               }
@@ -968,7 +993,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             const uint32_t cb = lr == 0 ? (uint32_t)((wn * 64 + lc4) * 4) : 0x80000000u;
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
-              asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"
+              asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"
                            :: "v"(csum[ni]), "v"(cok[ni] ? cb : 0x80000000u), "s"(rs), "i"(ni * 64) : "memory");
           }
         }
