@@ -520,6 +520,15 @@ __device__ __forceinline__ void stage_seq(char* lds, __amdgpu_buffer_rsrc_t rs, 
 // what other lanes wrote).
 static constexpr int ST_PITCH = 144;
 static constexpr int ST_BYTES = 32 * ST_PITCH;
+
+// the lane index as an opaque value: the lane-derived addresses of an epilogue are formed where
+// it runs, not hoisted above the main loop to stay live across it (the dQ kernel sits at 128
+// VGPRs, and the hoisted ones pushed a reload into its loop)
+__device__ __forceinline__ int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 __device__ __forceinline__ void store_tile32(char* scr, const f32x16 (&acc)[2], float mul,
                                              __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int row0, int lane) {
   const int r = lane & 31, h = lane >> 5;
@@ -540,6 +549,42 @@ __device__ __forceinline__ void store_tile32(char* scr, const f32x16 (&acc)[2], 
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)((int64_t)(row0 + 8 * j + rr) * ld_bytes + cc * 16), 0, 0);
   }
   asm volatile("" ::: "memory");
+}
+
+// Column sums of the rows < nvalid of the tile store_tile32 just wrote (its LDS image, as the
+// stored bf16 values): each lane adds 4 rows x 8 columns, xor-shuffles fold the 8 row groups,
+// and the block's waves (all of which must call) fold through red[wave][64] in wave order into
+// colpart[0..63] -- a bias-gradient partial without a second pass over the stored matrix, in a
+// fixed summation order.
+__device__ __forceinline__ void tile32_colsum(const char* scr, int row0, int nvalid, float* colpart,
+                                              float (*red)[64], int wave, int nw, int lane) {
+  const int rr = lane >> 3, cc = lane & 7;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (row0 + 8 * j + rr < nvalid) {
+      const bf16x8 b = *(const bf16x8*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += (float)b[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] += __shfl_xor(cs[e], 8, 64);
+    cs[e] += __shfl_xor(cs[e], 16, 64);
+    cs[e] += __shfl_xor(cs[e], 32, 64);
+  }
+  __syncthreads();                       // red is free (an earlier call's fold is done)
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wave][lane * 8 + e] = cs[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+    for (int w = 0; w < nw; ++w) t += red[w][threadIdx.x];
+    colpart[threadIdx.x] = t;
+  }
 }
 
 // grid B*H, block 64*NW.  Online softmax over key tiles of 64 (a final tile of 32 when NP is
@@ -644,28 +689,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   __syncthreads();
   const int64_t ldo = (int64_t)D * 2;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
-  store_tile32(smem + wave * ST_BYTES, oacc, 1.f / lt, ro, ldo, wave * 32, lane);
-}
-
-// Column sums of a [rows][64] fp32 LDS image (row pitch 65 floats: conflict-free row writes and
-// column reads) over its first 32*nw rows, in a fixed order: thread (c = tid % 64, row group
-// rg = tid / 64) sums rows 32rg..32rg+31 of column c, then 64 threads fold the groups.
-// part[c] = mul * sum.  All threads of the block must call it.
-__device__ __forceinline__ void lds_colsum64(const float* img, int nw, float* __restrict__ part, float mul,
-                                             float (*red)[64]) {
-  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  float t = 0.f;
-  if (rg < nw) {
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i) t += img[(rg * 32 + i) * 65 + c];
-  }
-  red[rg][c] = t;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    float u = 0.f;
-    for (int w = 0; w < nw; ++w) u += red[w][threadIdx.x];
-    part[threadIdx.x] = u * mul;
-  }
+  store_tile32(smem + wave * ST_BYTES, oacc, 1.f / lt, ro, ldo, wave * 32, lane_here());
 }
 
 // dQ (+ delta = rowsum(dO * O)): grid B*H, block 64*NW, wave w owns queries 32w..+31, K and V
@@ -748,40 +772,15 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
       for (int d2 = 0; d2 < 2; ++d2) dqt[d2] = mfma32(frag_tr(kt, k0 + 16 * s, 32 * d2, lane), sb, dqt[d2]);
     }
   }
-  // dQ through the (now free) K/V image: every wave must be done reading it
+  // dQ through the (now free) K/V image: every wave must be done reading it.  With colsum,
+  // also this head's q-bias gradient partial colsum[b][hd*64 ..] (column sums of the stored dQ)
   __syncthreads();
-  {
-    const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv + (int64_t)b * N * ld + hd * DH, bytes - hd * DH * 2);
-    store_tile32(smem + wave * ST_BYTES, dqt, scale, rdq, ldb, wave * 32, lane);
-  }
+  const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv + (int64_t)b * N * ld + hd * DH, bytes - hd * DH * 2);
+  const int ln = lane_here();
+  store_tile32(smem + wave * ST_BYTES, dqt, scale, rdq, ldb, wave * 32, ln);
   if (colsum) {
-    // Bias gradients of this (batch, head), from exact identities of softmax attention:
-    //   q: sum_q dQ[q]                          (rows q >= N are 0 here: P = 0 there)
-    //   k: sum_k dK[k] = sum_q (sum_k dS[q][k]) Q[q] = 0, since every row of dS sums to 0
-    //      (softmax is invariant to a shift shared by all keys)
-    //   v: sum_k dV[k] = sum_q (sum_k P[q][k]) dO[q] = sum_q dO[q], since rows of P sum to 1
-    // so the dK/dV kernel needs no reduction (its padded-key lanes would need masking) and
-    // the v part is a column sum of the dO rows this kernel already holds (zero past N).
-    // The rows go through the K/V LDS area (free after the loop), not through shuffles,
-    // which would keep extra registers live.
     __shared__ float red[NPMAX / 32][64];
-    float* img = (float*)smem;   // [NP][65] fp32 <= 2 * NPMAX * 128 bytes
-    float* part = colsum + (int64_t)b * 3 * D + hd * DH;
-    __syncthreads();
-#pragma unroll
-    for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) img[q * 65 + 32 * d2 + acc_row(r, h)] = dqt[d2][r];
-    __syncthreads();
-    lds_colsum64(img, nw, part, scale, red);
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) img[q * 65 + 16 * s + 8 * h + j] = (float)df[s][j];
-    __syncthreads();
-    lds_colsum64(img, nw, part + 2 * D, 1.f, red);
-    if (threadIdx.x < 64) part[D + threadIdx.x] = 0.f;
+    tile32_colsum(smem + wave * ST_BYTES, wave * 32, N, colsum + (int64_t)b * 3 * D + hd * DH, red, wave, nw, ln);
   }
 }
 
@@ -868,10 +867,14 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     const __amdgpu_buffer_rsrc_t rdk = make_rsrc(db + D + hd * DH, bytes - (D + hd * DH) * 2);
     const __amdgpu_buffer_rsrc_t rdv = make_rsrc(db + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
     char* scr = smem + wave * ST_BYTES;
-    store_tile32(scr, dkt, scale, rdk, ldb, wave * 32, lane);
-    store_tile32(scr, dvt, 1.f, rdv, ldb, wave * 32, lane);
-  }
-  (void)colsum;   // the k / v bias gradients come from the dQ kernel (see there)
+    __shared__ float red[NPMAX / 32][64];
+    float* part = colsum + (int64_t)b * 3 * D + hd * DH;   // the k- and v-bias gradient partials
+    const int ln = lane_here();
+    store_tile32(scr, dkt, scale, rdk, ldb, wave * 32, ln);
+    if (colsum) tile32_colsum(scr, wave * 32, N, part + D, red, wave, nw, ln);
+    store_tile32(scr, dvt, 1.f, rdv, ldb, wave * 32, ln);
+    if (colsum) tile32_colsum(scr, wave * 32, N, part + 2 * D, red, wave, nw, ln);
+  }   // the k / v bias gradients come from the dQ kernel (see there)
 }
 
 // ---------------------------------------------- fused single-pass backward (N <= NPMAX)

@@ -246,13 +246,13 @@ def attention_fwd(qkv: Tensor, B: int, N: int, H: int, scale: float):
 
 
 def attention_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, B: int, N: int, H: int,
-                  scale: float, bias_grad: Optional[Tensor] = None, fused_bias: bool = False) -> Tensor:
+                  scale: float, bias_grad: Optional[Tensor] = None, fused_bias: bool = True) -> Tensor:
     """dqkv; ``bias_grad`` (fp32 [3D]) += its column sums (the q/k/v bias gradient).
 
-    ``fused_bias=True`` takes the sums out of the backward kernels' registers
-    (vitmi_attention_bwd_bias: q from the dQ kernel, k = 0 and v = column sums of dO by softmax
-    identities); measured neutral end to end against the separate column-sum pass, which is the
-    default."""
+    ``fused_bias`` (default) forms the sums in the backward kernels from the LDS image each
+    output tile is stored through (vitmi_attention_bwd_bias: one [B][3D] partial row per batch,
+    folded in a fixed order), instead of a second pass over dqkv; ``fused_bias=False`` runs the
+    separate column-sum pass (kernels without the fused sums fall back to it anyway)."""
     D = o.shape[-1]
     assert do.is_contiguous() and do.dtype == qkv.dtype
     dqkv = torch.empty_like(qkv)
