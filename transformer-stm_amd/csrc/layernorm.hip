@@ -153,35 +153,39 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-// out[d] += sum_b part[b][d] for dgamma (rows 0..G-1), dbeta (G..2G-1), colsum(dx) (2G..3G-1).
-// 1024 threads = 16 waves x 64 columns; wave w sums rows w, w+16, ... (fixed order:
-// deterministic), then a 16-way LDS reduction.
+// out[d] += sum_b part[b][d] for dgamma (rows 0..G-1), dbeta (G..2G-1), colsum(dx) (2G..3G-1),
+// in a fixed order (deterministic).
 __global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int G, int D,
                                                         float* __restrict__ dgamma,
                                                         float* __restrict__ dbeta,
                                                         float* __restrict__ dxsum) {
-  __shared__ float red[3][16][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int d = blockIdx.x * 64 + lane;
-  float a = 0.f, b = 0.f, c = 0.f;
+  // block = 16 columns x 64 row groups (48 blocks at D = 768, not 12: the fold is latency-
+  // bound, 13.4 us with 64-column blocks); row group gi sums partials gi, gi+64, ..., then
+  // thread (array, column) adds the 64 group sums in order
+  __shared__ float red[3][64][17];
+  const int c = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  const int d = blockIdx.x * 16 + c;
+  float a = 0.f, b = 0.f, e = 0.f;
   if (d < D) {
-#pragma unroll 4
-    for (int i = w; i < G; i += 16) {
+#pragma unroll 2
+    for (int i = gi; i < G; i += 64) {
       a += part[(int64_t)i * D + d];
       b += part[(int64_t)(G + i) * D + d];
-      if (dxsum) c += part[(int64_t)(2 * G + i) * D + d];
+      if (dxsum) e += part[(int64_t)(2 * G + i) * D + d];
     }
   }
-  red[0][w][lane] = a;
-  red[1][w][lane] = b;
-  red[2][w][lane] = c;
+  red[0][gi][c] = a;
+  red[1][gi][c] = b;
+  red[2][gi][c] = e;
   __syncthreads();
-  if (w < 3 && d < D) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s += red[w][i][lane];
+  if (threadIdx.x < 48) {
+    const int w = threadIdx.x >> 4, c2 = threadIdx.x & 15, d2 = blockIdx.x * 16 + c2;
     float* out = w == 0 ? dgamma : (w == 1 ? dbeta : dxsum);
-    if (out) out[d] += s;
+    if (d2 < D && out) {
+      float sum = 0.f;
+      for (int k = 0; k < 64; ++k) sum += red[w][k][c2];
+      out[d2] += sum;
+    }
   }
 }
 
@@ -288,7 +292,7 @@ extern "C" int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtyp
     default: LNB(8) break;
   }
 #undef LNB
-  hipLaunchKernelGGL(ln_param_reduce, dim3((D + 63) / 64), dim3(1024), 0, s, (const float*)part, G,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((D + 15) / 16), dim3(1024), 0, s, (const float*)part, G,
                      D, dgamma, dbeta, dxsum);
   VITMI_LAUNCH_CHECK("layernorm_bwd");
   return VITMI_OK;
