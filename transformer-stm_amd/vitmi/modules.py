@@ -470,8 +470,15 @@ class _HeadFn(torch.autograd.Function):
                           _grad(head.bias) if head.bias is not None else None)
         dx = torch.zeros_like(x)
         last_fc2_bias = model.blocks[-1].mlp.fc2.bias if len(model.blocks) and model._fc2_bias_fused else None
+        # the last block's GEMMs take dx in the compute dtype: its zero rows are a fill and the
+        # cls rows come from the LN backward (no cast pass over dx)
+        T = ops.torch_dtype(model.cfg.dtype)
+        lp = torch.zeros(x.shape[0] * x.shape[1], x.shape[2], dtype=T, device=x.device) if T != F32 else None
         ops.layernorm_bwd(dy, x[:, 0], mean, rstd, norm.weight, _grad(norm.weight), _grad(norm.bias),
-                          dx=dx[:, 0], dxsum=_grad(last_fc2_bias) if last_fc2_bias is not None else None)
+                          dx=dx[:, 0], dxsum=_grad(last_fc2_bias) if last_fc2_bias is not None else None,
+                          lp_dtype=None if lp is None else T,
+                          dx_lp=None if lp is None else lp.view(x.shape[0], x.shape[1], x.shape[2])[:, 0])
+        _stash(dx, lp)
         hook = getattr(model, "_head_ready_hook", None)
         if hook is not None:
             hook()

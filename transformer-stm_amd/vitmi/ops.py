@@ -204,24 +204,28 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.
 def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
                   dgamma: Optional[Tensor], dbeta: Optional[Tensor], dres: Optional[Tensor] = None,
                   dx: Optional[Tensor] = None, lp_dtype: Optional[torch.dtype] = None,
-                  dxsum: Optional[Tensor] = None):
+                  dxsum: Optional[Tensor] = None, dx_lp: Optional[Tensor] = None):
     """dx = dres + LN'(dy); dgamma/dbeta (fp32) +=; dxsum += column sums of dx.
     Returns (dx fp32, dx_lp or None).
 
-    ``dx`` may be a pre-allocated (possibly row-strided) fp32 destination."""
+    ``dx`` and ``dx_lp`` (the low-precision copy, dtype lp_dtype) may be pre-allocated, possibly
+    row-strided destinations."""
     M, ldy = _rows(dy)
     _, ldx = _rows(x)
     D = x.shape[-1]
     if dx is None:
         dx = torch.empty(M, D, dtype=torch.float32, device=x.device)
     _, lddx = _rows(dx)
-    dx_lp = None
-    if lp_dtype is not None and lp_dtype != torch.float32:
+    lp_ld = D
+    if dx_lp is not None:
+        assert lp_dtype is not None and dx_lp.dtype == lp_dtype
+        lp_ld = _rows(dx_lp)[1]
+    elif lp_dtype is not None and lp_dtype != torch.float32:
         dx_lp = torch.empty(M, D, dtype=lp_dtype, device=x.device)
     ldres = _rows(dres)[1] if dres is not None else 0
     ws = _ws(lib().vitmi_layernorm_bwd_workspace_size(M, D), x)
     check(lib().vitmi_layernorm_bwd(M, D, _p(dy), dt(dy.dtype), ldy, _p(x), ldx, _p(mean), _p(rstd), _p(w),
-                                    _p(dres), ldres, _p(dx), lddx, _p(dx_lp), D, _p(dgamma), _p(dbeta),
+                                    _p(dres), ldres, _p(dx), lddx, _p(dx_lp), lp_ld, _p(dgamma), _p(dbeta),
                                     _p(dxsum), _p(ws), ws.numel(), _s()), "layernorm_bwd")
     return dx, dx_lp
 
