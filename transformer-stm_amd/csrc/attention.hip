@@ -784,97 +784,132 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   }
 }
 
-// dK/dV: grid B*H, block 64*NW, wave w owns keys 32w..+31; Q, dO, lse*log2e and delta of the
-// whole sequence in LDS.  Queries >= N get L2 = +inf -> P = 0, dS = 0.
+// dK/dV, persistent: grid = min(B*H, CUs) workgroups of 64*NW threads, each walking the (batch,
+// head) pairs bh = blockIdx.x, + gridDim.x, ...; wave w owns keys 32w..+31 and holds their K and
+// V rows in registers, the pair's Q and dO images sit in LDS.  At 165 VGPRs a CU holds one such
+// workgroup anyway, so a second LDS buffer costs no occupancy: the next pair's Q | dO DMA is
+// issued right after the pair-start barrier and lands under this pair's loop, and its K/V rows
+// and lse/delta are loaded into registers as soon as the loop is done, under the dK/dV stores
+// (one workgroup per pair left each CU idle during every prologue load).  Queries >= N get
+// L2 = +inf -> P = 0, dS = 0.
 template <int NPMAX>
 __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale,
-    float* __restrict__ colsum) {
-  // one LDS object: [Q | dO] images, then L2[NPMAX], delta[NPMAX]
-  __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128 + 2 * NPMAX * 4];
+    float* __restrict__ colsum, int npairs) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * NPMAX * 128];   // [buffer][Q | dO]
+  __shared__ __attribute__((aligned(16))) float l2s[NPMAX];
+  __shared__ __attribute__((aligned(16))) float dls[NPMAX];
+  __shared__ float red[NPMAX / 32][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6, NP = nw * 32;
-  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
   const int h = lane >> 5;
-  const bf16* base = qkv + (int64_t)b * N * ld;
   const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
   const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
-  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
-  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
-  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
-  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
-  char* qt = smem;
-  char* dt_ = smem + NP * 128;
-  float* l2s = (float*)(smem + 2 * NPMAX * 128);
-  float* dls = l2s + NPMAX;
-  stage_seq(qt, rq, ldb, NP, nw, wave, lane);
-  stage_seq(dt_, rdo, ldo, NP, nw, wave, lane);
-  for (int i = threadIdx.x; i < NP; i += blockDim.x) {
-    const bool ok = i < N;
-    l2s[i] = ok ? lse[(int64_t)bh * N + i] * LOG2E : INFINITY;
-    dls[i] = ok ? delta[(int64_t)bh * N + i] : 0.f;
-  }
   const int key = wave * 32 + (lane & 31);
-  bf16x8 kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = load_row16(rk, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
-    vf[s] = load_row16(rv, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
   const float c2 = scale * LOG2E;
-  f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
-#pragma unroll 1
-  for (int q0 = 0; q0 < NP; q0 += 32) {
-    f32x16 sa = zero16(), dp = zero16();
+  auto stage_pair = [&](int bh, int buf) {
+    const int b = bh / H, hd = bh - b * H;
+    const bf16* base = qkv + (int64_t)b * N * ld;
+    stage_seq(smem[buf], make_rsrc(base + hd * DH, bytes - hd * DH * 2), ldb, NP, nw, wave, lane);
+    stage_seq(smem[buf] + NP * 128, make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2), ldo, NP,
+              nw, wave, lane);
+  };
+  auto load_regs = [&](int bh, bf16x8 (&kf)[4], bf16x8 (&vf)[4], float& ls, float& dv) {
+    const int b = bh / H, hd = bh - b * H;
+    const bf16* base = qkv + (int64_t)b * N * ld;
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
-      dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key]
+      kf[s] = load_row16(rk, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
+      vf[s] = load_row16(rv, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
     }
+    const int i = threadIdx.x;
+    ls = i < N ? lse[(int64_t)bh * N + i] : 0.f;
+    dv = i < N ? delta[(int64_t)bh * N + i] : 0.f;
+  };
+
+  int bh = blockIdx.x;
+  if (bh >= npairs) return;
+  bf16x8 kf[4], vf[4];
+  float ls, dv;
+  stage_pair(bh, 0);
+  load_regs(bh, kf, vf, ls, dv);
+  int buf = 0;
+  bool first = true;
+  for (;;) {
+    // this pair's Q | dO pieces and register loads: everything but the previous pair's dK/dV
+    // stores (8 per wave, + 2 column-sum stores on wave 0), which are younger
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (colsum && wave == 0) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    first = false;
+    if (threadIdx.x < NP) {
+      const int i = threadIdx.x;
+      l2s[i] = i < N ? ls * LOG2E : INFINITY;
+      dls[i] = i < N ? dv : 0.f;
+    }
+    __syncthreads();   // Q | dO and l2s / dls visible; every wave is done with the other buffer
+    const int nbh = bh + gridDim.x;
+    const bool more = nbh < npairs;
+    if (more) stage_pair(nbh, buf ^ 1);
+    const char* qt = smem[buf];
+    const char* dt_ = qt + NP * 128;
+    f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+#pragma unroll 1
+    for (int q0 = 0; q0 < NP; q0 += 32) {
+      f32x16 sa = zero16(), dp = zero16();
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int q4 = q0 + 8 * g4 + 4 * h;   // rows acc_row(4*g4 + i, h) = q4 + i
-      const f32x4 L2 = *(const f32x4*)(l2s + q4);
-      const f32x4 dl = *(const f32x4*)(dls + q4);
+      for (int s = 0; s < 4; ++s) {
+        sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
+        dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key]
+      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = fexp2(fmaf(sa[4 * g4 + i], c2, -L2[i]));
-        sa[4 * g4 + i] = p;
-        dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int q4 = q0 + 8 * g4 + 4 * h;   // rows acc_row(4*g4 + i, h) = q4 + i
+        const f32x4 L2 = *(const f32x4*)(l2s + q4);
+        const f32x4 dl = *(const f32x4*)(dls + q4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = fexp2(fmaf(sa[4 * g4 + i], c2, -L2[i]));
+          sa[4 * g4 + i] = p;
+          dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
+#pragma unroll
+        for (int d2 = 0; d2 < 2; ++d2) {
+          dvt[d2] = mfma32(frag_tr(dt_, q0 + 16 * s, 32 * d2, lane), pb, dvt[d2]);
+          dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
+        }
       }
     }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
-#pragma unroll
-      for (int d2 = 0; d2 < 2; ++d2) {
-        dvt[d2] = mfma32(frag_tr(dt_, q0 + 16 * s, 32 * d2, lane), pb, dvt[d2]);
-        dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
-      }
+    if (more) load_regs(nbh, kf, vf, ls, dv);   // (kf / vf are dead until the next pair)
+    // dK, dV through this pair's (now free) Q | dO image: every wave must be done reading it
+    __syncthreads();
+    {
+      const int b = bh / H, hd = bh - b * H;
+      const bf16* db = dqkv + (int64_t)b * N * ld;
+      const __amdgpu_buffer_rsrc_t rdk = make_rsrc(db + D + hd * DH, bytes - (D + hd * DH) * 2);
+      const __amdgpu_buffer_rsrc_t rdv = make_rsrc(db + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+      char* scr = smem[buf] + wave * ST_BYTES;
+      float* part = colsum + (int64_t)b * 3 * D + hd * DH;   // the k- and v-bias gradient partials
+      const int ln = lane_here();
+      store_tile32(scr, dkt, scale, rdk, ldb, wave * 32, ln);
+      if (colsum) tile32_colsum(scr, wave * 32, N, part + D, red, wave, nw, ln);
+      store_tile32(scr, dvt, 1.f, rdv, ldb, wave * 32, ln);
+      if (colsum) tile32_colsum(scr, wave * 32, N, part + 2 * D, red, wave, nw, ln);
     }
+    if (!more) break;
+    bh = nbh;
+    buf ^= 1;
   }
-  // dK, dV through the (now free) Q/dO image: every wave must be done reading it
-  __syncthreads();
-  {
-    const bf16* db = dqkv + (int64_t)b * N * ld;
-    const __amdgpu_buffer_rsrc_t rdk = make_rsrc(db + D + hd * DH, bytes - (D + hd * DH) * 2);
-    const __amdgpu_buffer_rsrc_t rdv = make_rsrc(db + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
-    char* scr = smem + wave * ST_BYTES;
-    __shared__ float red[NPMAX / 32][64];
-    float* part = colsum + (int64_t)b * 3 * D + hd * DH;   // the k- and v-bias gradient partials
-    const int ln = lane_here();
-    store_tile32(scr, dkt, scale, rdk, ldb, wave * 32, ln);
-    if (colsum) tile32_colsum(scr, wave * 32, N, part + D, red, wave, nw, ln);
-    store_tile32(scr, dvt, 1.f, rdv, ldb, wave * 32, ln);
-    if (colsum) tile32_colsum(scr, wave * 32, N, part + 2 * D, red, wave, nw, ln);
-  }   // the k / v bias gradients come from the dQ kernel (see there)
 }
 
 // ---------------------------------------------- fused single-pass backward (N <= NPMAX)
@@ -1256,6 +1291,19 @@ using namespace vitmi;
 // Kernel policy (vitmi_attention_set_policy; tests / A-B timing): 0 = auto, 1 = always the
 // streamed kernels, 2 = auto with the single-pass fused backward for N <= SEQ_MAX.
 static constexpr int SEQ_MAX = 256;
+
+static int device_cus() {   // compute units of the current device (the persistent dK/dV grid)
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    else
+      cus = 256;
+  }
+  return cus;
+}
 static int g_attn_policy = 0;
 static bool seq_path(int N) { return N <= SEQ_MAX && g_attn_policy != 1; }
 static bool fused_bwd() { return g_attn_policy == 2; }
@@ -1329,8 +1377,10 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     } else {
       hipLaunchKernelGGL(attn_bwd_dq_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
                          (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
-      hipLaunchKernelGGL(attn_bwd_dkv_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
-                         (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum);
+      const int npairs = B * H, cus = device_cus();
+      hipLaunchKernelGGL(attn_bwd_dkv_seq_bf16<SEQ_MAX>, dim3(npairs < cus ? npairs : cus), block, 0, s,
+                         (const bf16*)qkv, (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale,
+                         colsum, npairs);
       if (colsum_done) *colsum_done = colsum != nullptr;
     }
   } else if (dtype == VITMI_BF16) {
