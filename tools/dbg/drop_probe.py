@@ -1,3 +1,6 @@
+"""Probe of the fused GELU-dropout epilogue at the ViT shape: which dropped elements come out
+nonzero, and where (found the SGPR hazard of the asm epilogue stores).
+usage: python tools/dbg/drop_probe.py"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "transformer-stm_amd")); sys.path.insert(0, ROOT)
