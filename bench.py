@@ -44,12 +44,13 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from vitmi import _lib, dp, ops, optim  # noqa: E402
-from vitmi.config import config_c3, config_c5  # noqa: E402
+from vitmi.config import config_c2, config_c3, config_c5  # noqa: E402
 from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
 METRIC = "images/sec fwd+bwd ViT-B/16 224px bs=256/GPU at 1/2/4/8 MI355X; % MFMA roofline"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level table)
 PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md)
+PEAK_FP32_TFLOPS = 157.3    # MI355X fp32 matrix
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle)
@@ -242,10 +243,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c3", "c5"], default="c3",
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3",
                     help="c3: ViT-B/16 224px bs 256/GPU (the headline metric); c5: ViT-L/16 384px bs 64/GPU "
-                         "(BASELINE config 5, N = 577 tokens: a secondary line, not the headline)")
-    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5)")
+                         "(BASELINE config 5, N = 577 tokens); c2: ViT-S/16 224px bs 128 fp32 (BASELINE config "
+                         "2). c2 and c5 are secondary lines, not the headline")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5, "
+                                                             "128 for c2)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm", choices=["vitmi", "torch"], default="vitmi",
                     help="vitmi: the library's RCCL communicator (vitmi_comm_*, side stream + hipEvent gating); "
@@ -273,11 +276,15 @@ def main():
     rank, world, local = dp.init_from_env(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cfg = config_c3() if args.config == "c3" else config_c5()
-    B = args.batch or (256 if args.config == "c3" else 64)
-    model_name = "vit_base_16" if args.config == "c3" else "vit_large_16"
-    metric = METRIC if args.config == "c3" else \
-        "images/sec fwd+bwd ViT-L/16 384px bs=64/GPU MI355X; % MFMA roofline (BASELINE config 5)"
+    cfg = {"c2": config_c2, "c3": config_c3, "c5": config_c5}[args.config]()
+    B = args.batch or {"c2": 128, "c3": 256, "c5": 64}[args.config]
+    model_name = {"c2": "vit_small_16", "c3": "vit_base_16", "c5": "vit_large_16"}[args.config]
+    metric = {"c3": METRIC,
+              "c5": "images/sec fwd+bwd ViT-L/16 384px bs=64/GPU MI355X; % MFMA roofline (BASELINE config 5)",
+              "c2": "images/sec fwd+bwd ViT-S/16 224px bs=128 fp32 MI355X; % fp32 MFMA roofline (BASELINE "
+                    "config 2)"}[args.config]
+    fp32 = cfg.dtype == "fp32"
+    peak = PEAK_FP32_TFLOPS if fp32 else PEAK_BF16_TFLOPS
 
     torch.manual_seed(0)
     model = VisionTransformer(cfg).to(dev)
@@ -367,9 +374,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp32" if fp32 else "bf16",
         "data": "synthetic (torch.rand images in [0,1), randint labels; random-init trunc_normal(.02) weights)",
-        "config": {"workload": f"{'ViT-B/16 224' if args.config == 'c3' else 'ViT-L/16 384'}x"
+        "config": {"workload": f"{ {'c2': 'ViT-S/16 224', 'c3': 'ViT-B/16 224', 'c5': 'ViT-L/16 384'}[args.config]}x"
                                f"{cfg.img_size}x3 fwd + CE loss + bwd"
                                + (f" + {args.grad_dtype} grad all-reduce ({args.comm} RCCL, "
                                   f"{args.bucket_mb:g} MiB buckets)" if world > 1 else "")
@@ -377,14 +384,14 @@ def main():
                    "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
                    "model": model_name, "global_batch": B * world, "seq_len": cfg.seq_len,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd bf16 [{M}x{F_}x{D}] +bias+GELU",
-                     "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+        "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd {'fp32' if fp32 else 'bf16'} [{M}x{F_}x{D}] +bias+GELU",
+                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": None,
                      "launches_timed": len(events), "avg_launch_ms": round(kern_ms, 4),
-                     "algorithmic_bytes": 2 * (M * D + F_ * D) + 2 * 2 * M * F_},
+                     "algorithmic_bytes": (4 if fp32 else 2) * (M * D + F_ * D + 2 * M * F_)},
         "optimizer_ms": (round(sum(a.elapsed_time(b) for a, b in opt_events) / len(opt_events), 3)
                          if opt_events else None),
-        "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (PEAK_BF16_TFLOPS * world), 4),
+        "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (peak * world), 4),
         "loss": round(float(loss.item()), 5),
         "build_id": _lib.lib().vitmi_build_id().decode(),
     }
