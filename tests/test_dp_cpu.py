@@ -59,7 +59,24 @@ def _worker(rank, world, port, q):
         out["arena_order"] = [b for _, b in r2.launch_log]
         dp.broadcast_parameters(m)
         out["param0"] = arena.flat[:8].clone().numpy()
-        # 3) the RCCL id of the vitmi communicator travels through the job's TCPStore
+        # 3) a model without an arena (the CvT regressor's path in train.fit): parameters and
+        #    buffers broadcast from rank 0, then the packed gradients averaged; a parameter
+        #    with no gradient on this rank counts as zero
+        torch.manual_seed(10 + rank)
+        lin = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.BatchNorm1d(5), torch.nn.Linear(5, 3))
+        lin[1].running_mean.fill_(float(rank + 1))
+        dp.broadcast_module(lin)
+        out["lin_w"] = lin[0].weight.detach().clone().numpy()
+        out["bn_mean"] = lin[1].running_mean.clone().numpy()
+        pr = dp.ParamGradReducer(list(lin.parameters()), bucket_mb=64 * 4 / (1 << 20))
+        for i, p in enumerate(lin.parameters()):
+            if not (rank == 1 and i == 0):
+                p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
+        pr.start()
+        pr.finish()
+        out["lin_grads"] = [p.grad.clone().numpy() for p in lin.parameters()]
+        out["lin_buckets"] = len(pr.red.bounds)
+        # 4) the RCCL id of the vitmi communicator travels through the job's TCPStore
         out["uid"] = dp.exchange_unique_id(rank, world)
         q.put((rank, out))
     finally:
@@ -89,4 +106,10 @@ def test_grad_reducer_gloo_world2():
         assert torch.allclose(o["arena_mean"], torch.full_like(o["arena_mean"], 1.5))
         assert o["arena_order"] == sorted(o["arena_order"])    # front-to-back readiness
         assert (res[r]["param0"] == res[0]["param0"]).all()     # broadcast from rank 0
+        assert (res[r]["lin_w"] == res[0]["lin_w"]).all() and (res[r]["bn_mean"] == 1.0).all()
+        assert res[r]["lin_buckets"] > 1
+        for i, g in enumerate(res[r]["lin_grads"]):
+            # rank 0 holds 1*(i+1), rank 1 holds 2*(i+1) (or nothing for parameter 0)
+            want = (i + 1) * (0.5 if i == 0 else 1.5)
+            assert torch.allclose(torch.from_numpy(g), torch.full(g.shape, want)), i
         assert len(res[r]["uid"]) == dp.UID_BYTES and res[r]["uid"] == res[0]["uid"]

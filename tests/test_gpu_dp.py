@@ -12,6 +12,7 @@ to the RCCL path. RCCL itself is exercised by the driver's multi-GPU bench."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -222,3 +223,83 @@ def test_rccl_two_ranks_on_one_gpu_or_skip():
         pytest.skip("RCCL: " + skips[0][:200])
     for r in range(world):
         assert res[r]["same"] and res[r]["val"] == 1.5
+
+
+# ------------------------------------------------------------------ CvT / SLS training (no arena)
+def _cvt_cfg():
+    from vitmi import cvt
+    return cvt.CvTConfig(img_size=64, num_classes=1, proc_dim=5, dtype="fp32",
+                         stages=[cvt.CvTStage(64, 7, 4, 1), cvt.CvTStage(128, 3, 2, 2, with_cls_token=True)])
+
+
+CVT_BS = 11          # 28 training rows -> global batches 11, 11, 6; ranks take 6+5, 6+5, 3+3 rows
+
+
+def _cvt_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vitmi import cvt, optim, sls, train
+        ds = sls.SLSDataset.synthetic(n_pieces=6, image_layers=7, height=64, width=64, device="cuda")
+        model = cvt.CvT(_cvt_cfg()).cuda()
+        model.reset_parameters(1)
+        if rank == 1:                     # fit must start from rank 0's weights
+            with torch.no_grad():
+                for p in model.parameters():
+                    p.mul_(0.5)
+        opt = optim.Adam(list(model.parameters()), learning_rate=1e-3)
+        hist = train.fit(model, ds, epochs=1, batch_size=CVT_BS, optimizer=opt, lr_schedule=None,
+                         seed=4, validate=False)
+        torch.cuda.synchronize()
+        q.put((rank, dict(params={k: p.detach().cpu().numpy() for k, p in model.named_parameters()},
+                          loss=hist["loss"][0], mae=hist["mae"][0], steps=opt.iterations)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_cvt_fit_two_ranks_matches_sharded_emulation():
+    """train.fit with a 2-rank process group (the MirroredStrategy path of models/CvT(Par).py:20-21
+    for the CvT regressor, which has no parameter arena): rank 1's perturbed weights are replaced
+    by rank 0's, each rank trains on its half of every global batch (ragged last batch), and the
+    averaged gradients keep the ranks identical.  The result equals one process that runs the two
+    half-batches itself, weights each half's loss by its share of the global batch, and steps once
+    per global batch; the epoch loss is the mean over all training rows."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cvt_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from vitmi import cvt, optim, sls, train
+    from vitmi.modules import mse_loss
+    ds = sls.SLSDataset.synthetic(n_pieces=6, image_layers=7, height=64, width=64, device="cuda")
+    model = cvt.CvT(_cvt_cfg()).cuda()
+    model.reset_parameters(1)
+    opt = optim.Adam(list(model.parameters()), learning_rate=1e-3)
+    gen = torch.Generator(device="cuda").manual_seed(4)
+    rows = ds.train_rows[torch.randperm(ds.train_rows.numel(), device="cuda", generator=gen)]
+    se, n = 0.0, 0
+    model.train()
+    for lo in range(0, rows.numel(), CVT_BS):
+        idx = rows[lo:lo + CVT_BS]
+        opt.zero_grad()
+        for r in range(world):
+            part = idx[r::world]
+            img, pr, y = (sls.gather_rows(t, part) for t in (ds.images, ds.proc, ds.labels))
+            pred = model(img, pr)
+            (mse_loss(pred, y) * (y.numel() / idx.numel())).backward()
+            se += float(((pred.detach()[:, 0] - y).double() ** 2).sum())
+            n += y.numel()
+        opt.step()
+    assert res[0]["steps"] == res[1]["steps"] == opt.iterations == 3
+    for k, p in model.named_parameters():
+        a, b = res[0]["params"][k], res[1]["params"][k]
+        assert (a == b).all(), k
+        assert np.abs(a - p.detach().cpu().numpy()).max() <= 2e-5, k
+    assert abs(res[0]["loss"] - se / n) <= 1e-6 * max(1.0, se / n)
+    assert res[0]["loss"] == res[1]["loss"] and res[0]["mae"] == res[1]["mae"]

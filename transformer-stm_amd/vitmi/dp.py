@@ -196,6 +196,73 @@ class GradReducer:
             self._prev_reserve = None
 
 
+class ParamGradReducer:
+    """Data parallelism for a model without a parameter arena (the CvT / SLS regressors of
+    models/CvT(Par).py, trained by vitmi.train.fit): after the backward, the parameters'
+    gradients are packed into one persistent flat fp32 buffer (one multi-tensor copy), averaged
+    by the same bucketed GradReducer (RCCL through the vitmi communicator, or the process
+    group), and unpacked.  These models are a few MB of parameters, so the exchange is not
+    overlapped with the backward; the ViT's arena path (attach) is."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], bucket_mb: float = 64.0, group=None,
+                 comm: Optional[VitmiComm] = None):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("ParamGradReducer: no trainable parameters")
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(n, dtype=torch.float32, device=self.params[0].device)
+        self.views: List[torch.Tensor] = []
+        off = 0
+        for p in self.params:
+            self.views.append(self.flat[off:off + p.numel()].view(p.shape))
+            off += p.numel()
+        self.red = GradReducer(self.flat, bucket_mb, group, comm=comm)
+
+    @property
+    def active(self) -> bool:
+        return self.red._active
+
+    def start(self) -> None:
+        """Before the backward (nothing to do: the exchange runs after it)."""
+
+    def finish(self) -> None:
+        self.reduce()
+
+    @torch.no_grad()
+    def reduce(self) -> None:
+        """Replace every parameter's .grad by its mean over ranks (a missing grad counts as 0)."""
+        if not self.active:
+            return
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        torch._foreach_copy_(self.views, [p.grad for p in self.params])
+        self.red.start()
+        self.red.mark_ready(self.flat.numel())
+        self.red.finish()
+        torch._foreach_copy_([p.grad for p in self.params], self.views)
+
+
+def broadcast_module(model: torch.nn.Module, src: int = 0, group=None, comm: Optional[VitmiComm] = None) -> None:
+    """Rank ``src``'s parameters and buffers (BatchNorm moving statistics) to every rank, for a
+    model without a parameter arena."""
+    if comm is not None:
+        if comm.world <= 1:
+            return
+    elif not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            if not t.is_floating_point():
+                continue
+            if comm is not None:
+                buf = t.detach().contiguous().float()
+                comm.broadcast(buf, src)
+                t.copy_(buf)
+            else:
+                dist.broadcast(t.data, src, group=group)
+
+
 def attach(model, bucket_mb: float = 64.0, group=None, comm: Optional[VitmiComm] = None,
            grad_dtype: str = "fp32", reserve_cus: int = 0) -> GradReducer:
     """Wire a GradReducer to a vitmi VisionTransformer's arena and backward hooks."""

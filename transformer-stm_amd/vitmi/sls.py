@@ -255,12 +255,16 @@ class SLSDataset:
         return self.images.shape[0]
 
     def batches(self, rows: Tensor, batch_size: int, shuffle: bool = True,
-                generator: Optional[torch.Generator] = None) -> Iterator[Tuple[Tensor, Tensor, Tensor]]:
-        """Keras fit order: a fresh permutation per epoch (shuffle=True), the last batch partial."""
+                generator: Optional[torch.Generator] = None,
+                shard: Tuple[int, int] = (0, 1)) -> Iterator[Tuple[Tensor, Tensor, Tensor]]:
+        """Keras fit order: a fresh permutation per epoch (shuffle=True), the last batch partial.
+        ``shard=(rank, world)`` yields only this rank's rows ``[rank::world]`` of every global
+        batch (the generator must be seeded alike on every rank, so the permutation agrees)."""
         if shuffle:
             rows = rows[torch.randperm(rows.numel(), device=rows.device, generator=generator)]
+        rank, world = shard
         for lo in range(0, rows.numel(), batch_size):
-            idx = rows[lo:lo + batch_size]
+            idx = rows[lo:lo + batch_size][rank::world]
             yield gather_rows(self.images, idx), gather_rows(self.proc, idx), gather_rows(self.labels, idx)
 
 

@@ -53,9 +53,34 @@ def evaluate(model, ds: SLSDataset, rows: Tensor, batch_size: int = 128) -> Dict
 def fit(model, ds: SLSDataset, epochs: int, batch_size: int = 128, optimizer: Optional[Adam] = None,
         learning_rate: float = 1e-3, lr_schedule: Optional[Callable[[int, float], float]] = keras_step_decay,
         shuffle: bool = True, seed: int = 0, validate: bool = True,
-        log: Optional[Callable[[str], None]] = None) -> Dict[str, List[float]]:
-    """models/CvT(Par).py:458-476.  Returns the Keras-style history (one entry per epoch)."""
+        log: Optional[Callable[[str], None]] = None, group=None, comm=None,
+        dp_bucket_mb: float = 64.0) -> Dict[str, List[float]]:
+    """models/CvT(Par).py:458-476.  Returns the Keras-style history (one entry per epoch).
+
+    Data parallel when the process group (``group``) or the vitmi RCCL communicator (``comm``)
+    spans more than one rank — the reference's MirroredStrategy (models/CvT(Par).py:20-21,
+    old_codes/BayConvT(Par)(Muti).py:16-19): ``batch_size`` stays the GLOBAL batch, every rank
+    takes the rows ``[rank::world]`` of each global batch (same shuffle on every rank), rank 0's
+    weights are broadcast first, and the gradients are averaged before every optimizer step with
+    each rank's loss weighted by its share of the batch, so a ragged last batch still gives the
+    global-batch-mean gradient.  BatchNorm normalises over each rank's rows (per-replica, as
+    under MirroredStrategy).  The epoch metrics are summed over ranks."""
+    from . import dp
     dev = ds.images.device
+    if comm is not None:
+        rank, world = comm.rank, comm.world
+    elif torch.distributed.is_initialized():
+        rank, world = torch.distributed.get_rank(group), torch.distributed.get_world_size(group)
+    else:
+        rank, world = 0, 1
+    red = None
+    if world > 1:
+        if hasattr(model, "arena"):     # the ViT: bucketed exchange overlapped with its backward
+            dp.broadcast_parameters(model, 0, group, comm)
+            red = dp.attach(model, dp_bucket_mb, group, comm)
+        else:
+            dp.broadcast_module(model, 0, group, comm)
+            red = dp.ParamGradReducer(list(model.parameters()), dp_bucket_mb, group, comm)
     # a model with a parameter arena gets the single fused launch (which also refreshes its bf16 shadow)
     target = model if hasattr(model, "arena") else list(model.parameters())
     opt = optimizer if optimizer is not None else Adam(target, learning_rate=learning_rate)
@@ -71,17 +96,32 @@ def fit(model, ds: SLSDataset, epochs: int, batch_size: int = 128, optimizer: Op
         se = torch.zeros((), dtype=torch.float64, device=dev)
         ae = torch.zeros((), dtype=torch.float64, device=dev)
         n = 0
-        for img, proc, y in ds.batches(ds.train_rows, batch_size, shuffle=shuffle, generator=gen):
+        n_train = ds.train_rows.numel()
+        for i, (img, proc, y) in enumerate(ds.batches(ds.train_rows, batch_size, shuffle=shuffle,
+                                                        generator=gen, shard=(rank, world))):
             opt.zero_grad()
-            pred = _predict(model, img, proc)
-            loss = mse_loss(pred, y)
-            loss.backward()
+            if red is not None:
+                red.start()
+            if y.numel():
+                pred = _predict(model, img, proc)
+                loss = mse_loss(pred, y)
+                if red is not None:     # this rank's share of the global batch, x world (averaged below)
+                    loss = loss * (y.numel() * world / min(batch_size, n_train - i * batch_size))
+                loss.backward()
+            if red is not None:
+                red.finish()
             opt.step()
+            if not y.numel():
+                continue
             with torch.no_grad():
                 d = (pred.detach()[:, 0] - y).double()
                 se += (d * d).sum()
                 ae += d.abs().sum()
             n += y.numel()
+        if red is not None:
+            sums = torch.stack([se, ae, torch.tensor(float(n), dtype=torch.float64, device=dev)])
+            sums = _sum_over_ranks(sums, group, comm)
+            se, ae, n = sums[0], sums[1], int(round(sums[2].item()))
         n = max(n, 1)
         hist["epoch"].append(epoch + 1)
         hist["loss"].append(se.item() / n)
@@ -95,6 +135,18 @@ def fit(model, ds: SLSDataset, epochs: int, batch_size: int = 128, optimizer: Op
         if log is not None:
             log(" ".join(f"{k}={hist[k][-1]:.6g}" for k in hist if hist[k]))
     return hist
+
+
+def _sum_over_ranks(v: Tensor, group, comm) -> Tensor:
+    if comm is not None:
+        from .dp import REDUCE_SUM
+        buf = v.float().contiguous()
+        side = torch.cuda.current_stream(buf.device)
+        comm.allreduce_async(buf, side, None, REDUCE_SUM)
+        return buf.double()
+    v = v.clone()
+    torch.distributed.all_reduce(v, group=group)
+    return v
 
 
 def write_history(hist: Dict[str, List[float]], path: str) -> None:
