@@ -235,11 +235,32 @@ def _cvt_cfg():
 CVT_BS = 11          # 28 training rows -> global batches 11, 11, 6; ranks take 6+5, 6+5, 3+3 rows
 
 
+class _SGD:
+    """Plain SGD for the comparison: Adam divides by sqrt(v) and so turns the rounding noise of a
+    gradient that is zero by construction (the key-projection biases, softmax-invariant) into
+    full-size steps; SGD keeps a parameter difference proportional to the gradient difference."""
+
+    def __init__(self, params, lr=0.05):
+        self.params, self.lr, self.iterations = list(params), lr, 0
+
+    def zero_grad(self):
+        for p in self.params:
+            if p.grad is not None:
+                p.grad.zero_()
+
+    @torch.no_grad()
+    def step(self):
+        for p in self.params:
+            if p.grad is not None:
+                p.sub_(p.grad, alpha=self.lr)
+        self.iterations += 1
+
+
 def _cvt_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from vitmi import cvt, optim, sls, train
+        from vitmi import cvt, sls, train
         ds = sls.SLSDataset.synthetic(n_pieces=6, image_layers=7, height=64, width=64, device="cuda")
         model = cvt.CvT(_cvt_cfg()).cuda()
         model.reset_parameters(1)
@@ -247,7 +268,7 @@ def _cvt_worker(rank, world, port, q):
             with torch.no_grad():
                 for p in model.parameters():
                     p.mul_(0.5)
-        opt = optim.Adam(list(model.parameters()), learning_rate=1e-3)
+        opt = _SGD(model.parameters())
         hist = train.fit(model, ds, epochs=1, batch_size=CVT_BS, optimizer=opt, lr_schedule=None,
                          seed=4, validate=False)
         torch.cuda.synchronize()
@@ -275,12 +296,13 @@ def test_cvt_fit_two_ranks_matches_sharded_emulation():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    from vitmi import cvt, optim, sls, train
+    from vitmi import cvt, sls
     from vitmi.modules import mse_loss
     ds = sls.SLSDataset.synthetic(n_pieces=6, image_layers=7, height=64, width=64, device="cuda")
     model = cvt.CvT(_cvt_cfg()).cuda()
     model.reset_parameters(1)
-    opt = optim.Adam(list(model.parameters()), learning_rate=1e-3)
+    p0 = {k: p.detach().clone() for k, p in model.named_parameters()}
+    opt = _SGD(model.parameters())
     gen = torch.Generator(device="cuda").manual_seed(4)
     rows = ds.train_rows[torch.randperm(ds.train_rows.numel(), device="cuda", generator=gen)]
     se, n = 0.0, 0
@@ -300,6 +322,7 @@ def test_cvt_fit_two_ranks_matches_sharded_emulation():
     for k, p in model.named_parameters():
         a, b = res[0]["params"][k], res[1]["params"][k]
         assert (a == b).all(), k
-        assert np.abs(a - p.detach().cpu().numpy()).max() <= 2e-5, k
+        moved = float((p.detach() - p0[k]).abs().max())
+        assert np.abs(a - p.detach().cpu().numpy()).max() <= 1e-6 + 1e-3 * moved, k
     assert abs(res[0]["loss"] - se / n) <= 1e-6 * max(1.0, se / n)
     assert res[0]["loss"] == res[1]["loss"] and res[0]["mae"] == res[1]["mae"]

@@ -1123,134 +1123,160 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_fused_seq_bf16(
 }
 
 // =============================================================== fp32 path (VALU)
-// One thread per query row; K/V chunks of 64 rows staged in LDS (broadcast reads).
+// Exact fp32 (expf, fp32 FMA; the parity configuration).  Four lanes per row, each holding 16
+// of its 64 head dims: a dot product is 16 FMAs in 4 independent chains plus a quad xor-reduce,
+// and a row's state (q / dO / K / V and the accumulators) fits in <= 64 registers, so a SIMD
+// holds several waves.  (One thread per row with 64-float arrays had 1 wave per SIMD and
+// 64-long dependent FMA chains: 2.1 ms per ViT-S dK/dV call.)  K/V (or Q/dO) chunks of 64 rows
+// are staged in LDS; a wave's 16 rows read the same LDS row (4 distinct addresses per read).
 static constexpr int F32_CH = 64;
 
-__global__ __launch_bounds__(64) void attn_fwd_f32(const float* __restrict__ qkv,
-                                                   float* __restrict__ o, float* __restrict__ lse,
-                                                   int N, int H, float scale) {
-  __shared__ float ks[F32_CH][DH], vs[F32_CH][DH];
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  return v;
+}
+// sum_d a[d] * b[d] over one lane's 16 dims (4 chains)
+__device__ __forceinline__ float dot16(const float (&a)[16], const float* __restrict__ b) {
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x4 v = *(const f32x4*)(b + 4 * t);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) c[e] = fmaf(a[4 * t + e], v[e], c[e]);
+  }
+  return (c[0] + c[1]) + (c[2] + c[3]);
+}
+// rows [r0, r0 + 64) of a head's 64 columns (rows >= N zero) -> LDS [64][DH], 256 threads
+__device__ __forceinline__ void stage_chunk_f32(float (*dst)[DH], const float* __restrict__ src, int64_t ld,
+                                                int r0, int N) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int i = threadIdx.x + 256 * t, r = i >> 4, c = (i & 15) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r0 + r < N) v = *(const f32x4*)(src + (int64_t)(r0 + r) * ld + c);
+    *(f32x4*)(&dst[r][c]) = v;
+  }
+}
+
+// grid (ceil(N/64), B*H), 256 threads: row q = 64 * blockIdx.x + tid / 4, dims 16 * (tid % 4) ..
+__global__ __launch_bounds__(256) void attn_fwd_f32(const float* __restrict__ qkv,
+                                                    float* __restrict__ o, float* __restrict__ lse,
+                                                    int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) float ks[F32_CH][DH];
+  __shared__ __attribute__((aligned(16))) float vs[F32_CH][DH];
   const int bh = blockIdx.y, b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D;
   const float* base = qkv + (int64_t)b * N * ld;
-  const int q = blockIdx.x * 64 + threadIdx.x;
-  float qr[DH], acc[DH];
+  const int q = blockIdx.x * 64 + (threadIdx.x >> 2), d0 = (threadIdx.x & 3) * 16;
   const bool ok = q < N;
+  float qr[16], acc[16];
 #pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    qr[d] = ok ? base[(int64_t)q * ld + hd * DH + d] * scale : 0.f;
+  for (int d = 0; d < 16; ++d) {
+    qr[d] = ok ? base[(int64_t)q * ld + hd * DH + d0 + d] * scale : 0.f;
     acc[d] = 0.f;
   }
   float m = -INFINITY, l = 0.f;
   for (int k0 = 0; k0 < N; k0 += F32_CH) {
     __syncthreads();
-    for (int i = threadIdx.x; i < F32_CH * DH; i += 64) {
-      const int r = i / DH, d = i % DH, key = k0 + r;
-      ks[r][d] = key < N ? base[(int64_t)key * ld + D + hd * DH + d] : 0.f;
-      vs[r][d] = key < N ? base[(int64_t)key * ld + 2 * D + hd * DH + d] : 0.f;
-    }
+    stage_chunk_f32(ks, base + D + hd * DH, ld, k0, N);
+    stage_chunk_f32(vs, base + 2 * D + hd * DH, ld, k0, N);
     __syncthreads();
     const int kn = min(F32_CH, N - k0);
     for (int r = 0; r < kn; ++r) {
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) s += qr[d] * ks[r][d];
+      const float s = quad_sum(dot16(qr, &ks[r][d0]));
       const float mn = fmaxf(m, s);
       const float a = expf(m - mn), p = expf(s - mn);
       l = l * a + p;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) acc[d] = acc[d] * a + p * vs[r][d];
+      for (int d = 0; d < 16; ++d) acc[d] = acc[d] * a + p * vs[r][d0 + d];
       m = mn;
     }
   }
   if (!ok) return;
   const float inv = 1.f / l;
-  float* orow = o + ((int64_t)b * N + q) * D + hd * DH;
+  float* orow = o + ((int64_t)b * N + q) * D + hd * DH + d0;
 #pragma unroll
-  for (int d = 0; d < DH; ++d) orow[d] = acc[d] * inv;
-  lse[(int64_t)bh * N + q] = m + logf(l);
+  for (int t = 0; t < 4; ++t)
+    *(f32x4*)(orow + 4 * t) = f32x4{acc[4 * t] * inv, acc[4 * t + 1] * inv, acc[4 * t + 2] * inv, acc[4 * t + 3] * inv};
+  if ((threadIdx.x & 3) == 0) lse[(int64_t)bh * N + q] = m + logf(l);
 }
 
-// dQ (thread per query) — dq = scale * sum_k P (dP - delta) K
-__global__ __launch_bounds__(64) void attn_bwd_dq_f32(const float* __restrict__ qkv,
-                                                      const float* __restrict__ dout,
-                                                      const float* __restrict__ lse,
-                                                      const float* __restrict__ delta,
-                                                      float* __restrict__ dqkv, int N, int H,
-                                                      float scale) {
-  __shared__ float ks[F32_CH][DH], vs[F32_CH][DH];
+// dQ (row = query) -- dq = scale * sum_k P (dP - delta) K
+__global__ __launch_bounds__(256) void attn_bwd_dq_f32(const float* __restrict__ qkv,
+                                                       const float* __restrict__ dout,
+                                                       const float* __restrict__ lse,
+                                                       const float* __restrict__ delta,
+                                                       float* __restrict__ dqkv, int N, int H,
+                                                       float scale) {
+  __shared__ __attribute__((aligned(16))) float ks[F32_CH][DH];
+  __shared__ __attribute__((aligned(16))) float vs[F32_CH][DH];
   const int bh = blockIdx.y, b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D;
   const float* base = qkv + (int64_t)b * N * ld;
-  const int q = blockIdx.x * 64 + threadIdx.x;
+  const int q = blockIdx.x * 64 + (threadIdx.x >> 2), d0 = (threadIdx.x & 3) * 16;
   const bool ok = q < N;
-  float qr[DH], dor[DH], acc[DH];
+  float qr[16], dor[16], acc[16];
 #pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    qr[d] = ok ? base[(int64_t)q * ld + hd * DH + d] * scale : 0.f;
-    dor[d] = ok ? dout[((int64_t)b * N + q) * D + hd * DH + d] : 0.f;
+  for (int d = 0; d < 16; ++d) {
+    qr[d] = ok ? base[(int64_t)q * ld + hd * DH + d0 + d] * scale : 0.f;
+    dor[d] = ok ? dout[((int64_t)b * N + q) * D + hd * DH + d0 + d] : 0.f;
     acc[d] = 0.f;
   }
   const float L = ok ? lse[(int64_t)bh * N + q] : 0.f;
   const float dl = ok ? delta[(int64_t)bh * N + q] : 0.f;
   for (int k0 = 0; k0 < N; k0 += F32_CH) {
     __syncthreads();
-    for (int i = threadIdx.x; i < F32_CH * DH; i += 64) {
-      const int r = i / DH, d = i % DH, key = k0 + r;
-      ks[r][d] = key < N ? base[(int64_t)key * ld + D + hd * DH + d] : 0.f;
-      vs[r][d] = key < N ? base[(int64_t)key * ld + 2 * D + hd * DH + d] : 0.f;
-    }
+    stage_chunk_f32(ks, base + D + hd * DH, ld, k0, N);
+    stage_chunk_f32(vs, base + 2 * D + hd * DH, ld, k0, N);
     __syncthreads();
     const int kn = min(F32_CH, N - k0);
     for (int r = 0; r < kn; ++r) {
-      float s = 0.f, dp = 0.f;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        s += qr[d] * ks[r][d];
-        dp += dor[d] * vs[r][d];
-      }
+      const float s = quad_sum(dot16(qr, &ks[r][d0]));
+      const float dp = quad_sum(dot16(dor, &vs[r][d0]));
       const float ds = expf(s - L) * (dp - dl);
 #pragma unroll
-      for (int d = 0; d < DH; ++d) acc[d] += ds * ks[r][d];
+      for (int d = 0; d < 16; ++d) acc[d] += ds * ks[r][d0 + d];
     }
   }
   if (!ok) return;
-  float* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
+  float* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH + d0;
 #pragma unroll
-  for (int d = 0; d < DH; ++d) row[d] = acc[d] * scale;
+  for (int t = 0; t < 4; ++t)
+    *(f32x4*)(row + 4 * t) = f32x4{acc[4 * t] * scale, acc[4 * t + 1] * scale, acc[4 * t + 2] * scale,
+                                   acc[4 * t + 3] * scale};
 }
 
-// dK, dV (thread per key) — dv = sum_q P dO, dk = scale * sum_q P (dP - delta) Q
-__global__ __launch_bounds__(64) void attn_bwd_dkv_f32(const float* __restrict__ qkv,
-                                                       const float* __restrict__ dout,
-                                                       const float* __restrict__ lse,
-                                                       const float* __restrict__ delta,
-                                                       float* __restrict__ dqkv, int N, int H,
-                                                       float scale) {
-  __shared__ float qs[F32_CH][DH], ds_[F32_CH][DH], ls[F32_CH], dls[F32_CH];
+// dK, dV (row = key) -- dv = sum_q P dO, dk = scale * sum_q P (dP - delta) Q
+__global__ __launch_bounds__(256) void attn_bwd_dkv_f32(const float* __restrict__ qkv,
+                                                        const float* __restrict__ dout,
+                                                        const float* __restrict__ lse,
+                                                        const float* __restrict__ delta,
+                                                        float* __restrict__ dqkv, int N, int H,
+                                                        float scale) {
+  __shared__ __attribute__((aligned(16))) float qs[F32_CH][DH];
+  __shared__ __attribute__((aligned(16))) float ds_[F32_CH][DH];
+  __shared__ float ls[F32_CH], dls[F32_CH];
   const int bh = blockIdx.y, b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D;
   const float* base = qkv + (int64_t)b * N * ld;
-  const int key = blockIdx.x * 64 + threadIdx.x;
+  const int key = blockIdx.x * 64 + (threadIdx.x >> 2), d0 = (threadIdx.x & 3) * 16;
   const bool ok = key < N;
-  float kr[DH], vr[DH], dk[DH], dv[DH];
+  float kr[16], vr[16], dk[16], dv[16];
 #pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    kr[d] = ok ? base[(int64_t)key * ld + D + hd * DH + d] * scale : 0.f;
-    vr[d] = ok ? base[(int64_t)key * ld + 2 * D + hd * DH + d] : 0.f;
+  for (int d = 0; d < 16; ++d) {
+    kr[d] = ok ? base[(int64_t)key * ld + D + hd * DH + d0 + d] * scale : 0.f;
+    vr[d] = ok ? base[(int64_t)key * ld + 2 * D + hd * DH + d0 + d] : 0.f;
     dk[d] = 0.f;
     dv[d] = 0.f;
   }
   for (int q0 = 0; q0 < N; q0 += F32_CH) {
     __syncthreads();
-    for (int i = threadIdx.x; i < F32_CH * DH; i += 64) {
-      const int r = i / DH, d = i % DH, q = q0 + r;
-      qs[r][d] = q < N ? base[(int64_t)q * ld + hd * DH + d] : 0.f;
-      ds_[r][d] = q < N ? dout[((int64_t)b * N + q) * D + hd * DH + d] : 0.f;
-    }
+    stage_chunk_f32(qs, base + hd * DH, ld, q0, N);
+    stage_chunk_f32(ds_, dout + (int64_t)b * N * D + hd * DH, D, q0, N);
     if (threadIdx.x < F32_CH) {
       const int q = q0 + threadIdx.x;
       ls[threadIdx.x] = q < N ? lse[(int64_t)bh * N + q] : 0.f;
@@ -1259,27 +1285,40 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_f32(const float* __restrict__
     __syncthreads();
     const int qn = min(F32_CH, N - q0);
     for (int r = 0; r < qn; ++r) {
-      float s = 0.f, dp = 0.f;
+      float qv[16], dov[16];
 #pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        s += kr[d] * qs[r][d];
-        dp += vr[d] * ds_[r][d];
+      for (int t = 0; t < 4; ++t) {
+        const f32x4 a = *(const f32x4*)(&qs[r][d0 + 4 * t]), c = *(const f32x4*)(&ds_[r][d0 + 4 * t]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          qv[4 * t + e] = a[e];
+          dov[4 * t + e] = c[e];
+        }
       }
+      float cs[4] = {0.f, 0.f, 0.f, 0.f}, cp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        cs[d & 3] = fmaf(kr[d], qv[d], cs[d & 3]);
+        cp[d & 3] = fmaf(vr[d], dov[d], cp[d & 3]);
+      }
+      const float s = quad_sum((cs[0] + cs[1]) + (cs[2] + cs[3]));
+      const float dp = quad_sum((cp[0] + cp[1]) + (cp[2] + cp[3]));
       const float p = expf(s - ls[r]);
       const float dsv = p * (dp - dls[r]);
 #pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        dv[d] += p * ds_[r][d];
-        dk[d] += dsv * qs[r][d];
+      for (int d = 0; d < 16; ++d) {
+        dv[d] = fmaf(p, dov[d], dv[d]);
+        dk[d] = fmaf(dsv, qv[d], dk[d]);
       }
     }
   }
   if (!ok) return;
-  float* row = dqkv + ((int64_t)b * N + key) * ld;
+  float* row = dqkv + ((int64_t)b * N + key) * ld + hd * DH + d0;
 #pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    row[D + hd * DH + d] = dk[d] * scale;
-    row[2 * D + hd * DH + d] = dv[d];
+  for (int t = 0; t < 4; ++t) {
+    *(f32x4*)(row + D + 4 * t) = f32x4{dk[4 * t] * scale, dk[4 * t + 1] * scale, dk[4 * t + 2] * scale,
+                                       dk[4 * t + 3] * scale};
+    *(f32x4*)(row + 2 * D + 4 * t) = f32x4{dv[4 * t], dv[4 * t + 1], dv[4 * t + 2], dv[4 * t + 3]};
   }
 }
 
@@ -1338,7 +1377,7 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
     hipLaunchKernelGGL(attn_fwd_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (bf16*)o, lse, N, H, scale);
   } else {
     dim3 grid((N + 63) / 64, B * H);
-    hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(64), 0, s, (const float*)qkv, (float*)o, lse, N, H, scale);
+    hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(256), 0, s, (const float*)qkv, (float*)o, lse, N, H, scale);
   }
   VITMI_LAUNCH_CHECK("attention_fwd");
   {
@@ -1394,9 +1433,9 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     hipLaunchKernelGGL(attn_bwd_delta<float>, dim3(blocks), dim3(256), 0, s, (const float*)o,
                        (const float*)dout, delta, B * N, N, H);
     dim3 grid((N + 63) / 64, B * H);
-    hipLaunchKernelGGL(attn_bwd_dkv_f32, grid, dim3(64), 0, s, (const float*)qkv, (const float*)dout,
+    hipLaunchKernelGGL(attn_bwd_dkv_f32, grid, dim3(256), 0, s, (const float*)qkv, (const float*)dout,
                        lse, (const float*)delta, (float*)dqkv, N, H, scale);
-    hipLaunchKernelGGL(attn_bwd_dq_f32, grid, dim3(64), 0, s, (const float*)qkv, (const float*)dout,
+    hipLaunchKernelGGL(attn_bwd_dq_f32, grid, dim3(256), 0, s, (const float*)qkv, (const float*)dout,
                        lse, (const float*)delta, (float*)dqkv, N, H, scale);
   }
   VITMI_LAUNCH_CHECK("attention_bwd");
