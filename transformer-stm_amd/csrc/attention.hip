@@ -1122,8 +1122,277 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_fused_seq_bf16(
   }
 }
 
-// =============================================================== fp32 path (VALU)
-// Exact fp32 (expf, fp32 FMA; the parity configuration).  Four lanes per row, each holding 16
+// =============================================================== fp32 path (MFMA, N <= NPMAX)
+// The fp32 parity configuration on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: full fp32
+// products and sums, no reduced-precision operand), with the whole-sequence structure of the
+// bf16 kernels: wave w owns 32 rows (queries, or keys in dK/dV), the other operand's sequence
+// sits in LDS as fp32 [NP][FP] images.  A 32x32x2 step consumes d = 32h + t on lane half h
+// (any pairing of d with steps is a valid reduction order as long as both operands use it), so
+// a lane's register row is 32 contiguous floats and the LDS operand is one ds_read_b128 per four
+// steps.  The P.V-type products take P (or dS) straight from the accumulator registers: step r
+// pairs the two rows acc_row(r, 0/1) the lane halves hold, and reads the matching LDS rows as
+// the A operand (ds_read_b32, 32 consecutive floats per half).  exp is expf (natural) as in the
+// VALU kernels; lse is natural-log.
+static constexpr int FP = 68;   // image pitch in floats: 16 rows of a b128 read land 16 B apart mod 256 B
+
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// rows [0, NP) of one head's 64 columns (rows >= N zero) -> LDS image [NP][FP]; the block has
+// 64 * NP / 32 = 2 NP threads, so each moves 8 of the NP * 16 float4 pieces
+__device__ __forceinline__ void stage_seq_f32(float* img, const float* __restrict__ src, int64_t ld, int N) {
+  const int nt = blockDim.x;
+  f32x4 v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int i = threadIdx.x + t * nt, r = i >> 4, c = (i & 15) * 4;
+    v[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (r < N) v[t] = *(const f32x4*)(src + (int64_t)r * ld + c);
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int i = threadIdx.x + t * nt, r = i >> 4, c = (i & 15) * 4;
+    *(f32x4*)(img + r * FP + c) = v[t];
+  }
+}
+
+// the lane's half-row of a head: x[32h + t], t < 32 (zero when the row is >= N), times mul
+__device__ __forceinline__ void load_half_row(float (&x)[32], const float* __restrict__ row, bool ok, int h,
+                                              float mul) {
+#pragma unroll
+  for (int t = 0; t < 32; t += 4) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (ok) v = *(const f32x4*)(row + 32 * h + t);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[t + e] = v[e] * mul;
+  }
+}
+
+// acc[i][j] += sum_d img[rb + i][d] * x_j[d], with lane j's register half-row x (d = 32h + t)
+__device__ __forceinline__ f32x16 sblock_f32(const float* img, int rb, const float (&x)[32], int lane, f32x16 acc) {
+  const float* row = img + (rb + (lane & 31)) * FP + 32 * (lane >> 5);
+#pragma unroll
+  for (int t = 0; t < 32; t += 4) {
+    const f32x4 a = *(const f32x4*)(row + t);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = mfma_f32(a[e], x[t + e], acc);
+  }
+  return acc;
+}
+
+// acc[dt][d][j] += sum_i img[rb + i][32 dt + d] * w[i][j], w = a 32x32 accumulator (row i = acc_row)
+__device__ __forceinline__ void pvblock_f32(const float* img, int rb, const f32x16& w, int lane, f32x16 (&acc)[2]) {
+  const float* base = img + rb * FP + (lane & 31);
+  const int h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float* row = base + acc_row(r, h) * FP;
+    acc[0] = mfma_f32(row[0], w[r], acc[0]);
+    acc[1] = mfma_f32(row[32], w[r], acc[1]);
+  }
+}
+
+// a wave's transposed 32 x 64 result (acc[dt]: lane j holds column j's d = 32 dt + acc_row(r, h))
+// times mul -> rows row0 + j of dst (ld floats, rows >= N skipped), through the wave's LDS
+// scratch [32][FP] so each row leaves as one 256-B line
+__device__ __forceinline__ void store_tile32_f32(float* scr, const f32x16 (&acc)[2], float mul, float* dst, int64_t ld,
+                                                 int row0, int N, int lane) {
+  const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *(f32x4*)(scr + j * FP + 32 * dt + 8 * g + 4 * h) =
+          f32x4{acc[dt][4 * g] * mul, acc[dt][4 * g + 1] * mul, acc[dt][4 * g + 2] * mul, acc[dt][4 * g + 3] * mul};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int c = (lane & 15) * 4;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int r = 4 * it + (lane >> 4);
+    const f32x4 v = *(const f32x4*)(scr + r * FP + c);
+    if (row0 + r < N) *(f32x4*)(dst + (int64_t)(row0 + r) * ld + c) = v;
+  }
+}
+
+// grid B*H, block 64*NW (NW = ceil(N/32)); online softmax over key blocks of 32, keys >= N
+// (only in the last block) masked
+template <int NPMAX>
+__global__ __launch_bounds__(NPMAX * 2) void attn_fwd_seq_f32(const float* __restrict__ qkv, float* __restrict__ o,
+                                                              float* __restrict__ lse, int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * NPMAX * FP];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NP = (blockDim.x >> 6) * 32;
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = qkv + (int64_t)b * N * ld;
+  float* kt = smem;
+  float* vt = smem + NP * FP;
+  const int h = lane >> 5, q = wave * 32 + (lane & 31);
+  stage_seq_f32(kt, base + D + hd * DH, ld, N);
+  stage_seq_f32(vt, base + 2 * D + hd * DH, ld, N);
+  float qr[32];
+  load_half_row(qr, base + (int64_t)q * ld + hd * DH, q < N, h, scale);
+  __syncthreads();
+
+  float m = -INFINITY, l = 0.f;
+  f32x16 oacc[2] = {zero16(), zero16()};
+#pragma unroll 1
+  for (int kb = 0; kb < NP; kb += 32) {
+    f32x16 st = sblock_f32(kt, kb, qr, lane, zero16());   // S^T[key][q]
+    if (kb + 32 > N) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kb + acc_row(r, h) >= N) st[r] = -INFINITY;
+    }
+    float tmax = st[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, st[r]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);                 // finite: every block holds a key < N
+    const float alpha = expf(m - mn);                // 0 on the first block
+    m = mn;
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = expf(st[r] - mn);
+      st[r] = p;
+      rs += p;
+    }
+    l = fmaf(l, alpha, rs);
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
+    }
+    pvblock_f32(vt, kb, st, lane, oacc);             // O^T[d][q] += V^T[d][key] P^T[key][q]
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (q < N && h == 0) lse[(int64_t)bh * N + q] = m + logf(lt);
+  __syncthreads();   // the K/V images are free: per-wave output scratch
+  store_tile32_f32(smem + wave * 32 * FP, oacc, 1.f / lt, o + (int64_t)b * N * D + hd * DH, D, wave * 32, N, lane);
+}
+
+// dQ (+ delta = rowsum(dO * O)): grid B*H, block 64*NW, K and V images in LDS.  Keys >= N have
+// zero K and V rows: their dS meets a zero K row in dQ = dS K.
+template <int NPMAX>
+__global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dq_seq_f32(const float* __restrict__ qkv,
+                                                                 const float* __restrict__ o,
+                                                                 const float* __restrict__ dout,
+                                                                 const float* __restrict__ lse,
+                                                                 float* __restrict__ delta, float* __restrict__ dqkv,
+                                                                 int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * NPMAX * FP];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NP = (blockDim.x >> 6) * 32;
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = qkv + (int64_t)b * N * ld;
+  float* kt = smem;
+  float* vt = smem + NP * FP;
+  const int h = lane >> 5, q = wave * 32 + (lane & 31);
+  const bool qok = q < N;
+  stage_seq_f32(kt, base + D + hd * DH, ld, N);
+  stage_seq_f32(vt, base + 2 * D + hd * DH, ld, N);
+  float dr[32], qr[32];
+  float dl;
+  {
+    float orow[32];
+    load_half_row(dr, dout + ((int64_t)b * N + q) * D + hd * DH, qok, h, 1.f);
+    load_half_row(orow, o + ((int64_t)b * N + q) * D + hd * DH, qok, h, 1.f);
+    float c[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 32; ++t) c[t & 3] = fmaf(orow[t], dr[t], c[t & 3]);
+    const float part = (c[0] + c[1]) + (c[2] + c[3]);
+    dl = part + __shfl_xor(part, 32, 64);
+  }
+  if (qok && h == 0) delta[(int64_t)bh * N + q] = dl;
+  load_half_row(qr, base + (int64_t)q * ld + hd * DH, qok, h, scale);
+  const float L = qok ? lse[(int64_t)bh * N + q] : INFINITY;   // q >= N -> P = 0
+  __syncthreads();
+
+  f32x16 dqa[2] = {zero16(), zero16()};
+#pragma unroll 1
+  for (int kb = 0; kb < NP; kb += 32) {
+    const f32x16 st = sblock_f32(kt, kb, qr, lane, zero16());   // S^T[key][q]
+    f32x16 dp = sblock_f32(vt, kb, dr, lane, zero16());         // dP^T[key][q]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] = expf(st[r] - L) * (dp[r] - dl);
+    pvblock_f32(kt, kb, dp, lane, dqa);                         // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+  }
+  __syncthreads();
+  store_tile32_f32(smem + wave * 32 * FP, dqa, scale, dqkv + (int64_t)b * N * ld + hd * DH, ld, wave * 32, N, lane);
+}
+
+// dK / dV: grid B*H, block 64*NW, wave w owns keys 32w..+31 (K scaled and V half-rows in
+// registers), Q and dO images in LDS.  Queries >= N get lse = +inf -> P = 0, dS = 0.
+template <int NPMAX>
+__global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_f32(const float* __restrict__ qkv,
+                                                                  const float* __restrict__ dout,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ delta,
+                                                                  float* __restrict__ dqkv, int N, int H,
+                                                                  float scale) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * NPMAX * FP];
+  __shared__ __attribute__((aligned(16))) float ls[NPMAX];
+  __shared__ __attribute__((aligned(16))) float dls[NPMAX];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NP = (blockDim.x >> 6) * 32;
+  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const float* base = qkv + (int64_t)b * N * ld;
+  float* qt = smem;
+  float* dt_ = smem + NP * FP;
+  const int h = lane >> 5, key = wave * 32 + (lane & 31);
+  stage_seq_f32(qt, base + hd * DH, ld, N);
+  stage_seq_f32(dt_, dout + (int64_t)b * N * D + hd * DH, D, N);
+  float kr[32], vr[32];
+  load_half_row(kr, base + (int64_t)key * ld + D + hd * DH, key < N, h, scale);
+  load_half_row(vr, base + (int64_t)key * ld + 2 * D + hd * DH, key < N, h, 1.f);
+  if (threadIdx.x < NP) {
+    const int i = threadIdx.x;
+    ls[i] = i < N ? lse[(int64_t)bh * N + i] : INFINITY;
+    dls[i] = i < N ? delta[(int64_t)bh * N + i] : 0.f;
+  }
+  __syncthreads();
+
+  f32x16 dka[2] = {zero16(), zero16()}, dva[2] = {zero16(), zero16()};
+#pragma unroll 1
+  for (int q0 = 0; q0 < NP; q0 += 32) {
+    f32x16 sa = sblock_f32(qt, q0, kr, lane, zero16());    // S[q][key]
+    f32x16 dp = sblock_f32(dt_, q0, vr, lane, zero16());   // dP[q][key]
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int q4 = q0 + 8 * g4 + 4 * h;                   // rows acc_row(4*g4 + i, h) = q4 + i
+      const f32x4 L = *(const f32x4*)(ls + q4);
+      const f32x4 dl = *(const f32x4*)(dls + q4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = expf(sa[4 * g4 + i] - L[i]);
+        sa[4 * g4 + i] = p;
+        dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
+      }
+    }
+    pvblock_f32(dt_, q0, sa, lane, dva);   // dV^T[d][key] += dO^T[d][q] P[q][key]
+    pvblock_f32(qt, q0, dp, lane, dka);    // dK^T[d][key] += Q^T[d][q] dS[q][key]
+  }
+  __syncthreads();
+  float* scr = smem + wave * 32 * FP;
+  float* db = dqkv + (int64_t)b * N * ld + hd * DH;
+  store_tile32_f32(scr, dka, scale, db + D, ld, wave * 32, N, lane);
+  store_tile32_f32(scr, dva, 1.f, db + 2 * D, ld, wave * 32, N, lane);
+}
+
+// =============================================================== fp32 path (VALU, N > NPMAX)
+// Exact fp32 (expf, fp32 FMA; the parity configuration) for sequences longer than the MFMA
+// kernels' LDS images (and policy 1).  Four lanes per row, each holding 16
 // of its 64 head dims: a dot product is 16 FMAs in 4 independent chains plus a quad xor-reduce,
 // and a row's state (q / dO / K / V and the accumulators) fits in <= 64 registers, so a SIMD
 // holds several waves.  (One thread per row with 64-float arrays had 1 wave per SIMD and
@@ -1375,6 +1644,9 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
   } else if (dtype == VITMI_BF16) {
     dim3 grid((N + 127) / 128, B * H);
     hipLaunchKernelGGL(attn_fwd_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (bf16*)o, lse, N, H, scale);
+  } else if (seq_path(N)) {
+    hipLaunchKernelGGL(attn_fwd_seq_f32<SEQ_MAX>, dim3(B * H), dim3(64 * ((N + 31) / 32)), 0, s, (const float*)qkv,
+                       (float*)o, lse, N, H, scale);
   } else {
     dim3 grid((N + 63) / 64, B * H);
     hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(256), 0, s, (const float*)qkv, (float*)o, lse, N, H, scale);
@@ -1386,6 +1658,7 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
     const double fl = 4.0 * bh * N * N * DH, by = bh * N * DH * 4 * es + bh * N * 4;
     if (dtype == VITMI_BF16 && seq_path(N)) VITMI_STAT(attn_fwd_seq_bf16<SEQ_MAX>, fl, by);
     else if (dtype == VITMI_BF16) VITMI_STAT(attn_fwd_bf16, fl, by);
+    else if (seq_path(N)) VITMI_STAT(attn_fwd_seq_f32<SEQ_MAX>, fl, by);
     else VITMI_STAT(attn_fwd_f32, fl, by);
   }
   return VITMI_OK;
@@ -1429,6 +1702,13 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
                        (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale);
     hipLaunchKernelGGL(attn_bwd_dkv_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
                        lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
+  } else if (seq_path(N)) {
+    // dQ first: it also writes delta, which the dK/dV kernel consumes
+    const dim3 block(64 * ((N + 31) / 32));
+    hipLaunchKernelGGL(attn_bwd_dq_seq_f32<SEQ_MAX>, dim3(B * H), block, 0, s, (const float*)qkv, (const float*)o,
+                       (const float*)dout, lse, delta, (float*)dqkv, N, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dkv_seq_f32<SEQ_MAX>, dim3(B * H), block, 0, s, (const float*)qkv,
+                       (const float*)dout, lse, (const float*)delta, (float*)dqkv, N, H, scale);
   } else {
     hipLaunchKernelGGL(attn_bwd_delta<float>, dim3(blocks), dim3(256), 0, s, (const float*)o,
                        (const float*)dout, delta, B * N, N, H);
@@ -1454,6 +1734,9 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     } else if (dtype == VITMI_BF16) {
       VITMI_STAT(attn_bwd_dq_bf16, fl, t * 6 * es + bh * N * 8);
       VITMI_STAT(attn_bwd_dkv_bf16, fl, t * 6 * es + bh * N * 8);
+    } else if (seq_path(N)) {
+      VITMI_STAT(attn_bwd_dq_seq_f32<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+      VITMI_STAT(attn_bwd_dkv_seq_f32<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
     }
   }
   return VITMI_OK;
