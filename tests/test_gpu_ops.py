@@ -150,6 +150,31 @@ def test_linear_wgrad_split_units(M, N, K):
     assert rel(dw, ref) < 2e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(256 * 5 + 40, 768, 512), (296, 264, 128)])
+def test_gemm_tn_layout_epilogues(M, N, K, policy):
+    """The TN layout (A and B both m/n-major, the weight-gradient operands) through the generic
+    entry with bf16 store, bias+GELU and fp32 residual epilogues: gemm256 remaps its half-tiles to
+    contiguous 128-line blocks there (line_of<.., RMP>), so every epilogue's row/column mapping is
+    exercised, ragged N included."""
+    a = rnd(K, M, dtype=BF, seed=51)                 # A(m,k) at a[k][m]
+    b = rnd(K, N, dtype=BF, seed=52, scale=0.05)     # B(k,n) at b[k][n]
+    bias = rnd(N, seed=53)
+    ref = a.float().t() @ b.float()
+    ad, bd = a.to(DEV), b.to(DEV)
+    y = ops.gemm(ad, bd, False, False, M, N, K, torch.empty(M, N, dtype=BF, device=DEV), ops.EPI_STORE,
+                 bias=bias.to(DEV))
+    assert rel(y.float(), ref + bias) < 8e-3
+    gp = torch.empty(M, N, dtype=BF, device=DEV)
+    a_ = ops.gemm(ad, bd, False, False, M, N, K, torch.empty(M, N, dtype=BF, device=DEV), ops.EPI_BIAS_GELU,
+                  bias=bias.to(DEV), aux=gp)
+    assert rel(a_.float(), F.gelu(ref + bias)) < 8e-3
+    assert rel(gp.float(), gelu_grad(ref + bias)) < 8e-3
+    res = rnd(M, N, seed=54)
+    y2 = ops.gemm(ad, bd, False, False, M, N, K, torch.empty(M, N, device=DEV), ops.EPI_RESIDUAL,
+                  bias=bias.to(DEV), residual=res.to(DEV))
+    assert rel(y2, ref + bias + res) < 1e-5
+
+
 @pytest.mark.parametrize("M,N,K,T,epi", [(197 * 64 + 3, 768, 3072, BF, "dgelu"), (50432 // 8, 768, 3072, BF, "dgelu"),
                                          (197 * 8, 256, 1024, BF, "dgelu"), (300, 128, 512, BF, "store"),
                                          (197 * 4, 768, 3072, torch.float32, "dgelu")])

@@ -127,7 +127,7 @@ __device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float
 
 // =============================================================== forward (bf16)
 // grid (ceil(N/128), B*H), 256 threads: wave w owns queries q0 + 32w .. +31.
-__global__ __launch_bounds__(256) void attn_fwd_bf16(const bf16* __restrict__ qkv,
+__global__ __launch_bounds__(256, 3) void attn_fwd_bf16(const bf16* __restrict__ qkv,
                                                      bf16* __restrict__ o, float* __restrict__ lse,
                                                      int N, int H, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][K|V] 8 KiB tiles
@@ -271,7 +271,7 @@ __global__ void attn_bwd_delta(const T* __restrict__ o, const T* __restrict__ do
 }
 
 // dK/dV: grid (ceil(N/128), B*H), wave w owns keys k0 = 128*bx + 32w .. +31.
-__global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkv_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
   // [buf][Q tile | dO tile] 2 x 16 KiB, then [buf][lse*log2e | delta] 2 x 512 B (one array: the
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_bf16(
 // dQ: grid (ceil(N/128), B*H), wave w owns queries q0 = 128*bx + 32w .. +31.
 // Also produces delta[bh][q] = sum_d dO[q][d] O[q][d] (consumed here and by the dK/dV
 // kernel, which therefore runs after this one).
-__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
+__global__ __launch_bounds__(256, 4) void attn_bwd_dq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
     float scale) {
