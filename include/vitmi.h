@@ -152,9 +152,10 @@ size_t vitmi_attention_bwd_workspace_size(int B, int N, int H);
  * Returns the previous policy. */
 int vitmi_attention_set_policy(int policy);
 /* vitmi_attention_bwd plus the qkv bias gradient: dbias[3*H*dh] += column sums of dqkv (the
- * q/k/v Dense biases, models/CvT(Par).py:132-134).  On the whole-sequence bf16 path (N <= 256)
- * the sums come from the dQ and dK/dV kernels' registers (per (batch, head) block, then a
- * fixed-order fold over the batch); elsewhere from a second pass over dqkv. */
+ * q/k/v Dense biases, models/CvT(Par).py:132-134).  On the bf16 paths the sums come from the
+ * dQ and dK/dV kernels' output images (per (batch, head) block on the whole-sequence path,
+ * N <= 256, per (batch, head, 128-row block) on the streamed one, then a fixed-order fold); the
+ * fp32 paths take a second pass over dqkv. */
 size_t vitmi_attention_bwd_bias_workspace_size(int B, int N, int H);
 int vitmi_attention_bwd_bias(int dtype, int B, int N, int H, int dh, float scale, const void* qkv, const void* o,
                              const void* dout, const float* lse, void* dqkv, float* dbias, void* workspace,

@@ -332,7 +332,7 @@ def test_attention_bwd_single_pass(B, N, H):
 
 
 @pytest.mark.parametrize("B,N,H,T", [(2, 197, 2, BF), (3, 17, 1, BF), (1, 256, 3, BF), (2, 1, 2, BF),
-                                     (2, 300, 1, BF), (2, 33, 2, torch.float32)])
+                                     (2, 300, 1, BF), (3, 577, 2, BF), (2, 33, 2, torch.float32)])
 def test_attention_bwd_fused_bias(B, N, H, T):
     """the q/k/v bias gradient out of the attention backward kernels (column sums of the dQ,
     dK, dV tiles as stored, formed from the LDS image they leave through) == a column-sum pass

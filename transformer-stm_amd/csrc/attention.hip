@@ -90,6 +90,20 @@ __device__ __forceinline__ bf16x8 frag_tr(const char* t, int k0, int c0, int lan
   return f;
 }
 
+// XCD-aware block order of the streamed kernels (grid (ceil(N/128), B*H)): the hardware deals
+// workgroups out round-robin over the 8 XCDs by linear id, which puts the ceil(N/128) blocks of
+// one (batch, head) on different XCDs, each streaming the pair's whole K/V (or Q/dO) through its
+// own L2.  Returned: the (block-in-pair, pair) this workgroup takes, such that every XCD walks a
+// contiguous range of the logical order (x fastest), so a pair's blocks share one L2.
+__device__ __forceinline__ void xcd_block(int& bx, int& bh) {
+  const int gx = gridDim.x, total = gx * gridDim.y;
+  const int i = blockIdx.y * gx + blockIdx.x;
+  const int x = i & 7, slot = i >> 3, per = total >> 3, rem = total & 7;
+  const int j = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + slot;
+  bh = j / gx;
+  bx = j - bh * gx;
+}
+
 // key/query index held in accumulator register r of a 32x32 tile for lane-half h
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -125,6 +139,83 @@ __device__ __forceinline__ void store4(bf16* p, float a, float b, float c, float
   *(bf16x4*)p = v;
 }
 
+// A wave's 32-row x 64-column output tile in the 32x32 accumulator layout (lane: row =
+// lane & 31; acc[c2][r] = column 32*c2 + acc_row(r, lane >> 5)) leaves as whole 128-B lines:
+// written as bf16 into a per-wave [32][144 B] LDS image, read back 16 B per lane and stored as
+// 8 rows x 128 B per instruction.  Stored straight from the accumulator, every line would be
+// written in eight 16-B pieces by eight instructions (store-issue bound).  Row r goes to byte
+// offset (row0 + r) * ld_bytes of rs; rows past rs's range (>= N) are dropped by the buffer
+// range check.  The compiler barriers keep the cross-lane exchange ordered (each lane reads
+// what other lanes wrote).
+static constexpr int ST_PITCH = 144;
+static constexpr int ST_BYTES = 32 * ST_PITCH;
+
+// the lane index as an opaque value: the lane-derived addresses of an epilogue are formed where
+// it runs, not hoisted above the main loop to stay live across it (the dQ kernel sits at 128
+// VGPRs, and the hoisted ones pushed a reload into its loop)
+__device__ __forceinline__ int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+__device__ __forceinline__ void store_tile32(char* scr, const f32x16 (&acc)[2], float mul,
+                                             __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int row0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)(acc[c2][4 * g4 + i] * mul);
+      *(bf16x4*)(scr + r * ST_PITCH + (32 * c2 + 8 * g4 + 4 * h) * 2) = v;
+    }
+  asm volatile("" ::: "memory");
+  const int rr = lane >> 3, cc = lane & 7;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32x4 v = *(const u32x4*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)((int64_t)(row0 + 8 * j + rr) * ld_bytes + cc * 16), 0, 0);
+  }
+  asm volatile("" ::: "memory");
+}
+
+// Column sums of the rows < nvalid of the tile store_tile32 just wrote (its LDS image, as the
+// stored bf16 values): each lane adds 4 rows x 8 columns, xor-shuffles fold the 8 row groups,
+// and the block's waves (all of which must call) fold through red[wave][64] in wave order into
+// colpart[0..63] -- a bias-gradient partial without a second pass over the stored matrix, in a
+// fixed summation order.
+__device__ __forceinline__ void tile32_colsum(const char* scr, int row0, int nvalid, float* colpart,
+                                              float (*red)[64], int wave, int nw, int lane) {
+  const int rr = lane >> 3, cc = lane & 7;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (row0 + 8 * j + rr < nvalid) {
+      const bf16x8 b = *(const bf16x8*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += (float)b[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] += __shfl_xor(cs[e], 8, 64);
+    cs[e] += __shfl_xor(cs[e], 16, 64);
+    cs[e] += __shfl_xor(cs[e], 32, 64);
+  }
+  __syncthreads();                       // red is free (an earlier call's fold is done)
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wave][lane * 8 + e] = cs[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+    for (int w = 0; w < nw; ++w) t += red[w][threadIdx.x];
+    colpart[threadIdx.x] = t;
+  }
+}
+
 // =============================================================== forward (bf16)
 // grid (ceil(N/128), B*H), 256 threads: wave w owns queries q0 + 32w .. +31.
 __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(const bf16* __restrict__ qkv,
@@ -133,7 +224,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(const bf16* __restrict__
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][K|V] 8 KiB tiles
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  int bx, bh;
+  xcd_block(bx, bh);
+  const int b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D;
   const int64_t ldb = ld * 2;
@@ -144,7 +237,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(const bf16* __restrict__
   __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
   __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
 
-  const int qw = blockIdx.x * 128 + wave * 32;  // first query of this wave
+  const int qw = bx * 128 + wave * 32;  // first query of this wave
   const int q = qw + (lane & 31);
   // Q^T operand fragments: lane col q, k = d = 16s + 8h + j
   bf16x8 qf[4];
@@ -236,19 +329,12 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(const bf16* __restrict__
   }
   if (qw >= N) return;
   const float lt = l + __shfl_xor(l, 32, 64);
-  if (q < N) {
-    const float inv = 1.f / lt;
-    bf16* orow = o + ((int64_t)b * N + q) * D + hd * DH;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * dt + 8 * g4 + 4 * h;
-        store4(orow + d, oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv, oacc[dt][4 * g4 + 2] * inv,
-               oacc[dt][4 * g4 + 3] * inv);
-      }
-    if (h == 0) lse[(int64_t)bh * N + q] = (m + log2f(lt)) * LN2;
-  }
+  if (q < N && h == 0) lse[(int64_t)bh * N + q] = (m + log2f(lt)) * LN2;
+  // O as whole 128-B lines through a per-wave image in the (free: the loop ended on a barrier)
+  // K/V buffers; rows >= N fall outside the descriptor's range
+  const int64_t ldo = (int64_t)D * 2;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
+  store_tile32(smem + wave * ST_BYTES, oacc, 1.f / lt, ro, ldo, qw, lane_here());
 }
 
 // =============================================================== backward (bf16)
@@ -273,14 +359,17 @@ __global__ void attn_bwd_delta(const T* __restrict__ o, const T* __restrict__ do
 // dK/dV: grid (ceil(N/128), B*H), wave w owns keys k0 = 128*bx + 32w .. +31.
 __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale) {
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale,
+    float* __restrict__ colsum) {
   // [buf][Q tile | dO tile] 2 x 16 KiB, then [buf][lse*log2e | delta] 2 x 512 B (one array: the
   // compiler must see a single LDS object next to the DMA, cdna_hip_programming.md §5 trap (a))
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192 + 2 * 512];
   float* rowst = (float*)(smem + 32768);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  int bx, bh;
+  xcd_block(bx, bh);
+  const int b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
   const int h = lane >> 5;
@@ -302,7 +391,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_bf16(
     }
   };
 
-  const int kw = blockIdx.x * 128 + wave * 32;
+  const int kw = bx * 128 + wave * 32;
   const int key = kw + (lane & 31);
   // K^T / V^T operand fragments (B operands): lane col = key, k = d = 16s + 8h + j
   bf16x8 kf[4], vf[4];
@@ -368,18 +457,20 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_bf16(
     if (t + 1 < nt) stage_rows(t + 1, buf ^ 1);
     __syncthreads();
   }
-  if (kw >= N || key >= N) return;
-  bf16* row = dqkv + ((int64_t)b * N + key) * ld;
-#pragma unroll
-  for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 32 * d2 + 8 * g4 + 4 * h;
-      store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
-             dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
-      store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
-             dvt[d2][4 * g4 + 3]);
-    }
+  // dK, dV as whole lines through a per-wave image in the (free) Q | dO buffers; rows >= N
+  // (whole waves past N hold zeros) fall outside the descriptors.  With colsum, the k- and
+  // v-bias gradient partials of this (batch, key block) row come from the same images.
+  const bf16* db = dqkv + (int64_t)b * N * ld;
+  const __amdgpu_buffer_rsrc_t rdk = make_rsrc(db + D + hd * DH, bytes - (D + hd * DH) * 2);
+  const __amdgpu_buffer_rsrc_t rdv = make_rsrc(db + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  const int ln = lane_here();
+  char* scr = smem + wave * ST_BYTES;
+  float* part = colsum + ((int64_t)b * gridDim.x + bx) * 3 * D + hd * DH;
+  __shared__ float red[4][64];
+  store_tile32(scr, dkt, scale, rdk, ldb, kw, ln);
+  if (colsum) tile32_colsum(scr, kw, N, part + D, red, wave, 4, ln);
+  store_tile32(scr, dvt, 1.f, rdv, ldb, kw, ln);
+  if (colsum) tile32_colsum(scr, kw, N, part + 2 * D, red, wave, 4, ln);
 }
 
 // dQ: grid (ceil(N/128), B*H), wave w owns queries q0 = 128*bx + 32w .. +31.
@@ -388,11 +479,13 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_bf16(
 __global__ __launch_bounds__(256, 4) void attn_bwd_dq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
-    float scale) {
+    float scale, float* __restrict__ colsum) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];  // [buf][K|V]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int bh = blockIdx.y, b = bh / H, hd = bh % H;
+  int bx, bh;
+  xcd_block(bx, bh);
+  const int b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
   const int h = lane >> 5;
@@ -404,7 +497,7 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq_bf16(
   __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
   __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
 
-  const int qw = blockIdx.x * 128 + wave * 32;
+  const int qw = bx * 128 + wave * 32;
   const int q = qw + (lane & 31);
   bf16x8 qf[4], df[4];
 #pragma unroll
@@ -479,16 +572,17 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq_bf16(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (qw >= N || !qok) return;
-  bf16* row = dqkv + ((int64_t)b * N + q) * ld + hd * DH;
-#pragma unroll
-  for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 32 * d2 + 8 * g4 + 4 * h;
-      store4(row + d, dqt[d2][4 * g4] * scale, dqt[d2][4 * g4 + 1] * scale,
-             dqt[d2][4 * g4 + 2] * scale, dqt[d2][4 * g4 + 3] * scale);
-    }
+  // dQ as whole lines through a per-wave image in the (free) K | V buffers (rows >= N fall
+  // outside the descriptor); with colsum also the q-bias gradient partial of this (batch,
+  // query block) row
+  const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv + (int64_t)b * N * ld + hd * DH, bytes - hd * DH * 2);
+  const int ln = lane_here();
+  store_tile32(smem + wave * ST_BYTES, dqt, scale, rdq, ldb, qw, ln);
+  if (colsum) {
+    __shared__ float red[4][64];
+    tile32_colsum(smem + wave * ST_BYTES, qw, N, colsum + ((int64_t)b * gridDim.x + bx) * 3 * D + hd * DH, red, wave, 4,
+                  ln);
+  }
 }
 
 // ====================================================== whole-sequence kernels (bf16)
@@ -507,83 +601,6 @@ __device__ __forceinline__ void stage_seq(char* lds, __amdgpu_buffer_rsrc_t rs, 
     const int c = (lane & 7) ^ att_swz(r);
     const uint32_t voff = (uint32_t)((int64_t)r * ld_bytes + c * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, lds + p * 1024), 16, voff, 0, 0, 0);
-  }
-}
-
-// A wave's 32-row x 64-column output tile in the 32x32 accumulator layout (lane: row =
-// lane & 31; acc[c2][r] = column 32*c2 + acc_row(r, lane >> 5)) leaves as whole 128-B lines:
-// written as bf16 into a per-wave [32][144 B] LDS image, read back 16 B per lane and stored as
-// 8 rows x 128 B per instruction.  Stored straight from the accumulator, every line would be
-// written in eight 16-B pieces by eight instructions (store-issue bound).  Row r goes to byte
-// offset (row0 + r) * ld_bytes of rs; rows past rs's range (>= N) are dropped by the buffer
-// range check.  The compiler barriers keep the cross-lane exchange ordered (each lane reads
-// what other lanes wrote).
-static constexpr int ST_PITCH = 144;
-static constexpr int ST_BYTES = 32 * ST_PITCH;
-
-// the lane index as an opaque value: the lane-derived addresses of an epilogue are formed where
-// it runs, not hoisted above the main loop to stay live across it (the dQ kernel sits at 128
-// VGPRs, and the hoisted ones pushed a reload into its loop)
-__device__ __forceinline__ int lane_here() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
-__device__ __forceinline__ void store_tile32(char* scr, const f32x16 (&acc)[2], float mul,
-                                             __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int row0, int lane) {
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int c2 = 0; c2 < 2; ++c2)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      bf16x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (bf16)(acc[c2][4 * g4 + i] * mul);
-      *(bf16x4*)(scr + r * ST_PITCH + (32 * c2 + 8 * g4 + 4 * h) * 2) = v;
-    }
-  asm volatile("" ::: "memory");
-  const int rr = lane >> 3, cc = lane & 7;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const u32x4 v = *(const u32x4*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (uint32_t)((int64_t)(row0 + 8 * j + rr) * ld_bytes + cc * 16), 0, 0);
-  }
-  asm volatile("" ::: "memory");
-}
-
-// Column sums of the rows < nvalid of the tile store_tile32 just wrote (its LDS image, as the
-// stored bf16 values): each lane adds 4 rows x 8 columns, xor-shuffles fold the 8 row groups,
-// and the block's waves (all of which must call) fold through red[wave][64] in wave order into
-// colpart[0..63] -- a bias-gradient partial without a second pass over the stored matrix, in a
-// fixed summation order.
-__device__ __forceinline__ void tile32_colsum(const char* scr, int row0, int nvalid, float* colpart,
-                                              float (*red)[64], int wave, int nw, int lane) {
-  const int rr = lane >> 3, cc = lane & 7;
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (row0 + 8 * j + rr < nvalid) {
-      const bf16x8 b = *(const bf16x8*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) cs[e] += (float)b[e];
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    cs[e] += __shfl_xor(cs[e], 8, 64);
-    cs[e] += __shfl_xor(cs[e], 16, 64);
-    cs[e] += __shfl_xor(cs[e], 32, 64);
-  }
-  __syncthreads();                       // red is free (an earlier call's fold is done)
-  if (lane < 8) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[wave][lane * 8 + e] = cs[e];
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    float t = 0.f;
-    for (int w = 0; w < nw; ++w) t += red[w][threadIdx.x];
-    colpart[threadIdx.x] = t;
   }
 }
 
@@ -1670,8 +1687,8 @@ extern "C" size_t vitmi_attention_bwd_workspace_size(int B, int N, int H) {
 
 static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scale, const void* qkv, const void* o,
                               const void* dout, const float* lse, void* dqkv, void* workspace, size_t ws_bytes,
-                              vitmi_stream_t stream, float* colsum, bool* colsum_done) {
-  if (colsum_done) *colsum_done = false;
+                              vitmi_stream_t stream, float* colsum, int* colsum_rows) {
+  if (colsum_rows) *colsum_rows = 0;
   if (int rc = attn_check(dtype, B, N, H, dh)) return rc;
   VITMI_CHECK_ARG(qkv && o && dout && lse && dqkv, "attention_bwd: null pointer");
   VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_attention_bwd_workspace_size(B, N, H),
@@ -1693,15 +1710,17 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
       hipLaunchKernelGGL(attn_bwd_dkv_seq_bf16<SEQ_MAX>, dim3(npairs < cus ? npairs : cus), block, 0, s,
                          (const bf16*)qkv, (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale,
                          colsum, npairs);
-      if (colsum_done) *colsum_done = colsum != nullptr;
+      if (colsum_rows) *colsum_rows = colsum ? B : 0;   // one partial row per batch
     }
   } else if (dtype == VITMI_BF16) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
     dim3 grid((N + 127) / 128, B * H);
     hipLaunchKernelGGL(attn_bwd_dq_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)o,
-                       (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale);
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
     hipLaunchKernelGGL(attn_bwd_dkv_bf16, grid, dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
-                       lse, (const float*)delta, (bf16*)dqkv, N, H, scale);
+                       lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum);
+    // one bias-gradient partial row per (batch, 128-row block)
+    if (colsum_rows) *colsum_rows = colsum ? B * (int)grid.x : 0;
   } else if (seq_path(N)) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
     const dim3 block(64 * ((N + 31) / 32));
@@ -1752,7 +1771,8 @@ extern "C" int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float
 
 extern "C" size_t vitmi_attention_bwd_bias_workspace_size(int B, int N, int H) {
   const size_t delta = ((size_t)B * H * N * sizeof(float) + 255) / 256 * 256;
-  const size_t part = (size_t)B * 3 * H * DH * sizeof(float);
+  // fused partial rows: one per batch (whole-sequence kernels) or per (batch, 128-row block)
+  const size_t part = (size_t)B * ((N + 127) / 128) * 3 * H * DH * sizeof(float);
   const size_t fallback = vitmi_bias_grad_workspace_size((int64_t)B * N, 3LL * H * DH);
   return delta + (part > fallback ? part : fallback);
 }
@@ -1765,11 +1785,11 @@ extern "C" int vitmi_attention_bwd_bias(int dtype, int B, int N, int H, int dh, 
                   "attention_bwd_bias: workspace too small");
   const size_t delta = ((size_t)B * H * N * sizeof(float) + 255) / 256 * 256;
   float* part = (float*)((char*)workspace + delta);
-  bool done = false;
+  int rows = 0;
   if (int rc = attention_bwd_impl(dtype, B, N, H, dh, scale, qkv, o, dout, lse, dqkv, workspace, delta,
-                                  stream, part, &done))
+                                  stream, part, &rows))
     return rc;
   const int64_t D3 = 3LL * H * DH;
-  if (done) return launch_colsum_finish(D3, B, part, dbias, (hipStream_t)stream);
+  if (rows) return launch_colsum_finish(D3, rows, part, dbias, (hipStream_t)stream);
   return vitmi_bias_grad(dtype, (int64_t)B * N, D3, dqkv, D3, dbias, part, ws_bytes - delta, stream);
 }

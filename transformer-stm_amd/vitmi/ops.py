@@ -254,8 +254,9 @@ def attention_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, B: int, N: in
     """dqkv; ``bias_grad`` (fp32 [3D]) += its column sums (the q/k/v bias gradient).
 
     ``fused_bias`` (default) forms the sums in the backward kernels from the LDS image each
-    output tile is stored through (vitmi_attention_bwd_bias: one [B][3D] partial row per batch,
-    folded in a fixed order), instead of a second pass over dqkv; ``fused_bias=False`` runs the
+    output tile is stored through (vitmi_attention_bwd_bias: one [3D] partial row per batch, or
+    per (batch, 128-row block) for N > 256, folded in a fixed order), instead of a second pass
+    over dqkv; ``fused_bias=False`` runs the
     separate column-sum pass (kernels without the fused sums fall back to it anyway)."""
     D = o.shape[-1]
     assert do.is_contiguous() and do.dtype == qkv.dtype
