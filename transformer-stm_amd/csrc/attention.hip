@@ -614,7 +614,10 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6, NP = nw * 32;
-  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  // pairs in DESCENDING order: the producer of this kernel's operand (the qkv GEMM for the
+  // forward, the out-proj dgrad writing dO for dQ) finished with the last rows, which are the
+  // ones still in the MALL; the dK/dV kernel after dQ then walks ascending (dQ ended at pair 0)
+  const int bh = gridDim.x - 1 - blockIdx.x, b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D, ldb = ld * 2;
   const int h = lane >> 5;
@@ -723,7 +726,10 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6, NP = nw * 32;
-  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
+  // pairs in DESCENDING order: the producer of this kernel's operand (the qkv GEMM for the
+  // forward, the out-proj dgrad writing dO for dQ) finished with the last rows, which are the
+  // ones still in the MALL; the dK/dV kernel after dQ then walks ascending (dQ ended at pair 0)
+  const int bh = gridDim.x - 1 - blockIdx.x, b = bh / H, hd = bh % H;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
   const int h = lane >> 5;
