@@ -419,25 +419,33 @@ __device__ __forceinline__ void stage_half(char* sub, __amdgpu_buffer_rsrc_t rs,
 // 1.5e-7: one exp, one rcp, 5 FMAs; used only where the result is rounded to bf16, the fp32
 // path keeps erff).  Written on f32x4 so that everything but the rcp / exp / |x| / sign steps
 // issues as packed v_pk_* pairs, the two independent halves of every step alternating (a packed
-// result consumed by the very next instruction costs an s_nop): 14 VALU per element instead of
-// 16 (the fc1 epilogue is VALU-bound; fc1 + GELU 334 -> 328 us).  0.5*erf comes directly from
-// coefficients pre-scaled by 0.5 (exact), the sign by copysign (v_bfi).
+// result consumed by the very next instruction costs an s_nop): 12 VALU per element instead of
+// 16 (the fc1 epilogue is VALU-bound; fc1 + GELU 334 -> 328 us at 14).  0.5*erf comes directly
+// from coefficients pre-scaled by 0.5 (exact), the sign by copysign (v_bfi).
 __device__ __forceinline__ void gelu4(f32x4 x, f32x4& a, f32x4& gp) {
-  f32x4 ax, t, e;
+  f32x4 ax, u, e;
 #pragma unroll
   for (int i = 0; i < 4; ++i) ax[i] = fabsf(x[i]);
   const f32x4 d = ax * (0.3275911f * 0.70710678118654752f) + 1.0f;
+  // u = -t = 1 / -d (the sign rides on v_rcp's source modifier).  In u every coefficient of the
+  // -0.5-scaled polynomial is positive and each Horner step is the exact negation of the one in
+  // t, so q = -0.5 P(t) bit for bit and 0.5 erf = 0.5 + q e is a plain FMA: no negated operand
+  // for the compiler to materialise with a v_xor per element
 #pragma unroll
-  for (int i = 0; i < 4; ++i) t[i] = __builtin_amdgcn_rcpf(d[i]);
-  const f32x4 earg = (x * x) * (-0.5f * 1.4426950408889634f);
+  for (int i = 0; i < 4; ++i) u[i] = __builtin_amdgcn_rcpf(-d[i]);
+  // exp(-x^2/2) = exp2(-(x k)^2), k = sqrt(log2(e) / 2): a packed multiply by an SGPR constant and
+  // a packed square, the minus sign on v_exp's source modifier (a literal factor after the square
+  // cannot be packed: it took two scalar multiplies per pair)
+  const f32x4 xk = x * 0.84932180028801907f;
+  const f32x4 y = xk * xk;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_exp2f(earg[i]);   // exp(-x^2/2)
-  f32x4 p = t * (0.5f * 1.061405429f) + (0.5f * -1.453152027f);
-  p = p * t + (0.5f * 1.421413741f);
-  p = p * t + (0.5f * -0.284496736f);
-  p = p * t + (0.5f * 0.254829592f);
-  p = p * t;
-  f32x4 h = 0.5f - p * e;                                  // 0.5 erf(|x| / sqrt 2)
+  for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_exp2f(-y[i]);
+  f32x4 q = u * (0.5f * 1.061405429f) + (0.5f * 1.453152027f);
+  q = q * u + (0.5f * 1.421413741f);
+  q = q * u + (0.5f * 0.284496736f);
+  q = q * u + (0.5f * 0.254829592f);
+  q = q * u;
+  f32x4 h = q * e + 0.5f;                                  // 0.5 erf(|x| / sqrt 2)
 #pragma unroll
   for (int i = 0; i < 4; ++i) h[i] = __builtin_copysignf(h[i], x[i]);
   const f32x4 cdf = h + 0.5f;
