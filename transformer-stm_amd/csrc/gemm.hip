@@ -16,6 +16,7 @@
 // k permutation, so the sum is unchanged.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 // Opens every inline-asm buffer store that takes SGPR operands (descriptor, soffset): under SGPR
 // pressure hipcc rematerialises such operands with v_readlane right before the statement, and a
@@ -984,21 +985,28 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         if constexpr (EPI == VITMI_EPI_DGELU) {
           if (g.colsum) {
             // sum the wave's 128 rows: 8 row groups in registers (above), then the 16 lanes
-            // of a column group (lane & 15 = row); lanes 0/16/32/48 store 4 columns per ni
+            // of a column group (lane & 15 = row, one DPP row): four row_shr adds leave the sum
+            // in lane 15 of the row (no LDS round trips, unlike ds_bpermute shuffles); lanes
+            // 15/31/47/63 store 4 columns per ni
+            auto row_shr_add = [](float x, auto n) {
+              constexpr int N = decltype(n)::value;
+              const int y = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x110 | N, 0xf, 0xf, true);
+              return x + __builtin_bit_cast(float, y);   // lanes < N of the row add 0 (bound_ctrl)
+            };
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 float x = csum[ni][e];
-                x += __shfl_xor(x, 1, 64);
-                x += __shfl_xor(x, 2, 64);
-                x += __shfl_xor(x, 4, 64);
-                x += __shfl_xor(x, 8, 64);
+                x = row_shr_add(x, std::integral_constant<int, 1>{});
+                x = row_shr_add(x, std::integral_constant<int, 2>{});
+                x = row_shr_add(x, std::integral_constant<int, 4>{});
+                x = row_shr_add(x, std::integral_constant<int, 8>{});
                 csum[ni][e] = x;
               }
             const int64_t prow = (m0 / BM) * 2 + wm;
             const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.colsum + prow * g.N + n0, clamp_bytes((g.N - n0) * 4));
-            const uint32_t cb = lr == 0 ? (uint32_t)((wn * 64 + lc4) * 4) : 0x80000000u;
+            const uint32_t cb = lr == 15 ? (uint32_t)((wn * 64 + lc4) * 4) : 0x80000000u;
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
               asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, 0 offen offset:%3\n\ts_nop 1"
