@@ -612,13 +612,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       else DST[nt][ks].v = tr_read(s_ + ks * 32 * 256, bmofs[nt]);                              \
     }                                                                                           \
   } while (0)
+// In a unit's first K-step (FIRST) the ks = 0 MFMA of every accumulator starts from an inline
+// zero C operand instead of an accumulator cleared by 128 v_mov per wave and tile
 #define MMA4(MH, NH, AS, BS)                                                                    \
   do {                                                                                          \
     __builtin_amdgcn_s_setprio(1);                                                              \
     _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
     _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                            \
-      acc[MH * 4 + mt][NH * 2 + nt] = mma(BS[nt][ks], AS[mt][ks], acc[MH * 4 + mt][NH * 2 + nt]); \
+      acc[MH * 4 + mt][NH * 2 + nt] = mma(BS[nt][ks], AS[mt][ks],                               \
+          FIRST && ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[MH * 4 + mt][NH * 2 + nt]);         \
     __builtin_amdgcn_s_setprio(0);                                                              \
   } while (0)
 
@@ -671,10 +674,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     int ks0n = 0, nkn = 0, zsn = 0;
     if (has_next) unit_of(next, m0n, n0n, ks0n, nkn, zsn);
     const __amdgpu_buffer_rsrc_t ran = rsrc_a(m0n, ks0n), rbn = rsrc_b(n0n, ks0n);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
       // vmcnt counts of the first step after an epilogue that issued S vector-memory ops:
       // 8 + S (capped at the counter's 63): S = 16 (bf16 store), 32 (GELU, fp32 store, split
@@ -690,14 +689,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         MMA4(MH, NH, AS, BS);                                                                   \
         barrier();                                                                              \
       } while (0)
-      for (int t = 0; t < nku; ++t) {
+      // one K-step; FIRST (step 0 of the unit, peeled) starts the accumulators from zero
+      auto kstep = [&](auto first_tag, const int t) {
+        constexpr bool FIRST = decltype(first_tag)::value;
         // step t+1 (B1, A1 still to issue, buffer buf^1) and step t+2 (A0, B0, buffer buf)
         const bool in1 = t + 1 < nku, in2 = t + 2 < nku;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
         const __amdgpu_buffer_rsrc_t a1 = in1 ? ra : ran, b1r = in1 ? rb : rbn;
         const __amdgpu_buffer_rsrc_t a2 = in2 ? ra : ran, b2r = in2 ? rb : rbn;
         const int t1 = in1 ? t + 1 : 0, t2 = in2 ? t + 2 : t + 2 - nku;
-        const int fst = t == 0 ? ep_ops : 0;
+        const int fst = FIRST ? ep_ops : 0;
         // P0 (A0,B0): DMA B1(t+1); retire B1(t)
         RD_A(ax, buf, 0);
         RD_B(b0, buf, 0);
@@ -730,7 +731,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         }
         COMPUTE(1, 0, ay, b0);
         buf ^= 1;
-      }
+      };
+      kstep(std::true_type{}, 0);
+      for (int t = 1; t < nku; ++t) kstep(std::false_type{}, t);
 #undef COMPUTE
 #undef WAITF
 #undef WAITV
