@@ -910,17 +910,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           }
         } else if constexpr (EB == VITMI_EPI_RESIDUAL) {
           // fp32 residual in, fp32 out, both as whole lines through the LDS image, half a row
-          // group (8 rows x 256 B) at a time: lane (rq, cq) moves 16 B of row 4j + rq, the lanes
-          // holding those rows in the accumulator layout (lr / 8 == half) read, update and write
-          // them back in between.  RB row groups of loads in flight (64 VGPRs).
-          constexpr int P32 = 272;   // 68 dwords: 8 rows fit the 2304-B image
-          const int rq = lane >> 4, cq = lane & 15;
-          const bool cqok = n0 + wn * 64 + cq * 4 < g.N;
+          // group's columns (16 rows x 32 fp32 = one 128-B line per row) at a time: lane (rr8, c8)
+          // moves 16 B of row 8j + rr8, then EVERY lane updates its two accumulator fragments of
+          // that column half in place (a row-half split left half the lanes idle in each pass),
+          // and the lines go back out.  Pitch 36 dwords: the 16 rows of a fragment access fall on
+          // distinct bank quads.  RB row groups of loads in flight (64 VGPRs).
+          constexpr int P32 = 144;   // 16 rows x 128 B at a 144-B pitch = the 2304-B image
+          const int rr8 = lane >> 3, c8 = lane & 7;
           const __amdgpu_buffer_rsrc_t rres =
               make_rsrc((const char*)(g.residual + m0 * g.ldr + n0), clamp_bytes(((g.M - m0) * g.ldr - n0) * 4));
-          auto vo32 = [&](int hh, int j, int64_t ld) -> uint32_t {
-            return cqok ? (uint32_t)(((int64_t)(wm * 128 + 8 * hh + 4 * j + rq) * ld + wn * 64 + cq * 4) * 4)
-                        : 0x80000000u;
+          auto vo32 = [&](int pp, int j, int64_t ld) -> uint32_t {
+            const int col = wn * 64 + pp * 32 + c8 * 4;
+            return n0 + col < g.N ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr8) * ld + col) * 4) : 0x80000000u;
           };
 #pragma unroll
           for (int mp = 0; mp < 8 / RB; ++mp) {
@@ -928,42 +929,41 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #pragma unroll
             for (int h = 0; h < RB; ++h)
 #pragma unroll
-              for (int hh = 0; hh < 2; ++hh)
+              for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                  rl[h][hh][j] = __builtin_amdgcn_raw_buffer_load_b128(rres, vo32(hh, j, g.ldr),
+                  rl[h][pp][j] = __builtin_amdgcn_raw_buffer_load_b128(rres, vo32(pp, j, g.ldr),
                                                                        (int)((RB * mp + h) * 16 * g.ldr * 4), 0);
 #pragma unroll
             for (int h = 0; h < RB; ++h) {
               const int mi = RB * mp + h;
 #pragma unroll
-              for (int hh = 0; hh < 2; ++hh) {
+              for (int pp = 0; pp < 2; ++pp) {
 #pragma unroll
-                for (int j = 0; j < 2; ++j) *(u32x4*)(scr + (4 * j + rq) * P32 + cq * 16) = rl[h][hh][j];
+                for (int j = 0; j < 2; ++j) *(u32x4*)(scr + (8 * j + rr8) * P32 + c8 * 16) = rl[h][pp][j];
                 lane_xchg();
-                if ((lr >> 3) == hh) {
 #pragma unroll
-                  for (int ni = 0; ni < 4; ++ni) {
-                    f32x4* pr = (f32x4*)(scr + (lr & 7) * P32 + (ni * 16 + lc4) * 4);
-                    f32x4 v = acc[mi][ni] + bv[ni];
-                    if constexpr (DROP) {
-                      const uint32_t rk = drop_row_key(g.drop_seed, g.drop_site, (uint32_t)(m0 + wm * 128 + mi * 16 + lr));
+                for (int q = 0; q < 2; ++q) {
+                  const int ni = 2 * pp + q;
+                  f32x4* pr = (f32x4*)(scr + lr * P32 + (q * 16 + lc4) * 4);
+                  f32x4 v = acc[mi][ni] + bv[ni];
+                  if constexpr (DROP) {
+                    const uint32_t rk = drop_row_key(g.drop_seed, g.drop_site, (uint32_t)(m0 + wm * 128 + mi * 16 + lr));
 #pragma unroll
-                      for (int e = 0; e < 4; ++e)
-                        v[e] *= drop_hash(rk, (uint32_t)(colc[ni] + e)) >= g.drop_thresh ? g.drop_scale : 0.f;
-                    }
-                    *pr = v + *pr;
+                    for (int e = 0; e < 4; ++e)
+                      v[e] *= drop_hash(rk, (uint32_t)(colc[ni] + e)) >= g.drop_thresh ? g.drop_scale : 0.f;
                   }
+                  *pr = v + *pr;
                 }
                 lane_xchg();
                 u32x4 d[2];
 #pragma unroll
-                for (int j = 0; j < 2; ++j) d[j] = *(const u32x4*)(scr + (4 * j + rq) * P32 + cq * 16);
-                lane_xchg();   // every lane's read before the next half rewrites the image
+                for (int j = 0; j < 2; ++j) d[j] = *(const u32x4*)(scr + (8 * j + rr8) * P32 + c8 * 16);
+                lane_xchg();   // every lane's read before the next pass rewrites the image
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                   asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
-                               :: "v"(d[j]), "v"(vo32(hh, j, g.ldc)), "s"(rc), "s"((int)(mi * 16 * g.ldc * 4))
+                               :: "v"(d[j]), "v"(vo32(pp, j, g.ldc)), "s"(rc), "s"((int)(mi * 16 * g.ldc * 4))
                                : "memory");
               }
             }
