@@ -715,7 +715,10 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
 // dQ (+ delta = rowsum(dO * O)): grid B*H, block 64*NW, wave w owns queries 32w..+31, K and V
 // of the whole sequence in LDS.  Keys >= N need no mask: their K rows are zero in LDS, so
 // their dS (whatever it is) meets a zero row of K in dQ = dS K.
-template <int NPMAX>
+// NWC > 0: the wave count (ceil(N / 32)) as a compile-time constant (the ViT shapes, N = 197:
+// 7), so the loop over the 32-row blocks unrolls and every LDS fragment address is a lane base
+// plus an immediate offset (the runtime loop spent 12 (dQ) / 25 (dK/dV) v_add per block on them)
+template <int NPMAX, int NWC = 0>
 __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
@@ -725,7 +728,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = blockDim.x >> 6, NP = nw * 32;
+  const int nw = NWC > 0 ? NWC : blockDim.x >> 6, NP = nw * 32;
   // pairs in DESCENDING order: the producer of this kernel's operand (the qkv GEMM for the
   // forward, the out-proj dgrad writing dO for dQ) finished with the last rows, which are the
   // ones still in the MALL; the dK/dV kernel after dQ then walks ascending (dQ ended at pair 0)
@@ -775,8 +778,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
 
   const float c2 = scale * LOG2E;
   f32x16 dqt[2] = {zero16(), zero16()};
-#pragma unroll 1
-  for (int k0 = 0; k0 < NP; k0 += 32) {
+  auto kblock = [&](const int k0) {
     f32x16 st = zero16(), dp = zero16();
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -794,6 +796,13 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
 #pragma unroll
       for (int d2 = 0; d2 < 2; ++d2) dqt[d2] = mfma32(frag_tr(kt, k0 + 16 * s, 32 * d2, lane), sb, dqt[d2]);
     }
+  };
+  if constexpr (NWC > 0) {
+#pragma unroll
+    for (int k0 = 0; k0 < NWC * 32; k0 += 32) kblock(k0);
+  } else {
+#pragma unroll 1
+    for (int k0 = 0; k0 < NP; k0 += 32) kblock(k0);
   }
   // dQ through the (now free) K/V image: every wave must be done reading it.  With colsum,
   // also this head's q-bias gradient partial colsum[b][hd*64 ..] (column sums of the stored dQ)
@@ -815,7 +824,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
 // and lse/delta are loaded into registers as soon as the loop is done, under the dK/dV stores
 // (one workgroup per pair left each CU idle during every prologue load).  Queries >= N get
 // L2 = +inf -> P = 0, dS = 0.
-template <int NPMAX>
+template <int NPMAX, int NWC = 0>   // NWC: see attn_bwd_dq_seq_bf16
 __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale,
@@ -826,7 +835,7 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
   __shared__ float red[NPMAX / 32][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = blockDim.x >> 6, NP = nw * 32;
+  const int nw = NWC > 0 ? NWC : blockDim.x >> 6, NP = nw * 32;
   const int D = H * DH;
   const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
   const int h = lane >> 5;
@@ -883,8 +892,7 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     const char* qt = smem[buf];
     const char* dt_ = qt + NP * 128;
     f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
-#pragma unroll 1
-    for (int q0 = 0; q0 < NP; q0 += 32) {
+    auto qblock = [&](const int q0) {
       f32x16 sa = zero16(), dp = zero16();
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -912,6 +920,13 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
           dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
         }
       }
+    };
+    if constexpr (NWC > 0) {
+#pragma unroll
+      for (int q0 = 0; q0 < NWC * 32; q0 += 32) qblock(q0);
+    } else {
+#pragma unroll 1
+      for (int q0 = 0; q0 < NP; q0 += 32) qblock(q0);
     }
     if (more) load_regs(nbh, kf, vf, ls, dv);   // (kf / vf are dead until the next pair)
     // dK, dV through this pair's (now free) Q | dO image: every wave must be done reading it
@@ -1710,12 +1725,19 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
       hipLaunchKernelGGL(attn_bwd_fused_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
                          (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, N, H, scale);
     } else {
-      hipLaunchKernelGGL(attn_bwd_dq_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
-                         (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
       const int npairs = B * H, cus = device_cus();
-      hipLaunchKernelGGL(attn_bwd_dkv_seq_bf16<SEQ_MAX>, dim3(npairs < cus ? npairs : cus), block, 0, s,
-                         (const bf16*)qkv, (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale,
-                         colsum, npairs);
+      const dim3 gkv(npairs < cus ? npairs : cus);
+      if ((N + 31) / 32 == 7) {   // N in (192, 224]: the ViT-B/ViT-S shape, N = 197
+        hipLaunchKernelGGL((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), dim3(B * H), block, 0, s, (const bf16*)qkv,
+                           (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
+        hipLaunchKernelGGL((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), gkv, block, 0, s, (const bf16*)qkv, (const bf16*)dout,
+                           lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
+      } else {
+        hipLaunchKernelGGL((attn_bwd_dq_seq_bf16<SEQ_MAX>), dim3(B * H), block, 0, s, (const bf16*)qkv,
+                           (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
+        hipLaunchKernelGGL((attn_bwd_dkv_seq_bf16<SEQ_MAX>), gkv, block, 0, s, (const bf16*)qkv, (const bf16*)dout,
+                           lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
+      }
       if (colsum_rows) *colsum_rows = colsum ? B : 0;   // one partial row per batch
     }
   } else if (dtype == VITMI_BF16) {
@@ -1753,8 +1775,13 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
       if (!colsum && fused_bwd()) {
         VITMI_STAT(attn_bwd_fused_seq_bf16<SEQ_MAX>, 2 * fl, t * 8 * es + bh * N * 4);
       } else {
-        VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
-        VITMI_STAT(attn_bwd_dkv_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+        if ((N + 31) / 32 == 7) {
+          VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+          VITMI_STAT((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+        } else {
+          VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+          VITMI_STAT(attn_bwd_dkv_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+        }
       }
     } else if (dtype == VITMI_BF16) {
       VITMI_STAT(attn_bwd_dq_bf16, fl, t * 6 * es + bh * N * 8);
