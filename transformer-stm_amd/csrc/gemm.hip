@@ -690,10 +690,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         barrier();                                                                              \
       } while (0)
       // one K-step; FIRST (step 0 of the unit, peeled) starts the accumulators from zero
-      auto kstep = [&](auto first_tag, const int t) {
+      // STEADY: t + 2 < nku is known (both prefetched steps belong to this unit), so the
+      // descriptor / step selects below fold away (≈ 40 scalar instructions per K-step)
+      auto kstep = [&](auto first_tag, auto steady_tag, const int t) {
         constexpr bool FIRST = decltype(first_tag)::value;
+        constexpr bool STEADY = decltype(steady_tag)::value;
         // step t+1 (B1, A1 still to issue, buffer buf^1) and step t+2 (A0, B0, buffer buf)
-        const bool in1 = t + 1 < nku, in2 = t + 2 < nku;
+        const bool in1 = STEADY || t + 1 < nku, in2 = STEADY || t + 2 < nku;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
         const __amdgpu_buffer_rsrc_t a1 = in1 ? ra : ran, b1r = in1 ? rb : rbn;
         const __amdgpu_buffer_rsrc_t a2 = in2 ? ra : ran, b2r = in2 ? rb : rbn;
@@ -732,8 +735,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         COMPUTE(1, 0, ay, b0);
         buf ^= 1;
       };
-      kstep(std::true_type{}, 0);
-      for (int t = 1; t < nku; ++t) kstep(std::false_type{}, t);
+      kstep(std::true_type{}, std::false_type{}, 0);
+      int t = 1;
+      for (; t + 2 < nku; ++t) kstep(std::false_type{}, std::true_type{}, t);
+      for (; t < nku; ++t) kstep(std::false_type{}, std::false_type{}, t);
 #undef COMPUTE
 #undef WAITF
 #undef WAITV
