@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from vitmi import _lib, dp, ops, optim  # noqa: E402
+from vitmi import _lib, dp, ops, optim, trace  # noqa: E402
 from vitmi.config import config_c2, config_c3, config_c5  # noqa: E402
 from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
@@ -154,9 +154,11 @@ def per_kernel_evidence(args, tmp):
         return {"error": "rocprofv3 not found"}
     steps = 3
     stats_json = os.path.join(tmp, "stats.json")
-    cmd = [rp, "--kernel-trace", "--stats", "-d", os.path.join(tmp, "kt"), "-o", "run", "--output-format", "csv",
+    cmd = [rp, "--kernel-trace", "--marker-trace", "--stats", "-d", os.path.join(tmp, "kt"), "-o", "run",
+           "--output-format", "csv",
            "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup", "2",
-           "--config", args.config, "--no-cpu-baseline", "--no-evidence", "--stats-out", stats_json]
+           "--config", args.config, "--no-cpu-baseline", "--no-evidence", "--no-secondary", "--roctx",
+           "--stats-out", stats_json]
     if args.batch:
         cmd += ["--batch", str(args.batch)]
     rc = _run(cmd, 300, log=os.path.join(tmp, "kt.log"))
@@ -202,7 +204,30 @@ def per_kernel_evidence(args, tmp):
     return {"source": "rocprofv3 --kernel-trace of a child run of this bench (3 timed steps after 2 warm-up, "
                       "bracketed by marker kernels); flops/bytes = the library's algorithmic work "
                       "(vitmi_stats_*) of the same launches; mfma_util vs the 2.5 PF bf16 dense peak",
-            "kernel_ms_per_step": round(tot, 3), "kernels": out}
+            "kernel_ms_per_step": round(tot, 3), "kernels": out,
+            "roctx_ranges": _roctx_ranges(tmp, steps)}
+
+
+def _roctx_ranges(tmp, steps):
+    """The child's ROCTx ranges (vitmi_trace_push/pop around forward / backward / all-reduce /
+    optimizer, recorded by rocprofv3 --marker-trace): count per step and mean HOST duration of
+    each (the enqueue time of the phase; its GPU time is the parent's phases_ms)."""
+    files = glob.glob(os.path.join(tmp, "kt", "**", "*marker_api_trace.csv"), recursive=True)
+    if not files:
+        return {"error": "no marker trace"}
+    agg = {}
+    for r in csv.DictReader(open(files[0])):
+        name = r.get("Function") or r.get("Operation") or r.get("Name") or "?"
+        if not name.startswith("vitmi:"):
+            continue
+        try:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+        except (KeyError, ValueError):
+            continue
+        a = agg.setdefault(name, [0, 0.0])
+        a[0] += 1
+        a[1] += d
+    return {k: {"per_step": round(c / (steps + 2), 2), "host_ms_mean": round(t / c, 3)} for k, (c, t) in agg.items()}
 
 
 def traffic_evidence(tmp, M):
@@ -250,9 +275,12 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5, "
                                                              "128 for c2)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--comm", choices=["vitmi", "torch"], default="vitmi",
+    ap.add_argument("--comm", choices=["vitmi", "torch", "gloo"], default="vitmi",
                     help="vitmi: the library's RCCL communicator (vitmi_comm_*, side stream + hipEvent gating); "
-                         "torch: torch.distributed all_reduce (ProcessGroupNCCL)")
+                         "torch: torch.distributed all_reduce (ProcessGroupNCCL); gloo: DIAGNOSTIC leg that runs "
+                         "every multi-rank code path (bootstrap, broadcast, per-rank seeds, barriers, the "
+                         "max-over-ranks time, teardown) with ranks sharing GPUs and gradients averaged through "
+                         "gloo on the host (its timing means nothing)")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="dtype of the gradient all-reduce (bf16 halves the bytes; vitmi comm only)")
     ap.add_argument("--reserve-cus", type=int, default=0,
@@ -265,17 +293,27 @@ def main():
     ap.add_argument("--optimizer", choices=["vitmi", "torch"], default="vitmi",
                     help="vitmi: Keras Adam, one fused launch over the arena (+ bf16 shadow); torch: fused torch Adam")
     ap.add_argument("--stats-out", default=None, help=argparse.SUPPRESS)   # evidence child: work table
+    ap.add_argument("--roctx", action="store_true", help="ROCTx ranges around the step's phases (vitmi.trace)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary C5 / C2 lines (child runs after the headline, N=1 only)")
+    ap.add_argument("--comm-timeout", type=float, default=600.0,
+                    help="seconds before a hung gradient exchange aborts the RCCL communicator (0: off)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     # with the vitmi communicator the process group only bootstraps (rendezvous, TCPStore,
     # barriers, the max-over-ranks time): gloo, so the job holds ONE RCCL communicator
-    backend = "gloo" if args.comm == "vitmi" else "nccl"
+    backend = "nccl" if args.comm == "torch" else "gloo"
+    local_env = int(os.environ.get("LOCAL_RANK", "0"))
+    # the gloo diagnostic leg may put several ranks on one GPU (device_count does not init HIP)
+    gpu = local_env % max(1, torch.cuda.device_count()) if args.comm == "gloo" else local_env
     if world_env > 1:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(gpu)
     rank, world, local = dp.init_from_env(backend)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    if args.roctx:
+        trace.enable()
     cfg = {"c2": config_c2, "c3": config_c3, "c5": config_c5}[args.config]()
     B = args.batch or {"c2": 128, "c3": 256, "c5": 64}[args.config]
     model_name = {"c2": "vit_small_16", "c3": "vit_base_16", "c5": "vit_large_16"}[args.config]
@@ -291,7 +329,7 @@ def main():
     model.reset_parameters(seed=0)
     comm = dp.VitmiComm.from_store(rank, world) if (world > 1 and args.comm == "vitmi") else None
     red = dp.attach(model, bucket_mb=args.bucket_mb, comm=comm, grad_dtype=args.grad_dtype,
-                    reserve_cus=args.reserve_cus if world > 1 else 0)
+                    reserve_cus=args.reserve_cus if world > 1 else 0, timeout_s=args.comm_timeout)
     dp.broadcast_parameters(model, comm=comm)
     if args.optimizer == "vitmi":
         opt = optim.Adam(model, learning_rate=1e-3)     # keras.optimizers.Adam(1e-3), models/CvT(Par).py:458
@@ -306,23 +344,34 @@ def main():
     img = torch.rand(B, cfg.in_chans, cfg.img_size, cfg.img_size, device=dev, generator=g)
     tgt = torch.randint(0, cfg.num_classes, (B,), device=dev, generator=g)
 
-    opt_events = []   # (start, end) around each timed optimizer step (reported separately)
+    phase_events = []   # per timed step: events between the phases (GPU time of each, compute stream)
+    phases = ("forward", "backward", "allreduce_wait", "optimizer")
 
     def step(timed=False):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if timed else None
+        if timed:
+            ev[0].record()
         arena.grad.zero_()
         red.start()
-        logits = model(img)
-        loss = cross_entropy(logits, tgt)
-        loss.backward()
-        red.finish()
+        with trace.range("vitmi:forward"):
+            logits = model(img)
+            loss = cross_entropy(logits, tgt)
+        if timed:
+            ev[1].record()
+        with trace.range("vitmi:backward"):
+            loss.backward()
+        if timed:
+            ev[2].record()
+        with trace.range("vitmi:allreduce"):
+            red.finish()
+        if timed:
+            ev[3].record()
         if not args.no_optimizer:
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            opt.step()
-            if timed:
-                e1.record()
-                opt_events.append((e0, e1))
+            with trace.range("vitmi:optimizer"):
+                opt.step()
+        if timed:
+            ev[4].record()
+            phase_events.append(ev)
         return loss
 
     for _ in range(args.warmup):
@@ -357,6 +406,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
 
+    phases_ms = {p: round(sum(e[i].elapsed_time(e[i + 1]) for e in phase_events) / max(1, len(phase_events)), 3)
+                 for i, p in enumerate(phases)}
     ms_step = elapsed / args.steps * 1e3
     imgs = B * world * args.steps / elapsed
     kern_ms = sum(a.elapsed_time(b) for a, b in events) / max(1, len(events))
@@ -389,8 +440,8 @@ def main():
                      "frac": round(achieved / peak, 4), "traffic": None,
                      "launches_timed": len(events), "avg_launch_ms": round(kern_ms, 4),
                      "algorithmic_bytes": (4 if fp32 else 2) * (M * D + F_ * D + 2 * M * F_)},
-        "optimizer_ms": (round(sum(a.elapsed_time(b) for a, b in opt_events) / len(opt_events), 3)
-                         if opt_events else None),
+        "optimizer_ms": phases_ms.get("optimizer"),
+        "phases_ms": phases_ms,
         "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (peak * world), 4),
         "loss": round(float(loss.item()), 5),
         "build_id": _lib.lib().vitmi_build_id().decode(),
@@ -415,13 +466,43 @@ def main():
         if os.path.isdir(keep):
             shutil.copytree(tmp, os.path.join(keep, "bench_evidence"), dirs_exist_ok=True)
         shutil.rmtree(tmp, ignore_errors=True)
+    if rank == 0 and world == 1 and not args.no_secondary and args.config == "c3" and not args.stats_out:
+        out["secondary"] = secondary_lines()
     if rank == 0:
         print(json.dumps(out), flush=True)
+    red.close()
     if comm is not None:
         comm.destroy()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def secondary_lines():
+    """BASELINE configs 5 (ViT-L/16 384px bs 64, N = 577) and 2 (ViT-S/16 224px bs 128 fp32) on
+    the driver's clock: child runs of this bench after the headline (10 timed steps each); the
+    headline `value` stays C3."""
+    out = {}
+    for cfg in ("c5", "c2"):
+        log = os.path.join(tempfile.gettempdir(), f"vitmi_secondary_{cfg}.log")
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--steps", "10", "--warmup", "3",
+               "--no-evidence", "--no-cpu-baseline", "--no-secondary"]
+        rc = _run(cmd, 300, log=log)
+        line = None
+        if rc == 0:
+            for ln in open(log):
+                if ln.startswith("{"):
+                    line = json.loads(ln)
+        if line is None:
+            out[cfg] = {"error": f"child rc={rc}"}
+            continue
+        out[cfg] = {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "step_mfma_frac", "dtype",
+                                         "phases_ms")}
+        out[cfg]["config"] = line["config"]
+        r = line["roofline"]
+        out[cfg]["dominant_kernel"] = {"kernel": r["kernel"], "avg_launch_ms": r["avg_launch_ms"],
+                                       "achieved_tflops": r["achieved"], "peak": r["peak"], "frac": r["frac"]}
+    return out
 
 
 def _dump_stats(path):

@@ -31,7 +31,7 @@ extern "C" {
 typedef void* vitmi_stream_t; /* hipStream_t */
 
 enum { VITMI_OK = 0, VITMI_ERR_INVALID = 1, VITMI_ERR_HIP = 2, VITMI_ERR_UNSUPPORTED = 3, VITMI_ERR_COMM = 4 };
-enum { VITMI_F32 = 0, VITMI_BF16 = 1 };
+enum { VITMI_F32 = 0, VITMI_BF16 = 1, VITMI_F64 = 2 /* comm only */ };
 
 /* GEMM epilogues (all apply `bias` (fp32, may be NULL) first where it applies) */
 enum {
@@ -45,9 +45,12 @@ enum {
 enum { VITMI_LOSS_CE = 0, VITMI_LOSS_MSE = 1 };
 
 int vitmi_version(void);
-/* content hash of the sources the library was built from (csrc/ + this header), as 16 hex
- * digits; __graft_entry__ compares it with the tree it runs in, so a stale .so is caught */
+/* "<sources>-<flags>": 16 hex digits of the content hash of the sources the library was built
+ * from (csrc/ + this header), then 8 of the hash of its compiler command line
+ * (vitmi_build_flags); __graft_entry__ compares the first part with the tree it runs in, so a
+ * stale .so is caught, and a variant built with other flags or -D switches has another id */
 const char* vitmi_build_id(void);
+const char* vitmi_build_flags(void);
 const char* vitmi_last_error(void);
 /* number of hipDevice compute units seen by the library (0 on error) */
 int vitmi_device_cus(void);
@@ -58,6 +61,12 @@ int vitmi_device_cus(void);
 int vitmi_stats_enable(int on);
 int vitmi_stats_count(void);
 int vitmi_stats_get(int i, char* name, int name_len, int64_t* calls, double* flops, double* bytes);
+/* ROCTx ranges (rocprofv3 --marker-trace): off by default; enabling binds the ROCm marker
+ * library at run time (VITMI_ERR_UNSUPPORTED if absent).  vitmi/trace.py wraps the training
+ * step's forward / backward / all-reduce / optimizer phases in them. */
+int vitmi_trace_enable(int on);
+int vitmi_trace_push(const char* name);
+int vitmi_trace_pop(void);
 
 /* ---------------------------------------------------------------------------
  * Generic MFMA GEMM:  C[M,N] (op)= sum_k A(m,k) * B(k,n)
@@ -65,6 +74,7 @@ int vitmi_stats_get(int i, char* name, int name_len, int64_t* calls, double* flo
  *   b_kmajor=1: B stored [N][ldb] (k contiguous);  0: B stored [K][ldb] (n contiguous)
  *   dtype: operand type (VITMI_BF16 -> v_mfma_f32_16x16x32_bf16, VITMI_F32 -> v_mfma_f32_16x16x4_f32)
  *   c_dtype: output type; aux (the saved GELU derivative gelu'(u)) has the operand dtype.
+ *   BIAS_GELU on bf16 operands writes bf16 (c_dtype VITMI_F32 is rejected).
  *   k-major operands need K % 64 == 0 (bf16) / K % 32 == 0 (f32); ragged M/N and a
  *   ragged reduction over m-major operands are zero-filled by the buffer range check.
  * Replaces the reference's Dense/EinsumDense MatMul and their autodiff transposes
@@ -165,6 +175,7 @@ int vitmi_attention_bwd_bias(int dtype, int B, int N, int H, int dh, float scale
  * Patch embedding Conv2D(k=P, s=P) as a GEMM (models/CvT(Par).py:203-212;
  * old_codes/MS_CvT.py:352-361): im2col of the fp32 NCHW images into
  * patches [B*(S/P)^2][C*P*P] of `dtype` (column order c, kh, kw = the conv weight's).
+ * Limits: S % P == 0, P % 4 == 0, C*P*P <= 4096 (one thread per 4 columns of a patch row).
  */
 int vitmi_patch_im2col(int dtype, int B, int C, int S, int P, const float* img, void* patches,
                        vitmi_stream_t stream);
@@ -177,6 +188,39 @@ int vitmi_tokens_assemble_bwd(int B, int np, int D, const float* dx, float* dtok
                               float* dcls, float* dpos, vitmi_stream_t stream);
 
 /* ---------------------------------------------------------------------------
+ * Per-op entry points under the names of SURVEY.md §8(b) (csrc/boundary.cpp).  Each composes
+ * the kernel-level entry points above on the same stream (bit-identical results) and takes a
+ * caller-owned workspace of at least the queried size.
+ *
+ * vitmi_patch_embed_fwd replaces ConvEmbed.call's Conv2D (models/CvT(Par).py:211-217) plus the
+ * block's cls concat (:264-268) and the position embedding:
+ *   patches (out, saved for the backward) = im2col(img) [B*np][C*P*P] of dtype, np = (S/P)^2;
+ *   x (out, fp32 [B][np+1][D]) = [cls ; patches W^T + bias] + pos   (cls/pos/bias may be NULL);
+ *   w: [D][C*P*P] of dtype (the conv weight flattened).
+ * vitmi_patch_embed_bwd: dW += ..., dbias += ..., dcls += ..., dpos += ... from dx (NULL skips). */
+size_t vitmi_patch_embed_fwd_workspace_size(int dtype, int B, int C, int S, int P, int D);
+int vitmi_patch_embed_fwd(int dtype, int B, int C, int S, int P, int D, const float* img, const void* w,
+                          const float* bias, const float* cls, const float* pos, void* patches, float* x,
+                          void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+size_t vitmi_patch_embed_bwd_workspace_size(int dtype, int B, int C, int S, int P, int D);
+int vitmi_patch_embed_bwd(int dtype, int B, int C, int S, int P, int D, const float* dx, const void* patches,
+                          float* dw, float* dbias, float* dcls, float* dpos, void* workspace, size_t ws_bytes,
+                          vitmi_stream_t stream);
+/* Autodiff of layers.Dense (models/CvT(Par).py:132-134,142,188,254,256): dx = dy W (dx_dtype,
+ * NULL skips), dW += dy^T x, db += column sums of dy (fp32, NULL skips).  dy/x/w of dtype. */
+size_t vitmi_linear_bwd_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
+int vitmi_linear_bwd(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* x, const void* w,
+                     void* dx, int dx_dtype, float* dw, float* db, void* workspace, size_t ws_bytes,
+                     vitmi_stream_t stream);
+/* Losses, mean over the batch: softmax cross-entropy (BASELINE configs, target int64 [B]) and
+ * Keras 'mean_squared_error' (models/CvT(Par).py:464-466, target fp32 [B][C]).  _fwd writes
+ * the scalar loss, _bwd d(loss)/d(logits) [B][C] (upstream gradient 1). */
+int vitmi_xent_fwd(int B, int C, const float* logits, const int64_t* target, float* loss, vitmi_stream_t stream);
+int vitmi_xent_bwd(int B, int C, const float* logits, const int64_t* target, float* dlogits, vitmi_stream_t stream);
+int vitmi_mse_fwd(int B, int C, const float* pred, const float* target, float* loss, vitmi_stream_t stream);
+int vitmi_mse_bwd(int B, int C, const float* pred, const float* target, float* dpred, vitmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------
  * Head (layers.Dense(num_classes) on LN(cls), models/CvT(Par).py:326-329,350) and loss
  * (compile(loss='mean_squared_error') :464-466; softmax-CE for >=2 classes).
  * y: fp32 [B][ldy]; W fp32 [C][D].
@@ -185,7 +229,8 @@ int vitmi_head_fwd(int B, int D, int C, const float* y, int64_t ldy, const float
                    const float* b, float* logits, vitmi_stream_t stream);
 int vitmi_head_bwd(int B, int D, int C, const float* dlogits, const float* y, int64_t ldy,
                    const float* w, float* dy, float* dw, float* db, vitmi_stream_t stream);
-/* loss = mean over batch; dlogits = d loss / d logits.  target: int64 [B] (CE) or f32 [B] (MSE) */
+/* loss = mean over batch; dlogits = d loss / d logits.  target: int64 [B] (CE) or f32 [B] (MSE).
+ * Either output may be NULL (not both). */
 int vitmi_loss_fwd_bwd(int kind, int B, int C, const float* logits, const void* target,
                        float* loss, float* dlogits, vitmi_stream_t stream);
 
@@ -324,7 +369,10 @@ enum { VITMI_REDUCE_SUM = 0, VITMI_REDUCE_AVG = 1 };
 int vitmi_comm_get_unique_id(char* uid /* [VITMI_COMM_UID_BYTES] */);
 int vitmi_comm_init(int rank, int world, const char* uid /* [VITMI_COMM_UID_BYTES] */);
 int vitmi_comm_info(int* rank, int* world);
-/* In-place all-reduce of `count` elements (VITMI_F32 | VITMI_BF16) on the side stream `side`,
+/* file name of the RCCL library the comm leg bound (dladdr of its ncclAllReduce): the copy
+ * torch already mapped, so the process holds one RCCL instance */
+int vitmi_comm_library(char* path, int len);
+/* In-place all-reduce of `count` elements (VITMI_F32 | VITMI_BF16 | VITMI_F64) on the side stream `side`,
  * after `ready_event` (a hipEvent_t recorded on the compute stream, may be NULL).  Returns once
  * enqueued; the caller orders its consumers after `side` (record an event / stream wait). */
 int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, int op, vitmi_stream_t side, void* ready_event);

@@ -21,8 +21,25 @@ static int fails = 0;
   } while (0)
 
 int main(void) {
-  EXPECT(vitmi_version() >= 200);
-  EXPECT(strlen(vitmi_build_id()) == 16);
+  EXPECT(vitmi_version() >= 300);
+  EXPECT(strlen(vitmi_build_id()) >= 17 && vitmi_build_id()[16] == '-');
+  EXPECT(strlen(vitmi_build_flags()) > 0);
+  /* SURVEY §8(b) composites: workspace queries, and validation before any launch */
+  EXPECT(vitmi_patch_embed_fwd_workspace_size(VITMI_BF16, 256, 3, 224, 16, 768) >= (size_t)256 * 196 * 768 * 4);
+  EXPECT(vitmi_patch_embed_bwd_workspace_size(VITMI_BF16, 256, 3, 224, 16, 768) > 0);
+  EXPECT(vitmi_patch_embed_fwd_workspace_size(VITMI_BF16, 2, 3, 30, 8, 64) == 0);
+  EXPECT(vitmi_patch_embed_fwd(VITMI_BF16, 2, 3, 32, 8, 64, (float*)16, (void*)16, NULL, NULL, NULL, (void*)16,
+                               (float*)16, (void*)16, 8, NULL) == VITMI_ERR_INVALID);
+  EXPECT(vitmi_patch_embed_bwd(VITMI_BF16, 2, 3, 32, 8, 64, NULL, (void*)16, NULL, NULL, NULL, NULL, (void*)16,
+                               1 << 30, NULL) == VITMI_ERR_INVALID);
+  EXPECT(vitmi_linear_bwd_workspace_size(VITMI_BF16, 50432, 768, 3072) > 0);
+  EXPECT(vitmi_linear_bwd(VITMI_BF16, 64, 64, 64, (void*)16, (void*)16, (void*)16, (void*)16, VITMI_BF16, NULL,
+                          NULL, (void*)16, 8, NULL) == VITMI_ERR_INVALID);
+  EXPECT(vitmi_xent_fwd(2, 2, (float*)16, (int64_t*)16, NULL, NULL) == VITMI_ERR_INVALID);
+  EXPECT(vitmi_xent_bwd(2, 2, (float*)16, (int64_t*)16, NULL, NULL) == VITMI_ERR_INVALID);
+  EXPECT(vitmi_mse_fwd(2, 1, (float*)16, (float*)16, NULL, NULL) == VITMI_ERR_INVALID);
+  EXPECT(vitmi_mse_bwd(0, 1, (float*)16, (float*)16, (float*)16, NULL) == VITMI_ERR_INVALID);
+  EXPECT(vitmi_trace_push("off") == VITMI_OK && vitmi_trace_pop() == VITMI_OK);   /* disabled: no-ops */
   /* GEMM validation: k-major with K % 64 != 0, null operands, bad dtype, tiny lda */
   EXPECT(vitmi_gemm(VITMI_BF16, 1, 1, 128, 128, 100, (void*)16, 128, (void*)16, 128, (void*)16, 128,
                     VITMI_BF16, VITMI_EPI_STORE, NULL, NULL, 0, NULL, 0, NULL, 0, NULL) == VITMI_ERR_INVALID);

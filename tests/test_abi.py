@@ -57,11 +57,52 @@ def test_argtypes_declared(name):
     assert fn.argtypes is not None and len(fn.argtypes) > 5
 
 
-def test_build_id_matches_sources():
-    """the .so was built from the csrc/ + include/ in this tree (a stale library is caught)"""
+def test_build_id_matches_sources_and_flags():
+    """the .so was built from the csrc/ + include/ in this tree (a stale library is caught), and
+    its id carries the hash of the compiler command line it reports (a -D variant differs)"""
     want = _lib.source_build_id()
     assert want is not None
-    assert _lib.lib().vitmi_build_id().decode() == want
+    src, flags = _lib.build_id_parts(_lib.lib().vitmi_build_id().decode())
+    assert src == want
+    cmd = _lib.lib().vitmi_build_flags().decode()
+    assert "--offload-arch=gfx950" in cmd and flags == _lib.flags_id(cmd)
+
+
+def test_section8b_entry_points_exported():
+    """the boundary exports vitmi_{patch_embed,layernorm,linear,attention,xent,
+    mse}_{fwd,bwd} (+ workspace queries), the comm leg, vitmi_last_error and vitmi_version."""
+    names = set(header_functions())
+    for op in ("patch_embed", "layernorm", "linear", "attention", "xent", "mse"):
+        for d in ("fwd", "bwd"):
+            assert f"vitmi_{op}_{d}" in names, (op, d)
+    for n in ("vitmi_patch_embed_fwd_workspace_size", "vitmi_patch_embed_bwd_workspace_size",
+              "vitmi_linear_bwd_workspace_size", "vitmi_layernorm_bwd_workspace_size",
+              "vitmi_attention_bwd_workspace_size", "vitmi_comm_init", "vitmi_comm_allreduce_async",
+              "vitmi_comm_destroy", "vitmi_last_error", "vitmi_version"):
+        assert n in names, n
+
+
+def test_section8b_host_validation():
+    lib = _lib.lib()
+    # workspace queries are pure host arithmetic
+    n = lib.vitmi_patch_embed_fwd_workspace_size(1, 256, 3, 224, 16, 768)
+    assert n >= 256 * 196 * 768 * 4
+    assert lib.vitmi_patch_embed_bwd_workspace_size(1, 256, 3, 224, 16, 768) >= 256 * 196 * 768 * 2
+    assert lib.vitmi_linear_bwd_workspace_size(1, 50432, 768, 768) >= lib.vitmi_linear_wgrad_workspace_size(
+        1, 50432, 768, 768)
+    # too-small workspaces and bad shapes fail before any launch
+    rc = lib.vitmi_patch_embed_fwd(1, 2, 3, 32, 8, 64, 16, 16, None, None, None, 16, 16, 16, 8, None)
+    assert rc == 1 and b"workspace" in lib.vitmi_last_error()
+    rc = lib.vitmi_patch_embed_fwd(1, 2, 3, 30, 8, 64, 16, 16, None, None, None, 16, 16, 16, 1 << 30, None)
+    assert rc == 1 and b"shape" in lib.vitmi_last_error()
+    rc = lib.vitmi_linear_bwd(1, 64, 64, 64, 16, 16, 16, 16, 1, 16, 16, 16, 8, None)
+    assert rc == 1 and b"workspace" in lib.vitmi_last_error()
+    assert lib.vitmi_xent_fwd(2, 2, 16, 16, None, None) == 1
+    assert lib.vitmi_mse_bwd(2, 1, 16, 16, None, None) == 1
+    # the bf16 GELU epilogue writes bf16: an fp32 C is rejected
+    rc = lib.vitmi_gemm(1, 1, 1, 128, 128, 64, 16, 64, 16, 64, 16, 128, 0, 1, None, 16, 128, None, 0,
+                        None, 0, None)
+    assert rc == 1 and b"GELU" in lib.vitmi_last_error()
 
 
 def test_comm_entry_points_validate_without_a_communicator():

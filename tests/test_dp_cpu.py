@@ -113,3 +113,64 @@ def test_grad_reducer_gloo_world2():
             want = (i + 1) * (0.5 if i == 0 else 1.5)
             assert torch.allclose(torch.from_numpy(g), torch.full(g.shape, want)), i
         assert len(res[r]["uid"]) == dp.UID_BYTES and res[r]["uid"] == res[0]["uid"]
+
+
+# ------------------------------------------------------------------ abort on timeout
+class _Ev:
+    def __init__(self, done):
+        self.done = done
+
+    def query(self):
+        return self.done
+
+
+def test_watchdog_aborts_a_hung_exchange_and_raises():
+    """CommWatchdog: a step's completion event that never fires makes the watchdog call the
+    abort (ncclCommAbort through vitmi_comm_destroy(1) in GradReducer.abort) and the training
+    thread's next check raises instead of hanging."""
+    import time
+
+    from vitmi.dp import CommWatchdog
+    aborted = []
+    wd = CommWatchdog(0.2, lambda: aborted.append(True), poll_s=0.01)
+    try:
+        wd.watch(_Ev(True))                  # finished steps are retired
+        wd.check()
+        wd.watch(_Ev(False))                 # a hung exchange
+        t0 = time.monotonic()
+        while not aborted and time.monotonic() - t0 < 5:
+            time.sleep(0.02)
+        assert aborted == [True]
+        import pytest
+        with pytest.raises(RuntimeError, match="aborted"):
+            wd.check()
+    finally:
+        wd.close()
+
+
+def test_watchdog_quiet_when_exchanges_finish():
+    import time
+
+    from vitmi.dp import CommWatchdog
+    aborted = []
+    wd = CommWatchdog(0.1, lambda: aborted.append(True), poll_s=0.01)
+    try:
+        for _ in range(5):
+            wd.watch(_Ev(True))
+        time.sleep(0.3)
+        wd.check()
+        assert not aborted
+    finally:
+        wd.close()
+
+
+def test_comm_binds_the_rccl_torch_loaded():
+    """The library's RCCL leg binds the librccl.so torch already mapped (dladdr of the bound
+    ncclAllReduce), so a process holds one RCCL instance (csrc/comm.cpp load_rccl)."""
+    import torch  # noqa: F401  (torch maps its RCCL at import)
+
+    from vitmi.dp import VitmiComm
+    mapped = sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "librccl" in ln})
+    assert mapped, "torch did not map an RCCL"
+    bound = VitmiComm.library()
+    assert os.path.realpath(bound) in {os.path.realpath(m) for m in mapped}, (bound, mapped)

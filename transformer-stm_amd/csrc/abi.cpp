@@ -1,4 +1,5 @@
 // abi.cpp — library-level entry points of the C ABI: version, error reporting.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -87,13 +88,61 @@ extern "C" int vitmi_stats_get(int i, char* name, int name_len, int64_t* calls, 
   return VITMI_OK;
 }
 
+// ---- ROCTx ranges (SURVEY.md §5 profiling: ranges around fwd / bwd / all-reduce / optimizer).
+// The ROCm 7 marker library (librocprofiler-sdk-roctx, what `rocprofv3 --marker-trace` records)
+// is bound at run time on the first enable, so the library has no link dependency on it; while
+// disabled (the default) a push/pop is one branch.
+namespace {
+typedef int (*roctx_push_t)(const char*);
+typedef int (*roctx_pop_t)(void);
+roctx_push_t g_roctx_push = nullptr;
+roctx_pop_t g_roctx_pop = nullptr;
+bool g_trace_on = false;
+}  // namespace
+
+extern "C" int vitmi_trace_enable(int on) {
+  if (on && !g_roctx_push) {
+    void* h = nullptr;
+    const char* names[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                           "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"};
+    for (const char* n : names)
+      if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!h) return vitmi::fail(VITMI_ERR_UNSUPPORTED, "trace_enable: cannot load the ROCTx library (%s)", dlerror());
+    g_roctx_push = (roctx_push_t)dlsym(h, "roctxRangePushA");
+    g_roctx_pop = (roctx_pop_t)dlsym(h, "roctxRangePop");
+    if (!g_roctx_push || !g_roctx_pop) {
+      g_roctx_push = nullptr;
+      return vitmi::fail(VITMI_ERR_UNSUPPORTED, "trace_enable: ROCTx library lacks roctxRangePushA/Pop");
+    }
+  }
+  g_trace_on = on != 0;
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_trace_push(const char* name) {
+  if (!g_trace_on) return VITMI_OK;
+  g_roctx_push(name ? name : "?");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_trace_pop(void) {
+  if (!g_trace_on) return VITMI_OK;
+  g_roctx_pop();
+  return VITMI_OK;
+}
+
 #ifndef VITMI_BUILD_ID
 #define VITMI_BUILD_ID "unknown"
 #endif
+#ifndef VITMI_BUILD_FLAGS
+#define VITMI_BUILD_FLAGS "unknown"
+#endif
 
-extern "C" int vitmi_version(void) { return 200; /* 0.2.0: + RCCL comm, build id */ }
+extern "C" int vitmi_version(void) { return 300; /* 0.3.0: + §8(b) per-op entry points, flags in the id */ }
 
 extern "C" const char* vitmi_build_id(void) { return VITMI_BUILD_ID; }
+
+extern "C" const char* vitmi_build_flags(void) { return VITMI_BUILD_FLAGS; }
 
 extern "C" const char* vitmi_last_error(void) { return vitmi::g_err; }
 

@@ -14,6 +14,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <string.h>
 #include "common.h"
 
@@ -71,6 +72,7 @@ int nccl_fail(const char* what, ncclResult_t r) {
 bool dtype_of(int dtype, ncclDataType_t& t) {
   if (dtype == VITMI_F32) t = ncclFloat32;
   else if (dtype == VITMI_BF16) t = ncclBfloat16;
+  else if (dtype == VITMI_F64) t = ncclFloat64;
   else return false;
   return true;
 }
@@ -103,6 +105,16 @@ extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
   g_comm = c;
   g_rank = rank;
   g_world = world;
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_comm_library(char* path, int len) {
+  VITMI_CHECK_ARG(path != nullptr && len > 0, "comm_library: bad buffer");
+  if (int rc = load_rccl()) return rc;
+  Dl_info info;
+  if (!dladdr(reinterpret_cast<void*>(g_rccl.all_reduce), &info) || !info.dli_fname)
+    return fail(VITMI_ERR_COMM, "comm_library: dladdr(ncclAllReduce) failed");
+  snprintf(path, (size_t)len, "%s", info.dli_fname);
   return VITMI_OK;
 }
 

@@ -257,13 +257,14 @@ __global__ void loss_kernel(int kind, int B, int C, const float* __restrict__ lo
       for (int c = 0; c < C; ++c) se += expf(z[c] - mx);
       const float lse = mx + logf(se);
       acc += lse - z[t];
-      for (int c = 0; c < C; ++c) dl[(int64_t)b * C + c] = (expf(z[c] - lse) - (c == t ? 1.f : 0.f)) * invB;
+      if (dl)
+        for (int c = 0; c < C; ++c) dl[(int64_t)b * C + c] = (expf(z[c] - lse) - (c == t ? 1.f : 0.f)) * invB;
     } else {  // MSE over all outputs (Keras mean_squared_error, C == 1 for the reference)
       const float* t = (const float*)target + (int64_t)b * C;
       for (int c = 0; c < C; ++c) {
         const float d = z[c] - t[c];
         acc += d * d / C;
-        dl[(int64_t)b * C + c] = 2.f * d * invB / C;
+        if (dl) dl[(int64_t)b * C + c] = 2.f * d * invB / C;
       }
     }
   }
@@ -273,7 +274,7 @@ __global__ void loss_kernel(int kind, int B, int C, const float* __restrict__ lo
     if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) loss[0] = red[0] * invB;
+  if (threadIdx.x == 0 && loss) loss[0] = red[0] * invB;
 }
 
 __global__ void cast_kernel(int64_t n, const float* __restrict__ src, bf16* __restrict__ dst) {
@@ -448,10 +449,10 @@ extern "C" int vitmi_head_bwd(int B, int D, int C, const float* dlogits, const f
                               const float* w, float* dy, float* dw, float* db,
                               vitmi_stream_t stream) {
   VITMI_CHECK_ARG(dlogits && y && w && dy && dw, "head_bwd: bad arguments");
+  VITMI_CHECK_ARG(C <= 65535, "head_bwd: at most 65535 classes");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(head_bwd_dy_kernel, dim3((unsigned)(((int64_t)B * D + 255) / 256)), dim3(256), 0, s,
                      B, D, C, dlogits, w, dy);
-  VITMI_CHECK_ARG(C <= 65535, "head_bwd: at most 65535 classes");
   hipLaunchKernelGGL(head_bwd_dw_kernel, dim3((unsigned)((D + 63) / 64), (unsigned)C), dim3(1024), 0, s,
                      B, D, C, dlogits, y, ldy, dw, db);
   VITMI_LAUNCH_CHECK("head_bwd");
@@ -461,7 +462,7 @@ extern "C" int vitmi_head_bwd(int B, int D, int C, const float* dlogits, const f
 extern "C" int vitmi_loss_fwd_bwd(int kind, int B, int C, const float* logits, const void* target,
                                   float* loss, float* dlogits, vitmi_stream_t stream) {
   VITMI_CHECK_ARG(kind == VITMI_LOSS_CE || kind == VITMI_LOSS_MSE, "loss: bad kind %d", kind);
-  VITMI_CHECK_ARG(logits && target && loss && dlogits && B > 0 && C > 0, "loss: bad arguments");
+  VITMI_CHECK_ARG(logits && target && (loss || dlogits) && B > 0 && C > 0, "loss: bad arguments");
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, kind, B, C, logits, target,
                      loss, dlogits);
   VITMI_LAUNCH_CHECK("loss");

@@ -1301,8 +1301,11 @@ static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits
       return cbf ? launch_layout<T, VITMI_EPI_STORE, bf16>(ak, bk, g, splits, big, s)
                  : launch_layout<T, VITMI_EPI_STORE, float>(ak, bk, g, splits, big, s);
     case VITMI_EPI_BIAS_GELU:
-      return cbf ? launch_layout<T, VITMI_EPI_BIAS_GELU, bf16>(ak, bk, g, splits, big, s)
-                 : launch_layout<T, VITMI_EPI_BIAS_GELU, float>(ak, bk, g, splits, big, s);
+      // bf16 operands: the GELU epilogue writes bf16 (activation and gelu'); gemm_impl rejects
+      // an fp32 C, so that variant is not instantiated
+      if constexpr (std::is_same<T, bf16>::value) return launch_layout<T, VITMI_EPI_BIAS_GELU, bf16>(ak, bk, g, splits, big, s);
+      else return cbf ? launch_layout<T, VITMI_EPI_BIAS_GELU, bf16>(ak, bk, g, splits, big, s)
+                      : launch_layout<T, VITMI_EPI_BIAS_GELU, float>(ak, bk, g, splits, big, s);
     case VITMI_EPI_RESIDUAL:
       return launch_layout<T, VITMI_EPI_RESIDUAL, float>(ak, bk, g, splits, big, s);
     case VITMI_EPI_DGELU:
@@ -1314,8 +1317,9 @@ static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits
       return launch_layout<T, EPI_PARTIAL, float>(ak, bk, g, splits, big, s);
     case EPI_GELU_DROP:   // forward linear layers only: x and W both k-major
       if (!(ak && bk)) break;
-      return cbf ? launch_t<T, true, true, EPI_GELU_DROP, bf16>(g, splits, big, s)
-                 : launch_t<T, true, true, EPI_GELU_DROP, float>(g, splits, big, s);
+      if constexpr (std::is_same<T, bf16>::value) return launch_t<T, true, true, EPI_GELU_DROP, bf16>(g, splits, big, s);
+      else return cbf ? launch_t<T, true, true, EPI_GELU_DROP, bf16>(g, splits, big, s)
+                      : launch_t<T, true, true, EPI_GELU_DROP, float>(g, splits, big, s);
     case EPI_RESIDUAL_DROP:
       if (!(ak && bk)) break;
       return launch_t<T, true, true, EPI_RESIDUAL_DROP, float>(g, splits, big, s);
@@ -1360,6 +1364,8 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   if (eb == VITMI_EPI_RESIDUAL) VITMI_CHECK_ARG(residual != nullptr && ldr >= N, "gemm: residual missing");
   if (eb == VITMI_EPI_RESIDUAL || eb == VITMI_EPI_ACCUM)
     VITMI_CHECK_ARG(c_dtype == VITMI_F32, "gemm: residual/accum epilogues write fp32");
+  if (eb == VITMI_EPI_BIAS_GELU && dtype == VITMI_BF16)
+    VITMI_CHECK_ARG(c_dtype == VITMI_BF16, "gemm: the bias+GELU epilogue on bf16 operands writes bf16");
   // 32-bit buffer offsets: one block's panel must stay under 2 GiB
   VITMI_CHECK_ARG((ak ? 128 * lda : K * lda) * es < 0x7fffffffLL, "gemm: A panel exceeds 2 GiB");
 

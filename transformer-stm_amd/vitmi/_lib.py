@@ -29,6 +29,7 @@ U = ctypes.c_uint32
 SIGNATURES = {
     "vitmi_version": (I, []),
     "vitmi_build_id": (ctypes.c_char_p, []),
+    "vitmi_build_flags": (ctypes.c_char_p, []),
     "vitmi_last_error": (ctypes.c_char_p, []),
     "vitmi_device_cus": (I, []),
     "vitmi_gemm": (I, [I, I, I, L, L, L, P, L, P, L, P, L, I, I, P, P, L, P, L, P, S, P]),
@@ -80,15 +81,29 @@ SIGNATURES = {
     "vitmi_stats_enable": (I, [I]),
     "vitmi_stats_count": (I, []),
     "vitmi_stats_get": (I, [I, P, I, P, P, P]),
+    "vitmi_trace_enable": (I, [I]),
+    "vitmi_trace_push": (I, [ctypes.c_char_p]),
+    "vitmi_trace_pop": (I, []),
     "vitmi_attention_set_policy": (I, [I]),
     "vitmi_gemm_set_reserved_cus": (I, [I]),
     "vitmi_comm_get_unique_id": (I, [P]),
     "vitmi_comm_init": (I, [I, I, P]),
     "vitmi_comm_info": (I, [P, P]),
+    "vitmi_comm_library": (I, [P, I]),
     "vitmi_comm_allreduce_async": (I, [P, L, I, I, P, P]),
     "vitmi_comm_broadcast": (I, [P, L, I, I, P]),
     "vitmi_comm_check": (I, []),
     "vitmi_comm_destroy": (I, [I]),
+    "vitmi_patch_embed_fwd_workspace_size": (S, [I, I, I, I, I, I]),
+    "vitmi_patch_embed_fwd": (I, [I, I, I, I, I, I, P, P, P, P, P, P, P, P, S, P]),
+    "vitmi_patch_embed_bwd_workspace_size": (S, [I, I, I, I, I, I]),
+    "vitmi_patch_embed_bwd": (I, [I, I, I, I, I, I, P, P, P, P, P, P, P, S, P]),
+    "vitmi_linear_bwd_workspace_size": (S, [I, L, L, L]),
+    "vitmi_linear_bwd": (I, [I, L, L, L, P, P, P, P, I, P, P, P, S, P]),
+    "vitmi_xent_fwd": (I, [I, I, P, P, P, P]),
+    "vitmi_xent_bwd": (I, [I, I, P, P, P, P]),
+    "vitmi_mse_fwd": (I, [I, I, P, P, P, P]),
+    "vitmi_mse_bwd": (I, [I, I, P, P, P, P]),
 }
 
 _lib = None
@@ -120,10 +135,22 @@ def exported_symbols():
     return list(SIGNATURES)
 
 
+def build_id_parts(build_id: str):
+    """vitmi_build_id() = "<sources>-<flags>" -> (sources, flags) hashes."""
+    src, _, flags = build_id.partition("-")
+    return src, flags
+
+
+def flags_id(flags: str) -> str:
+    """The flags part of the build id: first 8 hex digits of sha256(vitmi_build_flags())."""
+    import hashlib
+    return hashlib.sha256(flags.encode()).hexdigest()[:8]
+
+
 def source_build_id():
-    """The build id the Makefile stamps into the library (vitmi_build_id): sha256 over the bytes
-    of csrc/*.{cpp,h,hip} (sorted by path) followed by include/vitmi.h, first 16 hex digits.
-    None when the sources are not present next to the package."""
+    """The sources part of the build id the Makefile stamps into the library (vitmi_build_id):
+    sha256 over the bytes of csrc/*.{cpp,h,hip} (sorted by path) followed by include/vitmi.h,
+    first 16 hex digits.  None when the sources are not present next to the package."""
     import glob
     import hashlib
     pkg = os.path.dirname(_HERE)

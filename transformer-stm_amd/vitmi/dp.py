@@ -30,13 +30,16 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
+import time
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
 UID_BYTES = 128
-_F32, _BF16 = 0, 1
+_F32, _BF16, _F64 = 0, 1, 2
+_DT = {torch.float32: _F32, torch.bfloat16: _BF16, torch.float64: _F64}
 REDUCE_SUM, REDUCE_AVG = 0, 1
 
 
@@ -66,8 +69,8 @@ class VitmiComm:
 
     def allreduce_async(self, buf: torch.Tensor, side: "torch.cuda.Stream", ready=None, op: int = REDUCE_AVG) -> None:
         from ._lib import check, lib
-        assert buf.is_cuda and buf.is_contiguous() and buf.dtype in (torch.float32, torch.bfloat16)
-        dt = _F32 if buf.dtype == torch.float32 else _BF16
+        assert buf.is_cuda and buf.is_contiguous() and buf.dtype in _DT
+        dt = _DT[buf.dtype]
         check(lib().vitmi_comm_allreduce_async(buf.data_ptr(), buf.numel(), dt, op, side.cuda_stream,
                                                ready.cuda_event if ready is not None else None),
               "comm_allreduce_async")
@@ -81,6 +84,18 @@ class VitmiComm:
     def check(self) -> None:
         from ._lib import check, lib
         check(lib().vitmi_comm_check(), "comm_check")
+
+    @property
+    def live(self) -> bool:
+        return self._live
+
+    @staticmethod
+    def library() -> str:
+        """File name of the RCCL the comm leg bound (the copy torch mapped, not a second one)."""
+        from ._lib import check, lib
+        buf = ctypes.create_string_buffer(4096)
+        check(lib().vitmi_comm_library(buf, 4096), "comm_library")
+        return buf.value.decode()
 
     def destroy(self, abort: bool = False) -> None:
         if self._live:
@@ -105,11 +120,78 @@ def exchange_unique_id(rank: int, world: int, store=None, key: str = "vitmi_comm
     return uid
 
 
+class CommWatchdog:
+    """Abort-on-timeout for the RCCL leg ("an ncclCommAbort path on timeout").
+
+    ``watch(event)`` hands over a HIP event recorded on the comm side stream behind a step's last
+    all-reduce.  A daemon thread polls the events (``query()`` never blocks); if one is not done
+    ``timeout_s`` after it was handed over -- a peer died or hangs, so RCCL's kernels never
+    finish -- it calls ``on_timeout()`` (the reducer's abort: ``ncclCommAbort`` through
+    ``vitmi_comm_destroy(1)``, which lets the stuck kernels exit and the streams drain) and
+    records the failure; ``check()`` raises it in the training thread."""
+
+    def __init__(self, timeout_s: float, on_timeout: Callable[[], None], poll_s: float = 0.05):
+        self.timeout_s = float(timeout_s)
+        self.poll_s = poll_s
+        self._on_timeout = on_timeout
+        self._pending: List[Tuple[object, float]] = []
+        self._lock = threading.Lock()
+        self._wake = threading.Event()
+        self._stop = False
+        self.error: Optional[str] = None
+        self._thread = threading.Thread(target=self._run, name="vitmi-comm-watchdog", daemon=True)
+        self._thread.start()
+
+    def watch(self, event) -> None:
+        with self._lock:
+            self._pending.append((event, time.monotonic() + self.timeout_s))
+        self._wake.set()
+
+    def check(self) -> None:
+        if self.error is not None:
+            raise RuntimeError(self.error)
+
+    def close(self) -> None:
+        self._stop = True
+        self._wake.set()
+        self._thread.join(timeout=5)
+
+    def _run(self) -> None:
+        while not self._stop and self.error is None:
+            with self._lock:
+                pend = list(self._pending)
+            if not pend:
+                self._wake.wait(1.0)
+                self._wake.clear()
+                continue
+            done = 0
+            for ev, deadline in pend:
+                if ev.query():
+                    done += 1
+                    continue
+                if time.monotonic() > deadline:
+                    self.error = (f"vitmi comm: gradient all-reduce not finished after {self.timeout_s:g} s "
+                                  "(peer failure or hang); communicator aborted")
+                    try:
+                        self._on_timeout()
+                    finally:
+                        return
+                break                      # events complete in order: wait for this one
+            with self._lock:
+                del self._pending[:done]
+            time.sleep(self.poll_s)
+
+
 class GradReducer:
-    """Bucketed, overlapped all-reduce (mean) over one flat gradient buffer."""
+    """Bucketed, overlapped all-reduce (mean) over one flat gradient buffer.
+
+    ``timeout_s`` (vitmi RCCL leg): a step whose exchange has not finished that long after
+    ``finish()`` aborts the communicator (CommWatchdog) and the next ``start()``/``finish()``
+    raises; 0 disables the watchdog."""
 
     def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 64.0, group=None,
-                 comm: Optional[VitmiComm] = None, grad_dtype: str = "fp32", reserve_cus: int = 0):
+                 comm: Optional[VitmiComm] = None, grad_dtype: str = "fp32", reserve_cus: int = 0,
+                 timeout_s: float = 600.0):
         self.flat = flat_grad
         self.group = group
         self.comm = comm
@@ -137,9 +219,30 @@ class GradReducer:
                     if comm is not None and grad_dtype == "bf16" else None)
         self._prev_reserve: Optional[int] = None
         self.launch_log: List[Tuple[int, int]] = []   # (ready prefix, bucket index) for tests
+        self.watchdog = (CommWatchdog(timeout_s, self.abort)
+                         if comm is not None and timeout_s and timeout_s > 0 else None)
+
+    def _restore_reserve(self) -> None:
+        if self._prev_reserve is not None:
+            from ._lib import lib
+            lib().vitmi_gemm_set_reserved_cus(self._prev_reserve)
+            self._prev_reserve = None
+
+    def abort(self) -> None:
+        """Tear down after a failure: give the persistent GEMM its CUs back and abort the RCCL
+        communicator without waiting for peers (vitmi_comm_destroy(1) -> ncclCommAbort)."""
+        self._restore_reserve()
+        if self.comm is not None and self.comm.live:
+            self.comm.destroy(abort=True)
+
+    def close(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.close()
 
     def start(self) -> None:
         """Call before the backward of every step."""
+        if self.watchdog is not None:
+            self.watchdog.check()
         self._next, self._ready, self._handles = 0, 0, []
         self.launch_log = []
         if self._active and self.reserve_cus > 0 and self._prev_reserve is None:
@@ -180,20 +283,26 @@ class GradReducer:
     def finish(self) -> None:
         if not self._active:
             return
-        while self._next < len(self.bounds):
-            self._launch()
-        if self.comm is not None:
-            # the optimizer (on the compute stream) runs after every bucket's exchange
-            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
-        for h, buf in self._handles:
-            h.wait()   # nccl: the current (compute) stream waits on the RCCL stream
-            if self.backend != "nccl":
-                buf.div_(self.world)
-        self._handles = []
-        if self._prev_reserve is not None:
-            from ._lib import lib
-            lib().vitmi_gemm_set_reserved_cus(self._prev_reserve)
-            self._prev_reserve = None
+        try:
+            if self.watchdog is not None:
+                self.watchdog.check()
+            while self._next < len(self.bounds):
+                self._launch()
+            if self.comm is not None:
+                # the optimizer (on the compute stream) runs after every bucket's exchange
+                torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
+                if self.watchdog is not None:
+                    done = torch.cuda.Event()
+                    done.record(self._side)
+                    self.watchdog.watch(done)
+                self.comm.check()          # asynchronous RCCL errors surface here, not as a hang
+            for h, buf in self._handles:
+                h.wait()   # nccl: the current (compute) stream waits on the RCCL stream
+                if self.backend != "nccl":
+                    buf.div_(self.world)
+            self._handles = []
+        finally:
+            self._restore_reserve()
 
 
 class ParamGradReducer:
@@ -264,10 +373,11 @@ def broadcast_module(model: torch.nn.Module, src: int = 0, group=None, comm: Opt
 
 
 def attach(model, bucket_mb: float = 64.0, group=None, comm: Optional[VitmiComm] = None,
-           grad_dtype: str = "fp32", reserve_cus: int = 0) -> GradReducer:
+           grad_dtype: str = "fp32", reserve_cus: int = 0, timeout_s: float = 600.0) -> GradReducer:
     """Wire a GradReducer to a vitmi VisionTransformer's arena and backward hooks."""
     arena = model.arena()
-    red = GradReducer(arena.grad, bucket_mb, group, comm=comm, grad_dtype=grad_dtype, reserve_cus=reserve_cus)
+    red = GradReducer(arena.grad, bucket_mb, group, comm=comm, grad_dtype=grad_dtype, reserve_cus=reserve_cus,
+                      timeout_s=timeout_s)
 
     def end_of(params: Sequence[torch.nn.Parameter]) -> int:
         return max(arena.offsets[id(p)] + p.numel() for p in params)

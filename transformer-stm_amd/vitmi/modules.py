@@ -35,9 +35,14 @@ from .config import ViTConfig
 Tensor = torch.Tensor
 F32 = torch.float32
 
-# bf16 copies of dx produced by a backward, keyed by the fp32 tensor's address, so
-# the next backward up the chain does not re-cast its incoming gradient.
-_LP_STASH: Dict[int, Tensor] = {}
+# A backward that already holds a bf16 copy of the gradient it returns (the LayerNorm backward
+# writes both) hands it to the next backward up the chain as an attribute of the returned
+# tensor object, so that backward does not re-cast its incoming gradient.  The copy lives and
+# dies with that tensor object (no address-keyed table that a later allocation could alias),
+# and it is used only while the tensor is unmodified: autograd may accumulate another gradient
+# into it in place, which bumps its version counter.
+_LP_ATTR = "_vitmi_lp"
+LP_STATS = {"hit": 0, "miss": 0}     # test hook: how often the handed-over copy was used
 
 
 def _drop_args(mod: nn.Module, rate: float, site0: int):
@@ -68,18 +73,28 @@ def _lp(mod: nn.Module, p: Tensor, T: torch.dtype) -> Tensor:
     return ops.cast_bf16(p.detach().contiguous())
 
 
-def _take_lp(g: Tensor, T: torch.dtype) -> Tensor:
+def _take_lp(g: Tensor, T: torch.dtype, src: Optional[Tensor] = None) -> Tensor:
+    """``g`` (fp32, contiguous) in the compute dtype.  ``src`` is the tensor object autograd
+    passed in (``g`` may be a view of it): its handed-over bf16 copy is used when it is still
+    current, otherwise ``g`` is cast."""
     if T == F32:
         return g
-    lp = _LP_STASH.pop(g.data_ptr(), None)
-    if lp is not None and lp.shape == g.shape:
-        return lp
+    src = g if src is None else src
+    ent = src.__dict__.pop(_LP_ATTR, None)
+    if ent is not None:
+        lp, version, ptr = ent
+        if src._version == version and src.data_ptr() == ptr and lp.numel() == g.numel() and lp.dtype == T:
+            LP_STATS["hit"] += 1
+            return lp.view(g.shape)
+    LP_STATS["miss"] += 1
     return ops.cast_bf16(g.contiguous())
 
 
-def _stash(g: Tensor, lp: Optional[Tensor]) -> None:
+def _handover(g: Tensor, lp: Optional[Tensor]) -> Tensor:
+    """Attach the bf16 copy ``lp`` of ``g`` to the tensor object a backward returns."""
     if lp is not None:
-        _LP_STASH[g.data_ptr()] = lp
+        g.__dict__[_LP_ATTR] = (lp, g._version, g.data_ptr())
+    return g
 
 
 def _check_cuda(x: Tensor):
@@ -197,7 +212,7 @@ class _AttentionFn(torch.autograd.Function):
         mod, (B, N, D) = ctx.mod, ctx.shape
         T = xo.dtype
         g = dy.contiguous().float().view(B * N, D)
-        g_lp = _take_lp(g, T)
+        g_lp = _take_lp(g, T, dy)
         do = ops.linear_dgrad(g_lp, wo, T)
         ops.linear_wgrad(g_lp, o, _grad(mod.proj.weight))
         ops.bias_grad(g_lp, _grad(mod.proj.bias))
@@ -242,7 +257,7 @@ class _MlpFn(torch.autograd.Function):
         mod = ctx.mod
         T = xo.dtype
         g = dy.contiguous().float().view(-1, dy.shape[-1])
-        g_lp = _take_lp(g, T)
+        g_lp = _take_lp(g, T, dy)
         du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mod.fc1.bias))
         ops.linear_wgrad(g_lp, a, _grad(mod.fc2.weight))
         ops.bias_grad(g_lp, _grad(mod.fc2.bias))
@@ -277,11 +292,12 @@ class Block(nn.Module):
 
     def forward(self, x: Tensor, h: Optional[int] = None, w: Optional[int] = None) -> Tensor:
         _check_cuda(x)
-        return _BlockFn.apply(x, self, None, False, _drop_args(self, self.drop_rate, 0), *self.parameters())
+        return _BlockFn.apply(x, self, None, False, _drop_args(self, self.drop_rate, 0), False, *self.parameters())
 
 
 class _BlockFn(torch.autograd.Function):
-    """Fused block.  ``prev_fc2_bias``: the fc2 bias of the block feeding this one; its grad is
+    """Fused block.  ``first``: the block fed by the patch embedding (its input gradient is
+    not needed in bf16).  ``prev_fc2_bias``: the fc2 bias of the block feeding this one; its grad is
     colsum(d input), produced for free by this block's LN1 backward.  ``fc2_bias_done``: this
     block's own fc2 bias grad was already accumulated by its consumer (next block or head).
     ``drop``: (seed, rate, site0) -> training-mode dropout (models/CvT(Par).py:189,255,257) at
@@ -289,13 +305,12 @@ class _BlockFn(torch.autograd.Function):
     epilogues; the backward regenerates the masks (vitmi_dropout_apply)."""
 
     @staticmethod
-    def forward(ctx, x, blk, prev_fc2_bias, fc2_bias_done, drop, *params):
+    def forward(ctx, x, blk, prev_fc2_bias, fc2_bias_done, drop, first, *params):
         T = ops.torch_dtype(blk.dtype)
         B, N, D = x.shape
         M = B * N
         H = blk.attn.num_heads
-        x2 = x.contiguous().view(M, D)
-        assert x2.dtype == F32
+        x2 = x.contiguous().float().view(M, D)
         n1, n2 = blk.norm1, blk._norm2
         a_ = blk.attn
         wq, wo = _lp(blk, a_.qkv.weight, T), _lp(blk, a_.proj.weight, T)
@@ -314,6 +329,7 @@ class _BlockFn(torch.autograd.Function):
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
         ctx.blk, ctx.shape = blk, (B, N, D)
         ctx.prev_bias, ctx.bias_done, ctx.drop = prev_fc2_bias, fc2_bias_done, drop
+        ctx.first = first
         return out.view(B, N, D)
 
     @staticmethod
@@ -325,13 +341,13 @@ class _BlockFn(torch.autograd.Function):
         lpT = None if T == F32 else T
         n1, n2 = blk.norm1, blk._norm2
         a_, mlp = blk.attn, blk.mlp
-        g2 = dout.contiguous().view(M, D)
+        g2 = dout.contiguous().float().view(M, D)
         drop = ctx.drop
         if drop is None:
-            g2_lp = _take_lp(g2, T)
+            g2_lp = _take_lp(g2, T, dout)
         else:
             # the fc2 branch was dropped: its dgrad/wgrad/bias see g2 * mask / (1 - p)
-            _LP_STASH.pop(g2.data_ptr(), None)
+            dout.__dict__.pop(_LP_ATTR, None)
             seed, rate, site0 = drop
             g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
         # MLP branch
@@ -362,14 +378,17 @@ class _BlockFn(torch.autograd.Function):
         ops.linear_wgrad(dqkv, h1, _grad(a_.qkv.weight))
         dh1 = ops.linear_dgrad(dqkv, wq, T)
         prev = ctx.prev_bias
+        # the bf16 copy of dx is for a consumer that takes it (the block below); the patch
+        # embedding's backward reads dx in fp32
+        want_lp = drop is None and not ctx.first
         dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
-                                      dres=dx1, lp_dtype=lpT if drop is None else None,
+                                      dres=dx1, lp_dtype=lpT if want_lp else None,
                                       dxsum=_grad(prev) if prev is not None else None)
-        _stash(dx, dx_lp)
         hook = getattr(blk, "_grad_ready_hook", None)
         if hook is not None:
             hook(blk)
-        return (dx.view(B, N, D), None, None, None) + (None,) * (len(ctx.needs_input_grad) - 4)
+        out = _handover(dx.view(B, N, D), dx_lp)
+        return (out, None, None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 6)
 
 
 # ======================================================================= embedding
@@ -404,18 +423,22 @@ class _EmbedFn(torch.autograd.Function):
         G = S // P
         np_ = G * G
         D = emb.proj.weight.shape[0]
-        patches = ops.patch_im2col(img.contiguous().float(), P, T)
         w = _lp(emb, emb.proj.weight, T).reshape(D, -1)
-        conv = ops.linear_fwd(patches, w, emb.proj.bias, F32)
-        saved = [patches]
-        if emb.norm is not None:
+        cls_ = cls.detach().reshape(-1) if cls is not None else None
+        pos_ = pos.detach().reshape(-1) if pos is not None else None
+        if emb.norm is None:
+            # the §8(b) entry point: im2col -> patch GEMM (+bias) -> cls concat + pos-embed
+            x, patches = ops.patch_embed_fwd(img.contiguous().float(), w, emb.proj.bias, cls_, pos_, P, T)
+            saved = [patches]
+        else:
+            patches = ops.patch_im2col(img.contiguous().float(), P, T)
+            conv = ops.linear_fwd(patches, w, emb.proj.bias, F32)
             y, mean, rstd = ops.layernorm_fwd(conv, emb.norm.weight, emb.norm.bias, emb.norm.eps, F32)
-            saved += [conv, mean, rstd]
-            conv = y
-        x = ops.tokens_assemble(conv, B, np_, cls.detach().reshape(-1) if cls is not None else None,
-                                pos.detach().reshape(-1) if pos is not None else None)
+            saved = [patches, conv, mean, rstd]
+            x = ops.tokens_assemble(y, B, np_, cls_, pos_)
         ctx.save_for_backward(*saved)
         ctx.emb, ctx.cls, ctx.pos, ctx.dims = emb, cls, pos, (B, np_, D)
+        ctx.img_shape = (B, C, S, P)
         return x
 
     @staticmethod
@@ -434,11 +457,12 @@ class _EmbedFn(torch.autograd.Function):
             dconv, dconv_lp = ops.layernorm_bwd(dy, conv, mean, rstd, emb.norm.weight,
                                                 _grad(emb.norm.weight), _grad(emb.norm.bias), lp_dtype=lpT)
             g = dconv_lp if dconv_lp is not None else dconv
+            ops.linear_wgrad(g, patches, _grad(emb.proj.weight).view(D, -1))
+            ops.bias_grad(g, _grad(emb.proj.bias))
         else:
-            dtok, dtok_lp = ops.tokens_assemble_bwd(dx, B, np_, T == F32, lpT, dcls, dpos)
-            g = dtok_lp if dtok_lp is not None else dtok
-        ops.linear_wgrad(g, patches, _grad(emb.proj.weight).view(D, -1))
-        ops.bias_grad(g, _grad(emb.proj.bias))
+            Bi, C, S, P = ctx.img_shape
+            ops.patch_embed_bwd(dx, patches, Bi, C, S, P, _grad(emb.proj.weight).view(D, -1),
+                                _grad(emb.proj.bias), dcls, dpos)
         hook = getattr(emb, "_grad_ready_hook", None)
         if hook is not None:
             hook(emb)
@@ -462,7 +486,6 @@ class _HeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dlogits):
-        _LP_STASH.clear()
         x, y, mean, rstd = ctx.saved_tensors
         model = ctx.model
         norm, head = model.norm, model.head
@@ -478,7 +501,7 @@ class _HeadFn(torch.autograd.Function):
                           dx=dx[:, 0], dxsum=_grad(last_fc2_bias) if last_fc2_bias is not None else None,
                           lp_dtype=None if lp is None else T,
                           dx_lp=None if lp is None else lp.view(x.shape[0], x.shape[1], x.shape[2])[:, 0])
-        _stash(dx, lp)
+        _handover(dx, lp)
         hook = getattr(model, "_head_ready_hook", None)
         if hook is not None:
             hook()
@@ -676,7 +699,7 @@ class VisionTransformer(nn.Module):
         for i, blk in enumerate(self.blocks):
             prev_bias = self.blocks[i - 1].mlp.fc2.bias if i > 0 and drop is None else None
             d = None if drop is None else (drop[0], drop[1], 3 * i)
-            t = _BlockFn.apply(t, blk, prev_bias, drop is None, d, *blk.parameters())
+            t = _BlockFn.apply(t, blk, prev_bias, drop is None, d, i == 0, *blk.parameters())
         return t
 
     def forward(self, x: Tensor) -> Tensor:

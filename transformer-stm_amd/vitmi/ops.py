@@ -307,6 +307,73 @@ def tokens_assemble_bwd(dx: Tensor, B: int, np_: int, want_f32: bool, lp_dtype: 
     return dtok, dtok_lp
 
 
+# ---------------------------------------------------------------- §8(b) per-op entry points
+def patch_embed_fwd(img: Tensor, w: Tensor, bias: Optional[Tensor], cls: Optional[Tensor], pos: Optional[Tensor],
+                    P: int, dtype: torch.dtype):
+    """vitmi_patch_embed_fwd: Conv2D(k=P, s=P) + cls + pos -> (x fp32 [B, np+1, D], patches
+    [B*np, C*P*P] of dtype, saved for the backward).  w: [D, C*P*P] of dtype."""
+    B, C, S, S2 = img.shape
+    assert S == S2 and img.dtype == torch.float32 and img.is_contiguous()
+    D = w.shape[0]
+    assert w.is_contiguous() and w.dtype == dtype and w.shape[1] == C * P * P
+    G = S // P
+    patches = torch.empty(B * G * G, C * P * P, dtype=dtype, device=img.device)
+    x = torch.empty(B, G * G + 1, D, dtype=torch.float32, device=img.device)
+    ws = _ws(lib().vitmi_patch_embed_fwd_workspace_size(dt(dtype), B, C, S, P, D), img)
+    check(lib().vitmi_patch_embed_fwd(dt(dtype), B, C, S, P, D, _p(img), _p(w), _p(bias), _p(cls), _p(pos),
+                                      _p(patches), _p(x), _p(ws), ws.numel(), _s()), "patch_embed_fwd")
+    return x, patches
+
+
+def patch_embed_bwd(dx: Tensor, patches: Tensor, B: int, C: int, S: int, P: int, dw: Optional[Tensor],
+                    dbias: Optional[Tensor], dcls: Optional[Tensor], dpos: Optional[Tensor]) -> None:
+    """vitmi_patch_embed_bwd: dw [D, C*P*P] / dbias / dcls / dpos (fp32) += their gradients."""
+    dx = dx.contiguous()
+    D = dx.shape[-1]
+    dtype = patches.dtype
+    ws = _ws(lib().vitmi_patch_embed_bwd_workspace_size(dt(dtype), B, C, S, P, D), dx)
+    check(lib().vitmi_patch_embed_bwd(dt(dtype), B, C, S, P, D, _p(dx), _p(patches), _p(dw), _p(dbias), _p(dcls),
+                                      _p(dpos), _p(ws), ws.numel(), _s()), "patch_embed_bwd")
+
+
+def linear_bwd(dy: Tensor, x: Optional[Tensor], w: Optional[Tensor], dx_dtype: Optional[torch.dtype],
+               dw: Optional[Tensor], db: Optional[Tensor]) -> Optional[Tensor]:
+    """vitmi_linear_bwd: dx = dy W (when dx_dtype), dw += dy^T x, db += colsum(dy)."""
+    assert dy.is_contiguous()
+    M, N = dy.numel() // dy.shape[-1], dy.shape[-1]
+    K = w.shape[1] if w is not None else x.shape[-1]
+    dx = torch.empty(*dy.shape[:-1], K, dtype=dx_dtype, device=dy.device) if dx_dtype is not None else None
+    ws = _ws(lib().vitmi_linear_bwd_workspace_size(dt(dy.dtype), M, N, K), dy)
+    check(lib().vitmi_linear_bwd(dt(dy.dtype), M, N, K, _p(dy), _p(x), _p(w), _p(dx),
+                                 dt(dx_dtype) if dx_dtype is not None else 0, _p(dw), _p(db), _p(ws), ws.numel(),
+                                 _s()), "linear_bwd")
+    return dx
+
+
+def _loss_entry(name: str, logits: Tensor, target: Tensor, grad: bool) -> Tensor:
+    B, C = logits.shape
+    logits = logits.contiguous()
+    out = torch.empty_like(logits) if grad else torch.empty((), dtype=torch.float32, device=logits.device)
+    check(getattr(lib(), name)(B, C, _p(logits), _p(target.contiguous()), _p(out), _s()), name)
+    return out
+
+
+def xent_fwd(logits: Tensor, target: Tensor) -> Tensor:
+    return _loss_entry("vitmi_xent_fwd", logits, target.to(torch.int64), False)
+
+
+def xent_bwd(logits: Tensor, target: Tensor) -> Tensor:
+    return _loss_entry("vitmi_xent_bwd", logits, target.to(torch.int64), True)
+
+
+def mse_fwd(pred: Tensor, target: Tensor) -> Tensor:
+    return _loss_entry("vitmi_mse_fwd", pred, target.to(torch.float32).reshape(pred.shape), False)
+
+
+def mse_bwd(pred: Tensor, target: Tensor) -> Tensor:
+    return _loss_entry("vitmi_mse_bwd", pred, target.to(torch.float32).reshape(pred.shape), True)
+
+
 # ---------------------------------------------------------------- head / loss / cast
 def head_fwd(y: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     B, D = y.shape

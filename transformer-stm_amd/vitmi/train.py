@@ -140,10 +140,10 @@ def fit(model, ds: SLSDataset, epochs: int, batch_size: int = 128, optimizer: Op
 def _sum_over_ranks(v: Tensor, group, comm) -> Tensor:
     if comm is not None:
         from .dp import REDUCE_SUM
-        buf = v.float().contiguous()
+        buf = v.double().contiguous()       # float64 on the wire, as the process-group path
         side = torch.cuda.current_stream(buf.device)
         comm.allreduce_async(buf, side, None, REDUCE_SUM)
-        return buf.double()
+        return buf
     v = v.clone()
     torch.distributed.all_reduce(v, group=group)
     return v
