@@ -272,6 +272,9 @@ def main():
                     help="c3: ViT-B/16 224px bs 256/GPU (the headline metric); c5: ViT-L/16 384px bs 64/GPU "
                          "(BASELINE config 5, N = 577 tokens); c2: ViT-S/16 224px bs 128 fp32 (BASELINE config "
                          "2). c2 and c5 are secondary lines, not the headline")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default=None,
+                    help="override the config's compute dtype (the precision knob: fp32 = exact-fp32 MFMA "
+                         "GEMMs and attention, logits within 1e-3 of the CPU oracle at ViT-B depth 12)")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5, "
                                                              "128 for c2)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
@@ -315,6 +318,8 @@ def main():
     if args.roctx:
         trace.enable()
     cfg = {"c2": config_c2, "c3": config_c3, "c5": config_c5}[args.config]()
+    if args.dtype is not None:
+        cfg = cfg.replace(dtype=args.dtype)
     B = args.batch or {"c2": 128, "c3": 256, "c5": 64}[args.config]
     model_name = {"c2": "vit_small_16", "c3": "vit_base_16", "c5": "vit_large_16"}[args.config]
     metric = {"c3": METRIC,
@@ -483,10 +488,14 @@ def secondary_lines():
     the driver's clock: child runs of this bench after the headline (10 timed steps each); the
     headline `value` stays C3."""
     out = {}
-    for cfg in ("c5", "c2"):
+    runs = {"c5": ["--config", "c5", "--steps", "10", "--warmup", "3"],
+            "c2": ["--config", "c2", "--steps", "10", "--warmup", "3"],
+            # the precision knob: ViT-B/16 C3 with exact-fp32 arithmetic (logits within 1e-3)
+            "c3_fp32": ["--config", "c3", "--dtype", "fp32", "--steps", "3", "--warmup", "1"]}
+    for cfg, extra in runs.items():
         log = os.path.join(tempfile.gettempdir(), f"vitmi_secondary_{cfg}.log")
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg, "--steps", "10", "--warmup", "3",
-               "--no-evidence", "--no-cpu-baseline", "--no-secondary"]
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *extra, "--no-evidence", "--no-cpu-baseline",
+               "--no-secondary"]
         rc = _run(cmd, 300, log=log)
         line = None
         if rc == 0:

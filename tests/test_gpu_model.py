@@ -315,3 +315,17 @@ def test_fwd_bwd_is_bitwise_deterministic(dtype, batch):
     assert torch.equal(l0, l1) and torch.equal(s0, s1)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
+
+
+def test_vit_b_precision_knob_fp32_meets_1e3():
+    """The precision knob: ViT-B/16 224^2 at full depth 12 with dtype='fp32'
+    (exact-fp32 MFMA GEMMs and fp32 attention) meets the north star's logits-within-1e-3 against
+    the fp32 CPU oracle, forward AND backward, on the randomised-parameter stress case where the
+    bf16 default measures 3.6e-3."""
+    cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype="fp32")
+    params = vit_ref.init_params(cfg, seed=0)
+    img, tgt = vit_ref.synthetic_batch(cfg, 2)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    err, worst = compare(cfg, params, img, tgt, logit_tol=1e-3, grad_tol=1e-3, loss_tol=1e-5)
+    print(f"ViT-B/16 fp32 depth 12 bs 2: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
+    assert err <= 1e-4     # measured margin: fp32 sums in another order only
