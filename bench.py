@@ -451,6 +451,7 @@ def main():
         "loss": round(float(loss.item()), 5),
         "build_id": _lib.lib().vitmi_build_id().decode(),
     }
+    red.close()                               # the comm watchdog thread (the step loop is over)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps, model, dev)
     if rank == 0 and world == 1 and not args.no_evidence and args.config == "c3" and not args.stats_out:
@@ -475,7 +476,6 @@ def main():
         out["secondary"] = secondary_lines()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    red.close()
     if comm is not None:
         comm.destroy()
     if world > 1:
