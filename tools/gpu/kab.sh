@@ -11,6 +11,6 @@ for round in 1 2; do
   for v in base "$@"; do
     lib=""; [ $v != base ] && lib=$PWD/transformer-stm_amd/variants/$v.so
     VITMI_LIB=$lib timeout -k 10 120 $tool > gpurun_out/$tag/tool_${v}_$round.log 2>&1 || exit 1
-    VITMI_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-evidence --steps 10 --warmup 3 > gpurun_out/$tag/step_${v}_$round.log 2>&1 || exit 1
+    VITMI_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-evidence --no-secondary --steps 10 --warmup 3 > gpurun_out/$tag/step_${v}_$round.log 2>&1 || exit 1
   done
 done

@@ -1336,7 +1336,11 @@ static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K) {
   const int64_t t = big ? 256 : 128;
   const int64_t tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
   const int64_t ktiles = (K + bk_of(dtype) - 1) / bk_of(dtype);
-  return (int)splits_for(tiles, ktiles, big ? 256 : 512);
+  // about one round of the CUs the persistent grid may use: with reserved CUs (DP overlap) a
+  // fixed 256 left a few units for a second full round (fc1 wgrad 262 -> 440 us at 8 reserved)
+  init_cus();
+  const int avail = g_cus - g_reserved > 8 ? g_cus - g_reserved : 8;
+  return (int)splits_for(tiles, ktiles, big ? avail : 2 * avail);
 }
 
 static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K, const void* A,
