@@ -628,30 +628,14 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
   char* kt = smem;
   char* vt = smem + NP * 128;
-  const int q = wave * 32 + (lane & 31);
-  bf16x8 qf[4];
-#ifdef VITMI_ATTN_QREG
   stage_seq(kt, rk, ldb, NP, nw, wave, lane);
   stage_seq(vt, rv, ldb, NP, nw, wave, lane);
+  const int q = wave * 32 + (lane & 31);
+  bf16x8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  bool vready = true;
-#else
-  // Q rows arrive as whole 128-B lines too: staged by LDS-DMA into the V image, read back as
-  // fragments, and only then is V streamed into that image, under the first tile's Q K^T and
-  // softmax (per-lane 16-B fragment loads straight from HBM touch 32 lines per instruction)
-  stage_seq(kt, rk, ldb, NP, nw, wave, lane);
-  stage_seq(vt, rq, ldb, NP, nw, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = frag_row(vt, wave * 32, s, lane);
-  __syncthreads();   // every wave holds its Q fragments: the image takes V now
-  stage_seq(vt, rv, ldb, NP, nw, wave, lane);
-  bool vready = false;
-#endif
 
   const float c2 = scale * LOG2E;
   float m = -INFINITY, l = 0.f;
@@ -699,10 +683,6 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) oacc[dt][r] *= alpha;
-    }
-    if (!vready) {        // V landed (every wave's DMA): first tile only, uniform over waves
-      __syncthreads();
-      vready = true;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -766,13 +746,13 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
   char* kt = smem;
   char* vt = smem + NP * 128;
+  stage_seq(kt, rk, ldb, NP, nw, wave, lane);
+  stage_seq(vt, rv, ldb, NP, nw, wave, lane);
+
   const int q = wave * 32 + (lane & 31);
   const bool qok = q < N;
   bf16x8 qf[4], df[4];
   float dl;
-#ifdef VITMI_ATTN_QREG
-  stage_seq(kt, rk, ldb, NP, nw, wave, lane);
-  stage_seq(vt, rv, ldb, NP, nw, wave, lane);
   {
     bf16x8 of[4];
 #pragma unroll
@@ -795,37 +775,6 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;   // q >= N -> p = 0
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-#else
-  // Q and dO arrive as whole 128-B lines (LDS-DMA into the K / V images, read back as
-  // fragments); only O (for delta) is loaded as fragments.  Then K and V replace them.
-  stage_seq(kt, rq, ldb, NP, nw, wave, lane);
-  stage_seq(vt, rdo, ldo, NP, nw, wave, lane);
-  bf16x8 of[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) of[s] = load_row16(ro, (uint32_t)((int64_t)q * ldo + (16 * s + 8 * h) * 2));
-  const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;   // q >= N -> p = 0
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = frag_row(kt, wave * 32, s, lane);
-    df[s] = frag_row(vt, wave * 32, s, lane);
-  }
-  {
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) part += (float)of[s][j] * (float)df[s][j];
-    dl = part + __shfl_xor(part, 32, 64);
-  }
-  if (qok && h == 0) delta[(int64_t)bh * N + q] = dl;
-  __syncthreads();   // every wave holds its Q / dO fragments: the images take K and V now
-  stage_seq(kt, rk, ldb, NP, nw, wave, lane);
-  stage_seq(vt, rv, ldb, NP, nw, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-#endif
 
   const float c2 = scale * LOG2E;
   f32x16 dqt[2] = {zero16(), zero16()};
