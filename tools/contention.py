@@ -9,8 +9,13 @@ kernels queue until blocks drain unless `reserve_cus` CUs are kept free.  For ea
 this prints the step time and, per bucket, the side stream's wall time from the moment its
 event gate opened to the end of its traffic (HIP events on the side stream).
 
-usage: python tools/contention.py [steps] [reserve values...]   -> JSON on stdout
+With --emu B the side traffic is tools/proto/rccl_emu.hip instead: B persistent "channel"
+blocks that must all be running before any streams (RCCL's co-residency requirement), so a
+channel block that finds every CU held by the persistent GEMM delays the whole collective.
+
+usage: python tools/contention.py [steps] [--emu B] [reserve values...]   -> JSON on stdout
 """
+import ctypes
 import json
 import os
 import sys
@@ -30,11 +35,30 @@ class RcclShapedTraffic:
 
     world = 8
 
-    def __init__(self):
+    def __init__(self, emu_blocks=0):
         self.spans = []
         self._tmp = None
+        self.emu_blocks = emu_blocks
+        self._gen = 0
+        if emu_blocks:
+            self._lib = ctypes.CDLL(os.path.join(ROOT, "tools", "proto", "librccl_emu.so"))
+            self._lib.emu_allreduce_launch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                                       ctypes.c_uint, ctypes.c_void_p]
+            self._counter = torch.zeros(1, dtype=torch.int32, device="cuda")
 
     def allreduce_async(self, buf, side, ready=None, op=None):
+        if self.emu_blocks:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if ready is not None:
+                side.wait_event(ready)
+            e0.record(side)
+            rc = self._lib.emu_allreduce_launch(buf.data_ptr(), buf.numel() // 4 * 4, self.emu_blocks,
+                                                self._counter.data_ptr(), self._gen, side.cuda_stream)
+            assert rc == 0, rc
+            self._gen += 1
+            e1.record(side)
+            self.spans.append((e0, e1))
+            return
         if self._tmp is None or self._tmp.numel() < buf.numel():
             self._tmp = torch.empty(buf.numel(), dtype=buf.dtype, device=buf.device)
         tmp = self._tmp[:buf.numel()]
@@ -59,12 +83,12 @@ class RcclShapedTraffic:
         pass
 
 
-def run(steps, reserve, traffic):
+def run(steps, reserve, traffic, emu=0):
     cfg = config_c3()
     dev = torch.device("cuda", 0)
     model = VisionTransformer(cfg).to(dev)
     model.reset_parameters(seed=0)
-    comm = RcclShapedTraffic() if traffic else None
+    comm = RcclShapedTraffic(emu) if traffic else None
     red = dp.GradReducer(model.arena().grad, 64.0, comm=comm, reserve_cus=reserve, timeout_s=0) if traffic else None
     if red is not None:
         arena = model.arena()
@@ -104,7 +128,8 @@ def run(steps, reserve, traffic):
         step()
     e1.record()
     torch.cuda.synchronize()
-    out = {"reserve_cus": reserve, "traffic": traffic, "ms_per_step": round(e0.elapsed_time(e1) / steps, 3)}
+    out = {"reserve_cus": reserve, "traffic": ("emu%d" % emu if emu else "torch") if traffic else None,
+           "ms_per_step": round(e0.elapsed_time(e1) / steps, 3)}
     if comm is not None:
         sp = [a.elapsed_time(b) for a, b in comm.spans]
         nb = len(sp) // steps
@@ -118,13 +143,18 @@ def run(steps, reserve, traffic):
 
 
 def main():
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    reserves = [int(v) for v in sys.argv[2:]] or [0, 8, 16, 32]
+    args = sys.argv[1:]
+    steps = int(args.pop(0)) if args else 10
+    emu = 0
+    if args and args[0] == "--emu":
+        emu = int(args[1])
+        args = args[2:]
+    reserves = [int(v) for v in args] or [0, 8, 16, 32]
     rows = [run(steps, 0, False)]
     print(json.dumps(rows[-1]), flush=True)
     for rnd in range(2):                                   # two alternating rounds (rule 24)
         for r in reserves:
-            rows.append(dict(run(steps, r, True), round=rnd))
+            rows.append(dict(run(steps, r, True, emu), round=rnd))
             print(json.dumps(rows[-1]), flush=True)
     print(json.dumps({"rows": rows}))
 
