@@ -41,6 +41,13 @@ enum {
   VITMI_EPI_DGELU = 3,     /* C = acc * aux   (aux = gelu'(u) from BIAS_GELU)        */
   VITMI_EPI_ACCUM = 4      /* C(f32) += acc                                          */
 };
+/* OR'ed into BIAS_GELU / DGELU (bf16 operands only): aux is kept in the library's tile-native
+ * layout instead of a row-major [M][N] array -- vitmi_aux_tiled_bytes(M, N) bytes, written by a
+ * BIAS_GELU call and read by a DGELU call of the same M x N output, opaque to the caller.  The
+ * GEMM epilogues then store and load it straight from the accumulator registers (no LDS
+ * transpose): the fc1 forward / fc2 dgrad pair of the ViT MLP (models/CvT(Par).py:253-258). */
+#define VITMI_EPI_AUX_TILED 0x100
+size_t vitmi_aux_tiled_bytes(int64_t rows, int64_t cols);
 
 enum { VITMI_LOSS_CE = 0, VITMI_LOSS_MSE = 1 };
 

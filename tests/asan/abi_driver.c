@@ -51,12 +51,16 @@ int main(void) {
                     VITMI_BF16, VITMI_EPI_STORE, NULL, NULL, 0, NULL, 0, NULL, 0, NULL) == VITMI_ERR_INVALID);
   EXPECT(vitmi_linear_fwd(VITMI_BF16, 64, 64, 64, (void*)16, (void*)16, NULL, (void*)16, VITMI_BF16, 9, NULL,
                           NULL, NULL, 0, NULL) == VITMI_ERR_INVALID);
+  /* the tile-native gelu' layout is bf16-only */
+  EXPECT(vitmi_linear_fwd(VITMI_F32, 64, 64, 64, (void*)16, (void*)16, NULL, (void*)16, VITMI_F32,
+                          VITMI_EPI_BIAS_GELU | VITMI_EPI_AUX_TILED, (void*)16, NULL, NULL, 0, NULL) == VITMI_ERR_INVALID);
   EXPECT(vitmi_gemm(VITMI_BF16, 1, 1, 0, 128, 128, NULL, 128, NULL, 128, NULL, 128, VITMI_BF16,
                     VITMI_EPI_STORE, NULL, NULL, 0, NULL, 0, NULL, 0, NULL) == VITMI_OK);   /* empty */
   /* workspace queries at every ViT shape */
   const int64_t Ms[] = {1, 197, 50432, 64 * 577};
   for (int i = 0; i < 4; ++i) {
     (void)vitmi_linear_fwd_workspace_size(VITMI_BF16, Ms[i], 3072, 768);
+    EXPECT(vitmi_aux_tiled_bytes(Ms[i], 3072) == (size_t)((Ms[i] + 255) / 256) * 12 * 131072);
     (void)vitmi_linear_dgrad_workspace_size(VITMI_BF16, Ms[i], 3072, 768);
     (void)vitmi_linear_dgrad_bias_workspace_size(VITMI_BF16, Ms[i], 3072, 768);
     EXPECT(vitmi_linear_wgrad_workspace_size(VITMI_BF16, Ms[i], 768, 768) < ((size_t)1 << 34));

@@ -110,6 +110,38 @@ def test_gemm_tail_split(M, N, K):
         lib().vitmi_gemm_set_policy(0)
 
 
+@pytest.mark.parametrize("M,N,K,fpol,bpol", [(197 * 8 + 3, 1024, 256, 0, 0),      # gemm256, ragged M
+                                              (256 * 8 + 100, 256 + 64, 512, 3, 3),  # tail split + fix-up
+                                              (300, 320, 192, 1, 2),   # forward on the 128x128 kernel
+                                              (300, 320, 192, 2, 1)])  # backward on the 128x128 kernel
+def test_aux_tiled_matches_row_major(M, N, K, fpol, bpol):
+    """gelu' in the tile-native layout (VITMI_EPI_AUX_TILED): the GELU activation (plain and
+    with dropout) and the DGELU dgrad with its fused bias gradient are bit-identical to the
+    row-major layout's, whichever kernel wrote gelu' and whichever read it."""
+    from vitmi._lib import lib
+    x, w, b = rnd(M, K, dtype=BF, seed=61).to(DEV), rnd(N, K, dtype=BF, seed=62, scale=0.05).to(DEV), rnd(N, seed=63).to(DEV)
+    dy, w2 = rnd(M, 384, dtype=BF, seed=64).to(DEV), rnd(384, N, dtype=BF, seed=65, scale=0.05).to(DEV)
+    out = {}
+    try:
+        for tiled in (False, True):
+            lib().vitmi_gemm_set_policy(fpol)
+            a, u = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, aux_tiled=tiled)
+            ad, ud = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, dropout=(5, 2, 0.25), aux_tiled=tiled)
+            if tiled:
+                assert u.numel() * 2 == lib().vitmi_aux_tiled_bytes(M, N)
+            lib().vitmi_gemm_set_policy(bpol)
+            db = torch.zeros(N, device=DEV)
+            dx = ops.linear_dgrad(dy, w2, BF, ops.EPI_DGELU, aux=u, bias_grad=db, aux_tiled=tiled)
+            dxd = ops.linear_dgrad(dy, w2, BF, ops.EPI_DGELU, aux=ud, aux_tiled=tiled)
+            out[tiled] = (a, ad, dx, db, dxd)
+    finally:
+        lib().vitmi_gemm_set_policy(0)
+    for name, r, t in zip(("gelu", "gelu+dropout", "dgelu", "bias grad", "dgelu+dropout"), out[False], out[True]):
+        assert torch.equal(r, t), name
+    ref = (dy.float() @ w2.float()).cpu() * gelu_grad((x.float() @ w.float().t() + b).cpu())
+    assert rel(out[True][2].float(), ref) < 8e-3
+
+
 def test_gemm_tail_split_vit_shape():
     """The ViT-B/16 bs=256 N=768 shape on the real grid (591 tiles over the device's CUs),
     against torch's own GEMM on the GPU (the CPU reference would take minutes)."""

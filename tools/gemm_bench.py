@@ -45,13 +45,18 @@ def main():
         "square TN      [8192^3]": (lambda: ops.gemm(a8, b8, False, False, 8192, 8192, 8192, c8), 2 * 8192 ** 3),
         "fc1 fwd store  [M,3072,768]": (lambda: ops.linear_fwd(x, w1, b1, BF), 2 * M * F * D),
         "fc1 fwd f32out [M,3072,768]": (lambda: ops.linear_fwd(x, w1, b1, torch.float32), 2 * M * F * D),
-        "fc1 fwd +GELU  [M,3072,768]": (lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU), 2 * M * F * D),
+        "fc1 fwd +GELU  [M,3072,768]": (lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU, aux_tiled=True),
+                                        2 * M * F * D),
+        "fc1 +GELU rowmajor gelu'": (lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU), 2 * M * F * D),
         "qkv fwd store  [M,2304,768]": (lambda: ops.linear_fwd(x, wq, bq, BF), 2 * M * 3 * D * D),
         "fc2 fwd +resid [M,768,3072]": (lambda: ops.linear_fwd(h, w2, b2, torch.float32, ops.EPI_RESIDUAL, res),
                                         2 * M * F * D),
         "proj fwd +res  [M,768,768]": (lambda: ops.linear_fwd(x, wo, b2, torch.float32, ops.EPI_RESIDUAL, res),
                                        2 * M * D * D),
-        "fc2 dgrad dGELU[M,3072,768]": (lambda: ops.linear_dgrad(x, w2, BF, ops.EPI_DGELU, aux=h), 2 * M * F * D),
+        # (M x 3072 is a whole number of 256 x 256 tiles: h doubles as a tile-native gelu' buffer)
+        "fc2 dgrad dGELU[M,3072,768]": (lambda: ops.linear_dgrad(x, w2, BF, ops.EPI_DGELU, aux=h, aux_tiled=True),
+                                        2 * M * F * D),
+        "fc2 dGELU rowmajor gelu'": (lambda: ops.linear_dgrad(x, w2, BF, ops.EPI_DGELU, aux=h), 2 * M * F * D),
         "fc1 dgrad f32  [M,768,3072]": (lambda: ops.linear_dgrad(h, w1, torch.float32), 2 * M * F * D),
         "fc1 dgrad bf16 [M,768,3072]": (lambda: ops.linear_dgrad(h, w1, BF), 2 * M * F * D),
         "qkv dgrad bf16 [M,768,2304]": (lambda: ops.linear_dgrad(gq, wq, BF), 2 * M * 3 * D * D),

@@ -23,7 +23,7 @@ def main():
     w2 = ((torch.rand(D, F, device="cuda", generator=g) * 2 - 1) * 0.05).to(BF)
     b1, b2 = torch.zeros(F, device="cuda"), torch.zeros(D, device="cuda")
     res = torch.rand(M, D, device="cuda")
-    fn = {"fc1_gelu": lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU),
+    fn = {"fc1_gelu": lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU, aux_tiled=True),   # as the model
           "fc1_store": lambda: ops.linear_fwd(x, w1, b1, BF),
           "fc2_res": lambda: ops.linear_fwd(h, w2, b2, torch.float32, ops.EPI_RESIDUAL, res)}[which]
     for _ in range(iters):

@@ -43,9 +43,9 @@ def main():
     cases = [
         ("qkv fwd  [M x 2304 x 768] +bias", 2 * M * 3 * D * D, lambda: ops.linear_fwd(x, wqkv, bq, BF)),
         ("proj fwd [M x 768 x 768] +res", 2 * M * D * D, lambda: ops.linear_fwd(x, wo, bo, torch.float32, ops.EPI_RESIDUAL, res)),
-        ("fc1 fwd  [M x 3072 x 768] +GELU", 2 * M * F * D, lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU)),
+        ("fc1 fwd  [M x 3072 x 768] +GELU", 2 * M * F * D, lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU, aux_tiled=True)),
         ("fc2 fwd  [M x 768 x 3072] +res", 2 * M * D * F, lambda: ops.linear_fwd(h4, w2, b2, torch.float32, ops.EPI_RESIDUAL, res)),
-        ("fc2 dgrad [M x 3072 x 768] DGELU", 2 * M * F * D, lambda: ops.linear_dgrad(x, w2, BF, ops.EPI_DGELU, gp)),
+        ("fc2 dgrad [M x 3072 x 768] DGELU", 2 * M * F * D, lambda: ops.linear_dgrad(x, w2, BF, ops.EPI_DGELU, gp, aux_tiled=True)),
         ("fc1 dgrad [M x 768 x 3072]", 2 * M * D * F, lambda: ops.linear_dgrad(h4, w1, BF)),
         ("qkv dgrad [M x 768 x 2304]", 2 * M * D * 3 * D, lambda: ops.linear_dgrad(dq, wqkv, BF)),
         ("proj dgrad [M x 768 x 768]", 2 * M * D * D, lambda: ops.linear_dgrad(x, wo, BF)),

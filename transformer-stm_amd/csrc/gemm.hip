@@ -68,7 +68,22 @@ struct GemmArgs {
   // input gradient this is), one fp32 row per 128-row half tile: colsum[(2*tm + wm)*N + col]
   float* colsum;
   unsigned long long* stamps;        // DIAGNOSTIC build only (VITMI_GEMM_STAMPS)
+  int aux_tiled;                     // gelu' in the tile-native layout (VITMI_EPI_AUX_TILED)
 };
+
+// Element (row, col) of a tile-native gelu' buffer (VITMI_EPI_AUX_TILED; bf16 elements): 256x256
+// tiles in row-major tile order, each 128 KiB laid out as gemm256's epilogue registers hold it --
+// [wave (wm*4 + wn)][row group mi][column pair][lane][16 B], lane = (row & 15) + 16 * ((col >> 2) & 3)
+// -- so the BIAS_GELU epilogue stores and the DGELU epilogue loads whole KiB per instruction
+// straight from / into the accumulator layout.
+__device__ __forceinline__ int64_t aux_at(const GemmArgs& g, int64_t row, int64_t col) {
+  if (!g.aux_tiled) return row * g.ldaux + col;
+  const int64_t tile = (row >> 8) * ((g.N + 255) >> 8) + (col >> 8);
+  const int r = (int)(row & 255), c = (int)(col & 255);
+  const int wave = (r >> 7) * 4 + (c >> 6), mi = (r >> 4) & 7, ni = (c >> 4) & 3;
+  const int lane = (r & 15) + 16 * ((c >> 2) & 3);
+  return tile * 65536 + (((wave * 8 + mi) * 2 + (ni >> 1)) * 1024 + lane * 16 + (ni & 1) * 8) / 2 + (c & 3);
+}
 
 // (tile-row, tile-col) of tile index tl: row-major over the tiles_n tile columns (a persistent
 // block walks consecutive tiles, so an XCD's concurrent tiles share A row panels in its L2;
@@ -227,7 +242,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_
                                           float biasv) {
   if constexpr (EPI == EPI_GELU_DROP) {
     const float u = acc + biasv, f = drop_factor(g, row, col);
-    ((T*)g.aux)[row * g.ldaux + col] = from_f32<T>(gelu_grad_f(u) * f);
+    ((T*)g.aux)[aux_at(g, row, col)] = from_f32<T>(gelu_grad_f(u) * f);
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(gelu_f(u) * f);
   } else if constexpr (EPI == EPI_RESIDUAL_DROP) {
     ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + (acc + biasv) * drop_factor(g, row, col);
@@ -237,12 +252,12 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc + biasv);
   } else if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
     const float u = acc + biasv;
-    ((T*)g.aux)[row * g.ldaux + col] = from_f32<T>(gelu_grad_f(u));
+    ((T*)g.aux)[aux_at(g, row, col)] = from_f32<T>(gelu_grad_f(u));
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(gelu_f(u));
   } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
     ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + acc + biasv;
   } else if constexpr (EPI == VITMI_EPI_DGELU) {
-    const float gp = to_f32(((const T*)g.aux)[row * g.ldaux + col]);
+    const float gp = to_f32(((const T*)g.aux)[aux_at(g, row, col)]);
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc * gp);
   } else if constexpr (EPI == VITMI_EPI_ACCUM) {
     ((float*)g.C)[row * g.ldc + col] += acc;
@@ -792,7 +807,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       [[maybe_unused]] f32x4 csum[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
                                         f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
       if constexpr (EB == VITMI_EPI_BIAS_GELU)
-        ru = make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
+        ru = g.aux_tiled ? make_rsrc((char*)g.aux + ((m0 >> 8) * g.tiles_n + (n0 >> 8)) * 131072, 131072u)
+                         : make_rsrc((char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
       // bf16 outputs leave through the wave's LDS image of one 16-row group: each lane holds 4
       // columns of ONE row per fragment (16 rows x 32 B per store instruction: every store would
       // touch 16 lines with a quarter of each), so a row group is written to LDS and read back as
@@ -873,9 +889,21 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         if constexpr (CES == 2) {
           flush(rc, g.ldc, mi);
           if constexpr (EB == VITMI_EPI_BIAS_GELU) {
+            if (g.aux_tiled) {   // straight from the registers: 2 KiB-wide stores (aux_at)
+              const u32x4 w0 = __builtin_bit_cast(u32x4, bf16x8{us[0][0], us[0][1], us[0][2], us[0][3],
+                                                                us[1][0], us[1][1], us[1][2], us[1][3]});
+              const u32x4 w1 = __builtin_bit_cast(u32x4, bf16x8{us[2][0], us[2][1], us[2][2], us[2][3],
+                                                                us[3][0], us[3][1], us[3][2], us[3][3]});
+              asm volatile(VMEM_SGPR_GUARD
+                           "buffer_store_dwordx4 %0, %2, %3, %4 offen\n\t"
+                           "buffer_store_dwordx4 %1, %2, %3, %4 offen offset:1024\n\ts_nop 1"
+                           :: "v"(w0), "v"(w1), "v"((uint32_t)(wave * 16384 + lane * 16)), "s"(ru), "s"(mi * 2048)
+                           : "memory");
+            } else {
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) lds_put(ni, us[ni]);
-            flush(ru, g.ldaux, mi);
+              for (int ni = 0; ni < 4; ++ni) lds_put(ni, us[ni]);
+              flush(ru, g.ldaux, mi);
+            }
           }
         }
       };
@@ -893,25 +921,52 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           const __amdgpu_buffer_rsrc_t rx =
               make_rsrc((const char*)g.aux + (m0 * g.ldaux + n0) * 2, clamp_bytes(((g.M - m0) * g.ldaux - n0) * 2));
           u32x4 al[8][2];
-#pragma unroll
-          for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const uint32_t vo = ccok ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr) * g.ldaux + wn * 64 + cc * 8) * 2)
-                                       : 0x80000000u;
-              al[mi][j] = __builtin_amdgcn_raw_buffer_load_b128(rx, vo, (int)(mi * 16 * g.ldaux * 2), 0);
-            }
           const f32x4 z4[4] = {};
+          if (g.aux_tiled) {
+            // tile-native gelu' (aux_at): the lane's own 16 B of each row group, no exchange.
+            // Rows >= M of a tile may hold anything (the forward may have run the 128x128
+            // kernel, which writes valid elements only): they are zeroed, so the fused column
+            // sums see 0 * 0 there
+            const __amdgpu_buffer_rsrc_t rxt =
+                make_rsrc((const char*)g.aux + ((m0 >> 8) * g.tiles_n + (n0 >> 8)) * 131072, 131072u);
 #pragma unroll
-          for (int mi = 0; mi < 8; ++mi) {
+            for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) *(u32x4*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16) = al[mi][j];
-            lane_xchg();
-            bf16x4 lb[4];
+              for (int j = 0; j < 2; ++j)
+                al[mi][j] = __builtin_amdgcn_raw_buffer_load_b128(rxt, (uint32_t)(wave * 16384 + lane * 16),
+                                                                  mi * 2048 + j * 1024, 0);
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) lb[ni] = *(const bf16x4*)(scr + lr * EPI_PITCH + (ni * 16 + lc4) * 2);
-            lane_xchg();   // (the image is rewritten by emit_row after every lane's read)
-            emit_row(mi, z4, lb);
+            for (int mi = 0; mi < 8; ++mi) {
+              const bool rok = m0 + wm * 128 + mi * 16 + lr < g.M;
+              bf16x4 lb[4];
+#pragma unroll
+              for (int ni = 0; ni < 4; ++ni) {
+                const bf16x8 w = __builtin_bit_cast(bf16x8, rok ? al[mi][ni >> 1] : u32x4{0u, 0u, 0u, 0u});
+                const int o = (ni & 1) * 4;
+                lb[ni] = bf16x4{w[o], w[o + 1], w[o + 2], w[o + 3]};
+              }
+              emit_row(mi, z4, lb);
+            }
+          } else {
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const uint32_t vo = ccok ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr) * g.ldaux + wn * 64 + cc * 8) * 2)
+                                         : 0x80000000u;
+                al[mi][j] = __builtin_amdgcn_raw_buffer_load_b128(rx, vo, (int)(mi * 16 * g.ldaux * 2), 0);
+              }
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) *(u32x4*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16) = al[mi][j];
+              lane_xchg();
+              bf16x4 lb[4];
+#pragma unroll
+              for (int ni = 0; ni < 4; ++ni) lb[ni] = *(const bf16x4*)(scr + lr * EPI_PITCH + (ni * 16 + lc4) * 2);
+              lane_xchg();   // (the image is rewritten by emit_row after every lane's read)
+              emit_row(mi, z4, lb);
+            }
           }
         } else if constexpr (EB == VITMI_EPI_RESIDUAL) {
           // fp32 residual in, fp32 out, both as whole lines through the LDS image, half a row
@@ -1349,6 +1404,8 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
                      int64_t ldr, void* ws, size_t ws_bytes, hipStream_t s, bool allow_split,
                      const GemmArgs* drop = nullptr, float* colsum = nullptr, bool* colsum_done = nullptr) {
   if (colsum_done) *colsum_done = false;
+  const bool aux_tiled = (epi & VITMI_EPI_AUX_TILED) != 0;
+  epi &= ~VITMI_EPI_AUX_TILED;
   VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "gemm: bad dtype %d", dtype);
   VITMI_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return VITMI_OK;
@@ -1365,6 +1422,11 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   const int eb = epi_base(epi);
   if (eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_DGELU)
     VITMI_CHECK_ARG(aux != nullptr && ldaux >= N, "gemm: epilogue needs aux");
+  if (aux_tiled) {
+    VITMI_CHECK_ARG(eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_DGELU, "gemm: AUX_TILED needs BIAS_GELU or DGELU");
+    VITMI_CHECK_ARG(dtype == VITMI_BF16, "gemm: AUX_TILED needs bf16 operands (a bf16 gelu')");
+    VITMI_CHECK_ARG(((uintptr_t)aux % 16) == 0, "gemm: AUX_TILED aux must be 16-byte aligned");
+  }
   if (eb == VITMI_EPI_RESIDUAL) VITMI_CHECK_ARG(residual != nullptr && ldr >= N, "gemm: residual missing");
   if (eb == VITMI_EPI_RESIDUAL || eb == VITMI_EPI_ACCUM)
     VITMI_CHECK_ARG(c_dtype == VITMI_F32, "gemm: residual/accum epilogues write fp32");
@@ -1385,6 +1447,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.bias = bias; g.aux = aux; g.ldaux = ldaux;
   g.residual = residual; g.ldr = ldr;
+  g.aux_tiled = aux_tiled;
   if (drop) {
     g.drop_seed = drop->drop_seed; g.drop_site = drop->drop_site;
     g.drop_thresh = drop->drop_thresh; g.drop_scale = drop->drop_scale;
@@ -1487,6 +1550,11 @@ extern "C" size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajo
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
+extern "C" size_t vitmi_aux_tiled_bytes(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return (size_t)((rows + 255) / 256) * (size_t)((cols + 255) / 256) * 131072;
+}
+
 extern "C" size_t vitmi_linear_fwd_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
   return use256(dtype, M, N) ? tail_ws_bytes(M, N, K) : 0;
 }
@@ -1495,8 +1563,9 @@ extern "C" int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, cons
                                 const void* w, const float* bias, void* y, int y_dtype,
                                 int epilogue, void* aux, const float* residual, void* workspace,
                                 size_t ws_bytes, vitmi_stream_t stream) {
-  VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_BIAS_GELU ||
-                      epilogue == VITMI_EPI_RESIDUAL, "linear_fwd: bad epilogue %d", epilogue);
+  const int eb = epilogue & ~VITMI_EPI_AUX_TILED;
+  VITMI_CHECK_ARG(eb == VITMI_EPI_STORE || eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_RESIDUAL,
+                  "linear_fwd: bad epilogue %d", epilogue);
   return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, N, y_dtype, epilogue, bias, aux, N,
                    residual, N, workspace, ws_bytes, (hipStream_t)stream, false);
 }
@@ -1507,11 +1576,12 @@ extern "C" int vitmi_linear_fwd_dropout(int dtype, int64_t M, int64_t N, int64_t
                                         void* workspace, size_t ws_bytes, uint32_t seed,
                                         uint32_t site, uint32_t thresh, float scale,
                                         vitmi_stream_t stream) {
-  VITMI_CHECK_ARG(epilogue == VITMI_EPI_BIAS_GELU || epilogue == VITMI_EPI_RESIDUAL,
+  const int eb = epilogue & ~VITMI_EPI_AUX_TILED;
+  VITMI_CHECK_ARG(eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_RESIDUAL,
                   "linear_fwd_dropout: epilogue must be BIAS_GELU or RESIDUAL (got %d)", epilogue);
   GemmArgs d{};
   d.drop_seed = seed; d.drop_site = site; d.drop_thresh = thresh; d.drop_scale = scale;
-  const int epi = epilogue == VITMI_EPI_BIAS_GELU ? EPI_GELU_DROP : EPI_RESIDUAL_DROP;
+  const int epi = (eb == VITMI_EPI_BIAS_GELU ? EPI_GELU_DROP : EPI_RESIDUAL_DROP) | (epilogue & VITMI_EPI_AUX_TILED);
   return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, N, y_dtype, epi, bias, aux, N, residual, N,
                    workspace, ws_bytes, (hipStream_t)stream, false, &d);
 }
@@ -1525,7 +1595,8 @@ extern "C" int vitmi_linear_dgrad(int dtype, int64_t M, int64_t N, int64_t K, co
                                   const void* w, void* dx, int dx_dtype, int epilogue,
                                   const void* aux, void* workspace, size_t ws_bytes,
                                   vitmi_stream_t stream) {
-  VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_DGELU,
+  VITMI_CHECK_ARG((epilogue & ~VITMI_EPI_AUX_TILED) == VITMI_EPI_STORE ||
+                      (epilogue & ~VITMI_EPI_AUX_TILED) == VITMI_EPI_DGELU,
                   "linear_dgrad: bad epilogue %d", epilogue);
   // dx[M,K] = dy[M,N] . W[N,K]: reduction over N; A = dy (k-major), B = W as [N][K] (n-major)
   return gemm_impl(dtype, 1, 0, M, K, N, dy, N, w, K, dx, K, dx_dtype, epilogue, nullptr,
@@ -1544,7 +1615,8 @@ extern "C" size_t vitmi_linear_dgrad_bias_workspace_size(int dtype, int64_t M, i
 extern "C" int vitmi_linear_dgrad_bias(int dtype, int64_t M, int64_t N, int64_t K, const void* dy,
                                        const void* w, void* dx, int dx_dtype, int epilogue, const void* aux,
                                        float* db, void* workspace, size_t ws_bytes, vitmi_stream_t stream) {
-  VITMI_CHECK_ARG(epilogue == VITMI_EPI_STORE || epilogue == VITMI_EPI_DGELU,
+  VITMI_CHECK_ARG((epilogue & ~VITMI_EPI_AUX_TILED) == VITMI_EPI_STORE ||
+                      (epilogue & ~VITMI_EPI_AUX_TILED) == VITMI_EPI_DGELU,
                   "linear_dgrad_bias: bad epilogue %d", epilogue);
   VITMI_CHECK_ARG(db != nullptr, "linear_dgrad_bias: db is null");
   VITMI_CHECK_ARG(workspace && ws_bytes >= vitmi_linear_dgrad_bias_workspace_size(dtype, M, N, K),

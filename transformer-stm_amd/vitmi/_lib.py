@@ -37,6 +37,7 @@ SIGNATURES = {
     "vitmi_gemm_set_policy": (I, [I]),
     "vitmi_linear_fwd": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P, S, P]),
     "vitmi_linear_fwd_workspace_size": (S, [I, L, L, L]),
+    "vitmi_aux_tiled_bytes": (S, [L, L]),
     "vitmi_linear_dgrad": (I, [I, L, L, L, P, P, P, I, I, P, P, S, P]),
     "vitmi_linear_dgrad_workspace_size": (S, [I, L, L, L]),
     "vitmi_linear_wgrad": (I, [I, L, L, L, P, P, P, P, S, P]),

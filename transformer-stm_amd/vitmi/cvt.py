@@ -276,7 +276,8 @@ class _CvTBlockFn(torch.autograd.Function):
         x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
         h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, cfg.ln_eps, T)
         w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
-        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1])
+        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1],
+                                aux_tiled=T == torch.bfloat16)
         out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])
         ctx.save_for_backward(x2, h, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wo, w1, w2, *saved_proj)
         ctx.blk, ctx.dims, ctx.drop = blk, (B, N, D, H, W, with_cls, scale), drop
@@ -301,7 +302,8 @@ class _CvTBlockFn(torch.autograd.Function):
         else:   # the fc2 branch was dropped: its dgrad/wgrad/bias see g2 * mask / (1 - p)
             g2_lp = ops.dropout_apply(g2, drop[0], drop[2] + 2, drop[1], T)
         # MLP
-        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias))
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias),
+                              aux_tiled=T == torch.bfloat16)
         ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
         ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
         dh2 = ops.linear_dgrad(du, w1, T)

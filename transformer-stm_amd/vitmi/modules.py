@@ -245,7 +245,7 @@ class _MlpFn(torch.autograd.Function):
         x2 = x.contiguous().float().view(-1, shp[-1])
         xo = x2 if T == F32 else ops.cast_bf16(x2)
         w1, w2 = _lp(mod, mod.fc1.weight, T), _lp(mod, mod.fc2.weight, T)
-        a, u = ops.linear_fwd(xo, w1, mod.fc1.bias, T, ops.EPI_BIAS_GELU)
+        a, u = ops.linear_fwd(xo, w1, mod.fc1.bias, T, ops.EPI_BIAS_GELU, aux_tiled=T != F32)
         y = ops.linear_fwd(a, w2, mod.fc2.bias, F32)
         ctx.save_for_backward(xo, a, u, w1, w2)
         ctx.mod, ctx.shape = mod, shp
@@ -258,7 +258,7 @@ class _MlpFn(torch.autograd.Function):
         T = xo.dtype
         g = dy.contiguous().float().view(-1, dy.shape[-1])
         g_lp = _take_lp(g, T, dy)
-        du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mod.fc1.bias))
+        du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mod.fc1.bias), aux_tiled=T != F32)
         ops.linear_wgrad(g_lp, a, _grad(mod.fc2.weight))
         ops.bias_grad(g_lp, _grad(mod.fc2.bias))
         dx = ops.linear_dgrad(du, w1, F32)
@@ -324,7 +324,8 @@ class _BlockFn(torch.autograd.Function):
             dr = [(seed, site0 + j, rate) for j in range(3)]
         x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
         h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
-        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1])
+        # gelu' stays in the tile-native layout between fc1's epilogue and fc2's dgrad (bf16)
+        act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1], aux_tiled=T != F32)
         out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
         ctx.blk, ctx.shape = blk, (B, N, D)
@@ -352,7 +353,7 @@ class _BlockFn(torch.autograd.Function):
             g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
         # MLP branch
         # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
-        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias))
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias), aux_tiled=T != F32)
         ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
         if not ctx.bias_done:
             ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))

@@ -17,6 +17,7 @@ Tensor = torch.Tensor
 
 F32, BF16 = 0, 1
 EPI_STORE, EPI_BIAS_GELU, EPI_RESIDUAL, EPI_DGELU, EPI_ACCUM = 0, 1, 2, 3, 4
+EPI_AUX_TILED = 0x100   # gelu' in the library's tile-native layout (include/vitmi.h)
 LOSS_CE, LOSS_MSE = 0, 1
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
@@ -75,18 +76,25 @@ def dropout_params(p: float):
 
 
 def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dtype,
-               epilogue: int = EPI_STORE, residual: Optional[Tensor] = None, dropout=None):
+               epilogue: int = EPI_STORE, residual: Optional[Tensor] = None, dropout=None,
+               aux_tiled: bool = False):
     """y = x W^T + b (+GELU, +residual).  x [M,K], w [N,K] (same dtype).  Returns y
     (and gelu'(pre-activation), the saved GELU derivative, for EPI_BIAS_GELU).
     ``dropout`` = (seed, site, rate) fuses the dropout of the GELU output / of the branch
-    before the residual add into the epilogue (vitmi_linear_fwd_dropout)."""
+    before the residual add into the epilogue (vitmi_linear_fwd_dropout).
+    ``aux_tiled`` (bf16): gelu' comes back as an opaque buffer in the tile-native layout, for a
+    linear_dgrad(..., EPI_DGELU, aux_tiled=True) of the same [M, N]."""
     assert x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N = w.shape[0]
     assert w.shape[1] == K
     y = torch.empty(*x.shape[:-1], N, dtype=out_dtype, device=x.device)
     aux = None
-    if epilogue == EPI_BIAS_GELU:
+    aux_tiled = aux_tiled and epilogue == EPI_BIAS_GELU
+    if aux_tiled:
+        aux = torch.empty(lib().vitmi_aux_tiled_bytes(M, N) // 2, dtype=x.dtype, device=x.device)
+        epilogue |= EPI_AUX_TILED
+    elif epilogue == EPI_BIAS_GELU:
         aux = torch.empty(*x.shape[:-1], N, dtype=x.dtype, device=x.device)
     if residual is not None:
         assert residual.is_contiguous() and residual.dtype == torch.float32
@@ -108,7 +116,7 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
     if probe:
         e1.record()
         _PROBE["events"].append((e0, e1))
-    return (y, aux) if epilogue == EPI_BIAS_GELU else y
+    return (y, aux) if epilogue & ~EPI_AUX_TILED == EPI_BIAS_GELU else y
 
 
 def dropout_apply(x: Tensor, seed: int, site: int, rate: float, out_dtype: torch.dtype) -> Tensor:
@@ -124,11 +132,15 @@ def dropout_apply(x: Tensor, seed: int, site: int, rate: float, out_dtype: torch
 
 
 def linear_dgrad(dy: Tensor, w: Tensor, out_dtype: torch.dtype, epilogue: int = EPI_STORE,
-                 aux: Optional[Tensor] = None, bias_grad: Optional[Tensor] = None) -> Tensor:
-    """dx[M,K] = dy[M,N] W[N,K] (optionally * aux, the gelu' saved by the forward).
+                 aux: Optional[Tensor] = None, bias_grad: Optional[Tensor] = None,
+                 aux_tiled: bool = False) -> Tensor:
+    """dx[M,K] = dy[M,N] W[N,K] (optionally * aux, the gelu' saved by the forward; ``aux_tiled``:
+    aux is the tile-native buffer of linear_fwd(..., aux_tiled=True)).
     ``bias_grad`` (fp32 [K]) += column sums of dx, fused into the GEMM epilogue where the
     kernel allows (vitmi_linear_dgrad_bias)."""
     assert dy.is_contiguous() and w.is_contiguous() and dy.dtype == w.dtype
+    if aux_tiled and epilogue == EPI_DGELU:
+        epilogue |= EPI_AUX_TILED
     M, N = dy.numel() // dy.shape[-1], dy.shape[-1]
     K = w.shape[1]
     dx = torch.empty(*dy.shape[:-1], K, dtype=out_dtype, device=dy.device)
