@@ -25,6 +25,32 @@
 // store reads the stale soffset and lands on another row group (seen on the GELU-dropout and
 // residual epilogues).
 #define VMEM_SGPR_GUARD "s_nop 4\n\t"
+// cache-policy modifiers of the epilogue's output stores (empty: the default policy)
+// (VITMI_ST_MASK bits: 1 = gelu' aux, 2 = bf16 C, 4 = fp32 C / residual output, 8 = split-K
+// partial slabs; the bit's stores carry the non-temporal hint)
+#ifndef VITMI_ST_MASK
+#define VITMI_ST_MASK 3
+#endif
+#if VITMI_ST_MASK & 1
+#define VITMI_ST_AUX " nt"
+#else
+#define VITMI_ST_AUX ""
+#endif
+#if VITMI_ST_MASK & 2
+#define VITMI_ST_C16 " nt"
+#else
+#define VITMI_ST_C16 ""
+#endif
+#if VITMI_ST_MASK & 4
+#define VITMI_ST_C32 " nt"
+#else
+#define VITMI_ST_C32 ""
+#endif
+#if VITMI_ST_MASK & 8
+#define VITMI_ST_PART " nt"
+#else
+#define VITMI_ST_PART ""
+#endif
 
 namespace vitmi {
 
@@ -823,7 +849,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       // LDS executes one wave's accesses in order)
       auto lane_xchg = [] { asm volatile("" ::: "memory"); };
       // the image of row group mi -> rows m0 + wm*128 + 16 mi + (0..15) of the buffer `r` (bf16, ld)
-      auto flush = [&](__amdgpu_buffer_rsrc_t r, int64_t ld, int mi) {
+      auto flush = [&](__amdgpu_buffer_rsrc_t r, int64_t ld, int mi, bool aux = false) {
         lane_xchg();
         bf16x8 d[2];
         uint32_t vo[2];
@@ -832,12 +858,21 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           d[j] = *(const bf16x8*)(scr + (8 * j + rr) * EPI_PITCH + cc * 16);
           vo[j] = ccok ? (uint32_t)(((int64_t)(wm * 128 + 8 * j + rr) * ld + wn * 64 + cc * 8) * 2) : 0x80000000u;
         }
-        asm volatile(VMEM_SGPR_GUARD
-                     "buffer_store_dwordx4 %0, %2, %4, %5 offen\n\t"
-                     "buffer_store_dwordx4 %1, %3, %4, %5 offen\n\ts_nop 1"
-                     :: "v"(__builtin_bit_cast(u32x4, d[0])), "v"(__builtin_bit_cast(u32x4, d[1])), "v"(vo[0]),
-                        "v"(vo[1]), "s"(r), "s"((int)(mi * 16 * ld * 2))
-                     : "memory");
+        if (aux) {
+          asm volatile(VMEM_SGPR_GUARD
+                       "buffer_store_dwordx4 %0, %2, %4, %5 offen" VITMI_ST_AUX "\n\t"
+                       "buffer_store_dwordx4 %1, %3, %4, %5 offen" VITMI_ST_AUX "\n\ts_nop 1"
+                       :: "v"(__builtin_bit_cast(u32x4, d[0])), "v"(__builtin_bit_cast(u32x4, d[1])), "v"(vo[0]),
+                          "v"(vo[1]), "s"(r), "s"((int)(mi * 16 * ld * 2))
+                       : "memory");
+        } else {
+          asm volatile(VMEM_SGPR_GUARD
+                       "buffer_store_dwordx4 %0, %2, %4, %5 offen" VITMI_ST_C16 "\n\t"
+                       "buffer_store_dwordx4 %1, %3, %4, %5 offen" VITMI_ST_C16 "\n\ts_nop 1"
+                       :: "v"(__builtin_bit_cast(u32x4, d[0])), "v"(__builtin_bit_cast(u32x4, d[1])), "v"(vo[0]),
+                          "v"(vo[1]), "s"(r), "s"((int)(mi * 16 * ld * 2))
+                       : "memory");
+        }
         lane_xchg();   // and the next writes of the image stay after these reads
       };
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand.
@@ -871,8 +906,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           csum[ni] += v;                                       // rows >= M hold 0 (zero A rows)
         }
         if constexpr (CES == 4) {
-          asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
-                       :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
+          if constexpr (EPI == EPI_PARTIAL)
+            asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_PART "\n\ts_nop 1"
+                         :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
+          else
+            asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_C32 "\n\ts_nop 1"
+                         :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
         } else {
           bf16x4 o;
 #pragma unroll
@@ -895,14 +934,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
               const u32x4 w1 = __builtin_bit_cast(u32x4, bf16x8{us[2][0], us[2][1], us[2][2], us[2][3],
                                                                 us[3][0], us[3][1], us[3][2], us[3][3]});
               asm volatile(VMEM_SGPR_GUARD
-                           "buffer_store_dwordx4 %0, %2, %3, %4 offen\n\t"
-                           "buffer_store_dwordx4 %1, %2, %3, %4 offen offset:1024\n\ts_nop 1"
+                           "buffer_store_dwordx4 %0, %2, %3, %4 offen" VITMI_ST_AUX "\n\t"
+                           "buffer_store_dwordx4 %1, %2, %3, %4 offen offset:1024" VITMI_ST_AUX "\n\ts_nop 1"
                            :: "v"(w0), "v"(w1), "v"((uint32_t)(wave * 16384 + lane * 16)), "s"(ru), "s"(mi * 2048)
                            : "memory");
             } else {
 #pragma unroll
               for (int ni = 0; ni < 4; ++ni) lds_put(ni, us[ni]);
-              flush(ru, g.ldaux, mi);
+              flush(ru, g.ldaux, mi, true);
             }
           }
         }
@@ -1022,7 +1061,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
                 lane_xchg();   // every lane's read before the next pass rewrites the image
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                  asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
+                  asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen" VITMI_ST_C32 "\n\ts_nop 1"
                                :: "v"(d[j]), "v"(vo32(pp, j, g.ldc)), "s"(rc), "s"((int)(mi * 16 * g.ldc * 4))
                                : "memory");
               }
