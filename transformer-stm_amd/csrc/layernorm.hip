@@ -10,15 +10,25 @@
 
 namespace vitmi {
 
+// Outputs leave with the non-temporal hint, as gemm256's bf16 outputs (VITMI_NT_LN): forward
+// 36.7 -> 34.9 us, backward 126 -> 122 us, step +0.4 % (profiles/r03_store_nt/ln_*)
+#ifndef VITMI_NT_LN
+#define VITMI_NT_LN 1
+#endif
+template <typename V>
+__device__ __forceinline__ void put(V* p, V v) {
+  if constexpr (VITMI_NT_LN) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 template <typename TY>
 __device__ __forceinline__ void store4(TY* p, f32x4 v);
 template <>
-__device__ __forceinline__ void store4<float>(float* p, f32x4 v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void store4<float>(float* p, f32x4 v) { put((f32x4*)p, v); }
 template <>
 __device__ __forceinline__ void store4<bf16>(bf16* p, f32x4 v) {
   bf16x4 b;
   b[0] = (bf16)v[0]; b[1] = (bf16)v[1]; b[2] = (bf16)v[2]; b[3] = (bf16)v[3];
-  *(bf16x4*)p = b;
+  put((bf16x4*)p, b);
 }
 template <typename T>
 __device__ __forceinline__ f32x4 load4(const T* p);
@@ -131,7 +141,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       if (c < D) {
         const f32x4 o = (gy[i] - c1 - xh[i] * c2) * rs + rv[i];
         ds[i] += o;
-        *(f32x4*)(dx + row * lddx + c) = o;
+        put((f32x4*)(dx + row * lddx + c), o);
         if (LP) store4<bf16>(dx_lp + row * lddx_lp + c, o);
       }
     }
