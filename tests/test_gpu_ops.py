@@ -332,6 +332,41 @@ def test_attention_fwd_bwd(B, N, H, T, path, attn_policy):
         assert rel(d[:, i], g[:, i]) < (2e-2 if T == BF else 1e-5), name
 
 
+@pytest.mark.parametrize("B,N,H", [(48, 197, 12), (24, 224, 12), (40, 193, 9), (3, 197, 1)])
+def test_attention_persistent_many_pairs(B, N, H):
+    """N in (192, 224] at many (batch, head) pairs: the persistent dK/dV kernel walks several
+    pairs per workgroup with the next pair's Q | dO (inline-asm LDS-DMA) and K/V rows (inline-asm
+    loads) in flight (more pairs than CUs here, and fewer: B*H = 3); vs the fp32 reference, vs
+    the streamed kernels, and bitwise equal across runs."""
+    D = 64 * H
+    scale = 64 ** -0.5
+    qkv = rnd(B * N, 3 * D, dtype=BF, seed=41)
+    do = rnd(B * N, D, dtype=BF, seed=42)
+    o, lse = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
+    o_again, lse_again = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
+    assert torch.equal(o, o_again) and torch.equal(lse, lse_again)
+    o_ref, lse_ref = attn_ref(qkv, B, N, H, scale)
+    assert rel(o.float(), o_ref) < 1e-2
+    assert rel(lse, lse_ref) < 1e-5
+    dqkv = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
+    assert torch.equal(dqkv, ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale))
+    prev = ops.attention_set_policy(1)
+    try:
+        o_s, lse_s = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
+        d_s = ops.attention_bwd(qkv.to(DEV), o_s, do.to(DEV), lse_s, B, N, H, scale)
+    finally:
+        ops.attention_set_policy(prev)
+    assert rel(o.float(), o_s.float()) < 1e-2
+    assert rel(dqkv.float(), d_s.float()) < 2e-2
+    qq = qkv.float().clone().requires_grad_()
+    o2, _ = attn_ref(qq, B, N, H, scale)
+    o2.backward(do.float())
+    g = qq.grad.view(B * N, 3, D)
+    d = dqkv.float().cpu().view(B * N, 3, D)
+    for i, name in enumerate("qkv"):
+        assert rel(d[:, i], g[:, i]) < 2e-2, name
+
+
 @pytest.mark.parametrize("B,N,H", [(2, 197, 2), (1, 17, 3), (3, 1, 2), (1, 130, 1), (1, 256, 1),
                                    (2, 255, 1), (1, 33, 2), (1, 96, 1), (4, 197, 12)])
 def test_attention_bwd_single_pass(B, N, H):

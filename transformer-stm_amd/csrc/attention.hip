@@ -593,6 +593,18 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq_bf16(
 // 2 x 7 co-resident waves interleave freely.  Rows are padded to NP = 32*NW only (the
 // streamed kernels above pad to 128 queries x 64 keys: 1.69x the work at N = 197, here 1.29x).
 
+// One 1-KiB LDS-DMA piece (64 lanes x 16 B at lds) in inline asm.  The builtin form makes hipcc
+// emit `s_waitcnt vmcnt(0)` before LDS reads it cannot prove disjoint from a pending DMA (here:
+// the V reads of this pair against the next pair's pieces), which drains the prefetch every
+// pair; hidden from the compiler the pieces are counted by the kernel's own waits only (it has
+// no compiler-visible vector loads in its loop).  "s_nop 4": the descriptor may come from a VALU
+// write (v_readfirstlane); "s_nop 0": M0 written by SALU before the LDS-DMA reads it.
+__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rs, uint32_t voff, char* lds) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)LDS_PTR(char, lds);
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :: "v"(voff), "s"(rs), "s"(m0) : "memory");   // (hipcc reserves M0; no compiler code here uses it)
+}
+
 // Stage rows [0, NP) (128 B of one head each) of a token-major matrix into an LDS image.
 __device__ __forceinline__ void stage_seq(char* lds, __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int np,
                                           int nw, int wave, int lane) {
@@ -601,6 +613,33 @@ __device__ __forceinline__ void stage_seq(char* lds, __amdgpu_buffer_rsrc_t rs, 
     const int c = (lane & 7) ^ att_swz(r);
     const uint32_t voff = (uint32_t)((int64_t)r * ld_bytes + c * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, lds + p * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// Vector loads the compiler does not count (their destinations must not be read before the
+// caller's own s_waitcnt and a "+v" statement on them; cdna_hip_programming.md §5.7 item 1 form
+// (ii)).  The range check returns 0 past the descriptor's size.
+__device__ __forceinline__ u32x4 asm_load16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int imm) {
+  u32x4 v;
+  if (imm == 0) asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen" : "=&v"(v) : "v"(voff), "s"(rs) : "memory");
+  else if (imm == 32) asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen offset:32" : "=&v"(v) : "v"(voff), "s"(rs) : "memory");
+  else if (imm == 64) asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen offset:64" : "=&v"(v) : "v"(voff), "s"(rs) : "memory");
+  else asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen offset:96" : "=&v"(v) : "v"(voff), "s"(rs) : "memory");
+  return v;
+}
+__device__ __forceinline__ float asm_load4(__amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+  float v;
+  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, 0 offen" : "=&v"(v) : "v"(voff), "s"(rs) : "memory");
+  return v;
+}
+
+// stage_seq with the pieces issued by dma_piece (no compiler-visible LDS-DMA; see there)
+__device__ __forceinline__ void stage_seq_dma(char* lds, __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int np,
+                                              int nw, int wave, int lane) {
+  for (int p = wave; p < np / 8; p += nw) {
+    const int r = p * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ att_swz(r);
+    dma_piece(rs, (uint32_t)((int64_t)r * ld_bytes + c * 16), lds + p * 1024);
   }
 }
 
@@ -846,8 +885,8 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
   auto stage_pair = [&](int bh, int buf) {
     const int b = bh / H, hd = bh - b * H;
     const bf16* base = qkv + (int64_t)b * N * ld;
-    stage_seq(smem[buf], make_rsrc(base + hd * DH, bytes - hd * DH * 2), ldb, NP, nw, wave, lane);
-    stage_seq(smem[buf] + NP * 128, make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2), ldo, NP,
+    stage_seq_dma(smem[buf], make_rsrc(base + hd * DH, bytes - hd * DH * 2), ldb, NP, nw, wave, lane);
+    stage_seq_dma(smem[buf] + NP * 128, make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2), ldo, NP,
               nw, wave, lane);
   };
   auto load_regs = [&](int bh, bf16x8 (&kf)[4], bf16x8 (&vf)[4], float& ls, float& dv) {
@@ -855,14 +894,16 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     const bf16* base = qkv + (int64_t)b * N * ld;
     const __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
     const __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+    // inline-asm loads (see the loop head): the range check returns 0 past N
+    const uint32_t kvoff = (uint32_t)((int64_t)key * ldb + 16 * h);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      kf[s] = load_row16(rk, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
-      vf[s] = load_row16(rv, (uint32_t)((int64_t)key * ldb + (16 * s + 8 * h) * 2));
+      kf[s] = __builtin_bit_cast(bf16x8, asm_load16(rk, kvoff, 32 * s));
+      vf[s] = __builtin_bit_cast(bf16x8, asm_load16(rv, kvoff, 32 * s));
     }
-    const int i = threadIdx.x;
-    ls = i < N ? lse[(int64_t)bh * N + i] : 0.f;
-    dv = i < N ? delta[(int64_t)bh * N + i] : 0.f;
+    const uint32_t ioff = (uint32_t)threadIdx.x * 4;
+    ls = asm_load4(make_rsrc(lse + (int64_t)bh * N, (uint32_t)N * 4), ioff);
+    dv = asm_load4(make_rsrc(delta + (int64_t)bh * N, (uint32_t)N * 4), ioff);
   };
 
   int bh = blockIdx.x;
@@ -880,6 +921,12 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     else if (colsum && wave == 0) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     first = false;
+    // The K/V rows, lse and delta arrive by inline-asm loads and the next pair's Q | dO by
+    // inline-asm LDS-DMA (dma_piece): with compiler-visible loads hipcc waited vmcnt(0) here
+    // (the merge of the prologue and loop-carried states), draining the prefetch every pair.
+    // The wait above retired them; this statement is their definition point for the compiler.
+    asm volatile("" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(vf[0]), "+v"(vf[1]), "+v"(vf[2]),
+                 "+v"(vf[3]), "+v"(ls), "+v"(dv));
     if (threadIdx.x < NP) {
       const int i = threadIdx.x;
       l2s[i] = i < N ? ls * LOG2E : INFINITY;

@@ -1384,6 +1384,8 @@ static int launch_layout(int ak, int bk, GemmArgs g, int splits, bool big, hipSt
   if (ak && bk) return launch_t<T, true, true, EPI, TC>(g, splits, big, s);
   if (ak && !bk) return launch_t<T, true, false, EPI, TC>(g, splits, big, s);
   if (!ak && !bk) return launch_t<T, false, false, EPI, TC>(g, splits, big, s);
+  // A m-major x B k-major: weight gradients with the input operand stored transposed
+  if constexpr (EPI == EPI_PARTIAL || EPI == VITMI_EPI_ACCUM) return launch_t<T, false, true, EPI, TC>(g, splits, big, s);
   return fail(VITMI_ERR_UNSUPPORTED, "gemm: layout A m-major x B k-major not instantiated");
 }
 
