@@ -129,6 +129,16 @@ int vitmi_linear_dgrad_bias(int dtype, int64_t M, int64_t N, int64_t K, const vo
                             vitmi_stream_t stream);
 
 size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
+/* The same dW[N,K] += dy^T x with one operand given token-contiguous (transposed copies that the
+ * LayerNorm kernels below write beside their row-major outputs), so the GEMM reads only one
+ * operand with transposing LDS reads (models/CvT(Par).py:132-134,254,256: the Dense kernels'
+ * gradients).  _xt: x given as xt[K][ldxt] (ldxt >= M); _dyt: dy given as dyt[N][lddyt].
+ * Workspaces: vitmi_linear_wgrad_xt_workspace_size / vitmi_linear_wgrad_workspace_size. */
+int vitmi_linear_wgrad_xt(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* xt,
+                          int64_t ldxt, float* dw, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
+size_t vitmi_linear_wgrad_xt_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
+int vitmi_linear_wgrad_dyt(int dtype, int64_t M, int64_t N, int64_t K, const void* dyt, int64_t lddyt,
+                           const void* x, float* dw, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 /* db[N] (f32) += sum_m dy[m, n]  (dy [M][ldy] of `dtype`) */
 int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, int64_t ldy, float* db,
                     void* workspace, size_t ws_bytes, vitmi_stream_t stream);
@@ -150,6 +160,18 @@ int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtype, int64_t 
                         int64_t lddx, void* dx_lp, int64_t lddx_lp, float* dgamma, float* dbeta,
                         float* dxsum, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D);
+/* The same with the bf16 output also written transposed (yt / dxt [D][ldt], ldt >= M and a
+ * multiple of 8): the token-contiguous operand of the weight-gradient GEMMs
+ * (vitmi_linear_wgrad_xt / _dyt).  bf16 only; D <= 1024.  _bwd_t needs dx_lp. */
+int vitmi_layernorm_fwd_t(int64_t M, int D, const float* x, int64_t ldx, const float* gamma,
+                          const float* beta, float eps, void* y, int64_t ldy, void* yt, int64_t ldt,
+                          float* mean, float* rstd, vitmi_stream_t stream);
+int vitmi_layernorm_bwd_t(int64_t M, int D, const void* dy, int dy_dtype, int64_t lddy,
+                          const float* x, int64_t ldx, const float* mean, const float* rstd,
+                          const float* gamma, const float* dres, int64_t ldres, float* dx,
+                          int64_t lddx, void* dx_lp, int64_t lddx_lp, void* dxt, int64_t ldt,
+                          float* dgamma, float* dbeta, float* dxsum, void* workspace, size_t ws_bytes,
+                          vitmi_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * Multi-head scaled-dot-product attention (layers.MultiHeadAttention called (q, v, k),

@@ -266,6 +266,52 @@ def test_layernorm_fwd_bwd(D, T):
     assert rel(dsum, 2.0 + (xx.grad + dres).sum(0)) < 1e-5   # fused bias-grad column sums
 
 
+@pytest.mark.parametrize("M,D", [(197 * 3, 768), (64, 384), (33, 64), (256 * 197, 768)])
+def test_layernorm_transposed_outputs(M, D):
+    """layernorm_fwd_t / layernorm_bwd_t (32-row tiles through LDS) == the row-kernels' bf16
+    outputs bit for bit, with the transposed copies equal to their transposes (M not a multiple
+    of 32 included); the parameter-gradient partials sum in another order (1e-5)."""
+    x = (rnd(M, D, seed=71) * 2 + 0.5).to(DEV)
+    w, b = (1 + 0.1 * rnd(D, seed=72)).to(DEV), (0.1 * rnd(D, seed=73)).to(DEV)
+    y, mean, rstd = ops.layernorm_fwd(x, w, b, 1e-6, BF)
+    y2, mean2, rstd2, yt = ops.layernorm_fwd_t(x, w, b, 1e-6)
+    assert torch.equal(y, y2) and torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+    assert torch.equal(yt, y.t())
+    dy = rnd(M, D, seed=74).to(BF).to(DEV)
+    dres = rnd(M, D, seed=75).to(DEV)
+    grads = []
+    for _ in range(2):
+        dg, dbb, dsum = (torch.full((D,), v, device=DEV) for v in (0.5, -0.5, 2.0))
+        grads.append((dg, dbb, dsum))
+    dx, dx_lp = ops.layernorm_bwd(dy, x, mean, rstd, w, *grads[0][:2], dres=dres, lp_dtype=BF, dxsum=grads[0][2])
+    dx2, dx_lp2, dxt = ops.layernorm_bwd_t(dy, x, mean, rstd, w, *grads[1][:2], dres=dres, dxsum=grads[1][2])
+    assert torch.equal(dx, dx2) and torch.equal(dx_lp, dx_lp2) and torch.equal(dxt, dx_lp.t())
+    for a, c in zip(grads[0], grads[1]):
+        assert rel(c, a) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(64 * 9, 384, 192), (1024, 256, 320), (256 * 197, 2304, 768),
+                                   (256 * 197, 768, 3072)])
+def test_linear_wgrad_transposed_operands(M, N, K):
+    """dW += dy^T x with x given transposed (linear_wgrad_xt: the product dW^T through a
+    transposing split-K fold) or dy given transposed (linear_wgrad_dyt) == the token-major
+    linear_wgrad up to fp32 summation order.  (The transposed operand is read k-major: the token
+    count must be a multiple of 64, which the module path checks before taking it.)"""
+    g = torch.Generator(device=DEV).manual_seed(7)
+    dy = (torch.rand(M, N, device=DEV, generator=g) * 2 - 1).to(BF)
+    x = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(BF)
+    base = torch.rand(N, K, device=DEV, generator=g)
+    ref = base.clone()
+    ops.linear_wgrad(dy, x, ref)
+    a = base.clone()
+    ops.linear_wgrad_xt(dy, x.t().contiguous(), a)
+    c = base.clone()
+    ops.linear_wgrad_dyt(dy.t().contiguous(), x, c)
+    assert rel(a, ref) < 1e-6 and rel(c, ref) < 1e-6
+    exact = base.double() + dy.double().t() @ x.double()
+    assert rel(a, exact) < 1e-5
+
+
 def test_layernorm_strided_rows():
     B, N, D = 5, 17, 192
     x = rnd(B, N, D, seed=20)

@@ -95,6 +95,7 @@ struct GemmArgs {
   float* colsum;
   unsigned long long* stamps;        // DIAGNOSTIC build only (VITMI_GEMM_STAMPS)
   int aux_tiled;                     // gelu' in the tile-native layout (VITMI_EPI_AUX_TILED)
+  int ct;                            // EPI_PARTIAL: slabs hold C^T ([N][M], row stride ldc)
 };
 
 // Element (row, col) of a tile-native gelu' buffer (VITMI_EPI_AUX_TILED; bf16 elements): 256x256
@@ -273,7 +274,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_
   } else if constexpr (EPI == EPI_RESIDUAL_DROP) {
     ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + (acc + biasv) * drop_factor(g, row, col);
   } else if constexpr (EPI == EPI_PARTIAL) {
-    ((float*)g.C)[blockIdx.z * g.split_stride + row * g.ldc + col] = acc;
+    ((float*)g.C)[blockIdx.z * g.split_stride + (g.ct ? col * g.ldc + row : row * g.ldc + col)] = acc;
   } else if constexpr (EPI == VITMI_EPI_STORE) {
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc + biasv);
   } else if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
@@ -810,6 +811,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       if constexpr (EPI == EPI_PARTIAL) zoff = (int64_t)(blockIdx.z + zs) * g.split_stride;
       char* cbase = (char*)g.C + (zoff + m0 * g.ldc + n0) * CES;
       const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, clamp_bytes(((g.M - m0) * g.ldc - n0) * CES));
+      // (EPI_PARTIAL with ct: the C^T slab from its element (n0, m0))
+      [[maybe_unused]] const __amdgpu_buffer_rsrc_t rct =
+          make_rsrc((char*)g.C + (zoff + n0 * g.ldc + m0) * 4, clamp_bytes(((g.N - n0) * g.ldc - m0) * 4));
       const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
       const uint32_t vbase = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldc + wn * 64 + lc4) * CES);
       // Branch-free ragged N (straight-line epilogue code schedules far better): lanes past
@@ -906,10 +910,23 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           csum[ni] += v;                                       // rows >= M hold 0 (zero A rows)
         }
         if constexpr (CES == 4) {
-          if constexpr (EPI == EPI_PARTIAL)
-            asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_PART "\n\ts_nop 1"
-                         :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
-          else
+          if constexpr (EPI == EPI_PARTIAL) {
+            if (g.ct) {
+              // C^T slab [N][M]: each of the lane's 4 columns is a slab row; the 16 lanes of a
+              // column group store 16 consecutive m (64 B) per instruction.  Rows >= M dropped.
+              const bool mok = m0 + wm * 128 + mi * 16 + lr < g.M;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const uint32_t vo = cok[ni] && mok ? (uint32_t)(((int64_t)(wn * 64 + ni * 16 + lc4 + e) * g.ldc +
+                                                                 wm * 128 + mi * 16 + lr) * 4) : 0x80000000u;
+                asm volatile(VMEM_SGPR_GUARD "buffer_store_dword %0, %1, %2, 0 offen" VITMI_ST_PART "\n\ts_nop 1"
+                             :: "v"(v[e]), "v"(vo), "s"(rct) : "memory");
+              }
+            } else {
+              asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_PART "\n\ts_nop 1"
+                           :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
+            }
+          } else
             asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_C32 "\n\ts_nop 1"
                          :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
         } else {
@@ -1139,7 +1156,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       constexpr int EP = CES2 ? (EB == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU ? 32 : 16)
                               : (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ? 64
                                  : EPI == VITMI_EPI_DGELU ? 48 : 32);
-      ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : EP;
+      ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : (EPI == EPI_PARTIAL && g.ct ? 128 : EP);
     }
     if (!has_next) break;
     it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
@@ -1443,7 +1460,10 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
                      int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
                      int epi, const float* bias, void* aux, int64_t ldaux, const float* residual,
                      int64_t ldr, void* ws, size_t ws_bytes, hipStream_t s, bool allow_split,
-                     const GemmArgs* drop = nullptr, float* colsum = nullptr, bool* colsum_done = nullptr) {
+                     const GemmArgs* drop = nullptr, float* colsum = nullptr, bool* colsum_done = nullptr,
+                     bool tc = false) {
+  // tc: C^T += A B (EPI_ACCUM only): the split-K slabs are written transposed (EPI_PARTIAL with
+  // ct) and folded into the dense C[N][M] by the plain reduction, whatever the split count
   if (colsum_done) *colsum_done = false;
   const bool aux_tiled = (epi & VITMI_EPI_AUX_TILED) != 0;
   epi &= ~VITMI_EPI_AUX_TILED;
@@ -1459,7 +1479,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   VITMI_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "gemm: A/B must be 16-byte aligned");
   VITMI_CHECK_ARG(ak ? lda >= K : lda >= M, "gemm: lda too small");
   VITMI_CHECK_ARG(bk ? ldb >= K : ldb >= N, "gemm: ldb too small");
-  VITMI_CHECK_ARG(ldc >= N, "gemm: ldc too small");
+  VITMI_CHECK_ARG(ldc >= (tc ? M : N), "gemm: ldc too small");
   const int eb = epi_base(epi);
   if (eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_DGELU)
     VITMI_CHECK_ARG(aux != nullptr && ldaux >= N, "gemm: epilogue needs aux");
@@ -1500,7 +1520,9 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   if (K == 0) g.k_per_split = BK;
   splits = (int)((K + g.k_per_split - 1) / g.k_per_split);
   if (splits < 1) splits = 1;
-  if (splits > 1) {
+  if (tc) VITMI_CHECK_ARG(epi == VITMI_EPI_ACCUM && ws && ws_bytes >= (size_t)splits * M * N * sizeof(float),
+                         "gemm: transposed accumulate needs the split workspace");
+  if (splits > 1 && !tc) {
     const size_t need = (size_t)splits * M * N * sizeof(float);
     if (ws == nullptr || ws_bytes < need) splits = 1, g.k_per_split = ktiles * BK;
   }
@@ -1521,7 +1543,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
     }
   }
   const bool big_ok = big2;
-  if (splits == 1) {
+  if (splits == 1 && !tc) {
     g.k_per_split = (K > 0 ? ktiles : 1) * BK;
     g.tail_ws = (float*)ws;   // tail split of the persistent gemm256 launch (if it fits)
     g.tail_ws_bytes = ws ? ws_bytes : 0;
@@ -1534,11 +1556,12 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   }
   // split-K: partial slabs then one reduction pass into C (+=)
   GemmArgs gp = g;
-  gp.C = ws; gp.ldc = N; gp.split_stride = M * N;
+  gp.C = ws; gp.ldc = tc ? M : N; gp.split_stride = M * N;
+  gp.ct = tc;
   int rc = dtype == VITMI_BF16 ? dispatch<bf16>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big_ok, s)
                                : dispatch<float>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big_ok, s);
   if (rc) return rc;
-  VITMI_CHECK_ARG(ldc == N, "gemm: split-K accumulate needs a dense C");
+  VITMI_CHECK_ARG(ldc == (tc ? M : N), "gemm: split-K accumulate needs a dense C");
   const int64_t n = M * N;
   int blocks = (int)((n / 4 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
@@ -1679,6 +1702,30 @@ extern "C" size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_
   // dW[N,K]: GEMM rows N, cols K, reduction M
   const int splits = choose_splits(dtype, N, K, M);
   return splits > 1 ? (size_t)splits * N * K * sizeof(float) : 0;
+}
+
+extern "C" size_t vitmi_linear_wgrad_xt_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
+  // the transposed product dW^T[K,N]: GEMM rows K, cols N, reduction M; at least one slab
+  const int splits = choose_splits(dtype, K, N, M);
+  return (size_t)(splits > 1 ? splits : 1) * N * K * sizeof(float);
+}
+
+extern "C" int vitmi_linear_wgrad_xt(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* xt,
+                                     int64_t ldxt, float* dw, void* workspace, size_t ws_bytes,
+                                     vitmi_stream_t stream) {
+  // dW[N,K] += sum_m dy[m][n] xt[k][m], formed as the product dW^T = xt dy: A(k,m) = xt (m
+  // contiguous: k-major in GEMM terms), B(m,n) = dy (n contiguous); the slabs are written transposed
+  return gemm_impl(dtype, 1, 0, K, N, M, xt, ldxt, dy, N, dw, K, VITMI_F32, VITMI_EPI_ACCUM, nullptr, nullptr, 0,
+                   nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, true, nullptr, nullptr, nullptr, true);
+}
+
+extern "C" int vitmi_linear_wgrad_dyt(int dtype, int64_t M, int64_t N, int64_t K, const void* dyt, int64_t lddyt,
+                                      const void* x, float* dw, void* workspace, size_t ws_bytes,
+                                      vitmi_stream_t stream) {
+  // dW[N,K] += sum_m dyt[n][m] x[m][k]: A(n,m) = dyt (m contiguous), B(m,k) = x (k contiguous);
+  // workspace: vitmi_linear_wgrad_workspace_size
+  return gemm_impl(dtype, 1, 0, N, K, M, dyt, lddyt, x, K, dw, K, VITMI_F32, VITMI_EPI_ACCUM, nullptr, nullptr, 0,
+                   nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, true);
 }
 
 extern "C" int vitmi_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy,

@@ -24,6 +24,7 @@ product is exact fp32 (f32-input MFMA).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -42,6 +43,11 @@ F32 = torch.float32
 # and it is used only while the tensor is unmodified: autograd may accumulate another gradient
 # into it in place, which bumps its version counter.
 _LP_ATTR = "_vitmi_lp"
+# bf16 weight gradients from token-contiguous operand copies (ops.layernorm_fwd_t / _bwd_t ->
+# ops.linear_wgrad_xt / _dyt) with VITMI_WGRAD_T=1.  Off by default: the GEMMs gain what
+# tools/wgrad_layout.py predicts (-1.1 ms per step) but writing the transposed copies from the
+# LayerNorm kernels costs as much
+WGRAD_T = os.environ.get("VITMI_WGRAD_T", "0") == "1"
 LP_STATS = {"hit": 0, "miss": 0}     # test hook: how often the handed-over copy was used
 
 
@@ -79,21 +85,31 @@ def _take_lp(g: Tensor, T: torch.dtype, src: Optional[Tensor] = None) -> Tensor:
     current, otherwise ``g`` is cast."""
     if T == F32:
         return g
+    return _take_lp2(g, T, src)[0]
+
+
+def _take_lp2(g: Tensor, T: torch.dtype, src: Optional[Tensor] = None):
+    """(``g`` in the compute dtype, its transposed copy [D, rows] or None): as ``_take_lp``, plus
+    the token-contiguous copy a LayerNorm backward may have handed over with it (the operand of
+    ``ops.linear_wgrad_dyt``)."""
+    if T == F32:
+        return g, None
     src = g if src is None else src
     ent = src.__dict__.pop(_LP_ATTR, None)
     if ent is not None:
-        lp, version, ptr = ent
+        lp, version, ptr, lpt = ent
         if src._version == version and src.data_ptr() == ptr and lp.numel() == g.numel() and lp.dtype == T:
             LP_STATS["hit"] += 1
-            return lp.view(g.shape)
+            return lp.view(g.shape), lpt
     LP_STATS["miss"] += 1
-    return ops.cast_bf16(g.contiguous())
+    return ops.cast_bf16(g.contiguous()), None
 
 
-def _handover(g: Tensor, lp: Optional[Tensor]) -> Tensor:
-    """Attach the bf16 copy ``lp`` of ``g`` to the tensor object a backward returns."""
+def _handover(g: Tensor, lp: Optional[Tensor], lpt: Optional[Tensor] = None) -> Tensor:
+    """Attach the bf16 copy ``lp`` of ``g`` (and its transpose ``lpt``) to the tensor object a
+    backward returns."""
     if lp is not None:
-        g.__dict__[_LP_ATTR] = (lp, g._version, g.data_ptr())
+        g.__dict__[_LP_ATTR] = (lp, g._version, g.data_ptr(), lpt)
     return g
 
 
@@ -315,7 +331,15 @@ class _BlockFn(torch.autograd.Function):
         a_ = blk.attn
         wq, wo = _lp(blk, a_.qkv.weight, T), _lp(blk, a_.proj.weight, T)
         w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
-        h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
+        # bf16: the LayerNorm outputs are also written transposed (token-contiguous); the
+        # backward's qkv / fc1 weight gradients read those instead of h1 / h2 (linear_wgrad_xt)
+        # (the GEMM reads the transposed copies k-major: the token count must be a multiple of 64)
+        xt = T != F32 and WGRAD_T and M % 64 == 0
+        if xt:
+            h1, m1, r1, h1s = ops.layernorm_fwd_t(x2, n1.weight, n1.bias, blk.eps)
+        else:
+            h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
+            h1s = h1
         qkv = ops.linear_fwd(h1, wq, a_.qkv.bias, T)
         o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
         dr = [None, None, None]
@@ -323,29 +347,35 @@ class _BlockFn(torch.autograd.Function):
             seed, rate, site0 = drop
             dr = [(seed, site0 + j, rate) for j in range(3)]
         x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
-        h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
+        if xt:
+            h2, m2, r2, h2s = ops.layernorm_fwd_t(x1, n2.weight, n2.bias, blk.eps)
+        else:
+            h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
+            h2s = h2
         # gelu' stays in the tile-native layout between fc1's epilogue and fc2's dgrad (bf16)
         act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1], aux_tiled=T != F32)
         out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])
-        ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
-        ctx.blk, ctx.shape = blk, (B, N, D)
+        ctx.save_for_backward(x2, h1s, m1, r1, qkv, o, lse, x1, h2s, m2, r2, u, act, wq, wo, w1, w2)
+        ctx.blk, ctx.shape, ctx.xt = blk, (B, N, D), xt
         ctx.prev_bias, ctx.bias_done, ctx.drop = prev_fc2_bias, fc2_bias_done, drop
         ctx.first = first
         return out.view(B, N, D)
 
     @staticmethod
     def backward(ctx, dout):
-        (x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2) = ctx.saved_tensors
+        # h1s / h2s: the LayerNorm outputs, transposed [D, M] when ctx.xt
+        (x2, h1s, m1, r1, qkv, o, lse, x1, h2s, m2, r2, u, act, wq, wo, w1, w2) = ctx.saved_tensors
         blk, (B, N, D) = ctx.blk, ctx.shape
         M = B * N
-        T = h1.dtype
+        T = h1s.dtype
         lpT = None if T == F32 else T
         n1, n2 = blk.norm1, blk._norm2
         a_, mlp = blk.attn, blk.mlp
         g2 = dout.contiguous().float().view(M, D)
         drop = ctx.drop
+        g2_lpt = None
         if drop is None:
-            g2_lp = _take_lp(g2, T, dout)
+            g2_lp, g2_lpt = _take_lp2(g2, T, dout)
         else:
             # the fc2 branch was dropped: its dgrad/wgrad/bias see g2 * mask / (1 - p)
             dout.__dict__.pop(_LP_ATTR, None)
@@ -354,10 +384,16 @@ class _BlockFn(torch.autograd.Function):
         # MLP branch
         # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
         du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias), aux_tiled=T != F32)
-        ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
+        if g2_lpt is not None:
+            ops.linear_wgrad_dyt(g2_lpt, act, _grad(mlp.fc2.weight))
+        else:
+            ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
         if not ctx.bias_done:
             ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
-        ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
+        if ctx.xt:
+            ops.linear_wgrad_xt(du, h2s, _grad(mlp.fc1.weight))
+        else:
+            ops.linear_wgrad(du, h2s, _grad(mlp.fc1.weight))
         dh2 = ops.linear_dgrad(du, w1, T)
         # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
         if drop is None:
@@ -376,19 +412,28 @@ class _BlockFn(torch.autograd.Function):
         # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale,
                                  bias_grad=_grad(a_.qkv.bias) if a_.qkv.bias is not None else None)
-        ops.linear_wgrad(dqkv, h1, _grad(a_.qkv.weight))
+        if ctx.xt:
+            ops.linear_wgrad_xt(dqkv, h1s, _grad(a_.qkv.weight))
+        else:
+            ops.linear_wgrad(dqkv, h1s, _grad(a_.qkv.weight))
         dh1 = ops.linear_dgrad(dqkv, wq, T)
         prev = ctx.prev_bias
         # the bf16 copy of dx is for a consumer that takes it (the block below); the patch
         # embedding's backward reads dx in fp32
         want_lp = drop is None and not ctx.first
-        dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
-                                      dres=dx1, lp_dtype=lpT if want_lp else None,
-                                      dxsum=_grad(prev) if prev is not None else None)
+        dx_lpt = None
+        if want_lp and lpT is not None and WGRAD_T and M % 64 == 0:
+            # with its transpose: the fc2 weight gradient of the block below (linear_wgrad_dyt)
+            dx, dx_lp, dx_lpt = ops.layernorm_bwd_t(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
+                                                    dres=dx1, dxsum=_grad(prev) if prev is not None else None)
+        else:
+            dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
+                                          dres=dx1, lp_dtype=lpT if want_lp else None,
+                                          dxsum=_grad(prev) if prev is not None else None)
         hook = getattr(blk, "_grad_ready_hook", None)
         if hook is not None:
             hook(blk)
-        out = _handover(dx.view(B, N, D), dx_lp)
+        out = _handover(dx.view(B, N, D), dx_lp, dx_lpt)
         return (out, None, None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 6)
 
 
