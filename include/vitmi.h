@@ -160,6 +160,12 @@ int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtype, int64_t 
                         int64_t lddx, void* dx_lp, int64_t lddx_lp, float* dgamma, float* dbeta,
                         float* dxsum, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D);
+/* Residual add fused into the forward: xo = x + yb (fp32 residual stream + a bf16 branch output,
+ * [M][ldyb]), then y = LN(xo) (models/CvT(Par).py:261-289: the out-projection's residual add
+ * followed by the second LayerNorm).  xo fp32 [M][ldxo]. */
+int vitmi_layernorm_fwd_res(int64_t M, int D, const float* x, int64_t ldx, const void* yb, int64_t ldyb,
+                            const float* gamma, const float* beta, float eps, float* xo, int64_t ldxo, void* y,
+                            int y_dtype, int64_t ldy, float* mean, float* rstd, vitmi_stream_t stream);
 /* The same with the bf16 output also written transposed (yt / dxt [D][ldt], ldt >= M and a
  * multiple of 8): the token-contiguous operand of the weight-gradient GEMMs
  * (vitmi_linear_wgrad_xt / _dyt).  bf16 only; D <= 1024.  _bwd_t needs dx_lp. */

@@ -266,6 +266,21 @@ def test_layernorm_fwd_bwd(D, T):
     assert rel(dsum, 2.0 + (xx.grad + dres).sum(0)) < 1e-5   # fused bias-grad column sums
 
 
+@pytest.mark.parametrize("D", [64, 384, 768, 1024])
+@pytest.mark.parametrize("T", [BF, torch.float32])
+def test_layernorm_fwd_residual(D, T):
+    """layernorm_fwd_res: xo = x + y (bf16 branch output) bit for bit, and LN(xo) == the plain
+    LayerNorm kernel on xo bit for bit."""
+    M = 197 * 2 + 3
+    x = (rnd(M, D, seed=81) * 2 + 0.5).to(DEV)
+    yb = rnd(M, D, seed=82).to(BF).to(DEV)
+    w, b = (1 + 0.1 * rnd(D, seed=83)).to(DEV), (0.1 * rnd(D, seed=84)).to(DEV)
+    xo, h, mean, rstd = ops.layernorm_fwd_res(x, yb, w, b, 1e-6, T)
+    assert torch.equal(xo, x + yb.float())
+    h2, mean2, rstd2 = ops.layernorm_fwd(xo, w, b, 1e-6, T)
+    assert torch.equal(h, h2) and torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+
+
 @pytest.mark.parametrize("M,D", [(197 * 3, 768), (64, 384), (33, 64), (256 * 197, 768)])
 def test_layernorm_transposed_outputs(M, D):
     """layernorm_fwd_t / layernorm_bwd_t (32-row tiles through LDS) == the row-kernels' bf16

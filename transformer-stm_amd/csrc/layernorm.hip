@@ -164,6 +164,63 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
+// ------------------------------------------------ residual add fused into the forward
+// xo = x + y (fp32 residual stream + the bf16 branch output), then LayerNorm of xo: the
+// out-projection GEMM of the block then stores its output as bf16 (a plain-store epilogue)
+// instead of loading and storing the fp32 residual tile in its epilogue, where those loads and
+// stores sit serialised after the K-loop (K = 768: about half that GEMM's time).
+template <int NV, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_res_kernel(int64_t M, int D, const float* __restrict__ x, int64_t ldx,
+                                                         const bf16* __restrict__ yb, int64_t ldyb,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps,
+                                                         float* __restrict__ xo, int64_t ldxo,
+                                                         TY* __restrict__ y, int64_t ldy,
+                                                         float* __restrict__ mean, float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + row * ldx;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    v[i] = c < D ? *(const f32x4*)(xr + c) + load4<bf16>(yb + row * ldyb + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    if (c < D) *(f32x4*)(xo + row * ldxo + c) = v[i];   // default policy: LN backward re-reads it
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    if (c < D) {
+      const f32x4 d = v[i] - mu;
+      q += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+  TY* yr = y + row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + 64 * i) * 4;
+    if (c < D) {
+      const f32x4 g = *(const f32x4*)(gamma + c);
+      const f32x4 b = *(const f32x4*)(beta + c);
+      store4<TY>(yr + c, (v[i] - mu) * rs * g + b);
+    }
+  }
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
 // ------------------------------------------------ transposed bf16 copies (weight-gradient operands)
 // The weight-gradient GEMMs reduce over tokens; with both operands token-major (TN) every
 // fragment is a transposed LDS read, and the A side's reads bound the loop (tools/wgrad_layout.py:
@@ -583,5 +640,40 @@ extern "C" int vitmi_layernorm_bwd_t(int64_t M, int D, const void* dy, int dy_dt
   hipLaunchKernelGGL(ln_param_reduce, dim3((D + 15) / 16), dim3(1024), 0, s, (const float*)part, G, D, dgamma,
                      dbeta, dxsum);
   VITMI_LAUNCH_CHECK("layernorm_bwd_t");
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_layernorm_fwd_res(int64_t M, int D, const float* x, int64_t ldx, const void* yb,
+                                       int64_t ldyb, const float* gamma, const float* beta, float eps,
+                                       float* xo, int64_t ldxo, void* y, int y_dtype, int64_t ldy, float* mean,
+                                       float* rstd, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "layernorm_fwd_res: D must be a multiple of 4 in [4, 2048]");
+  VITMI_CHECK_ARG(ldx % 4 == 0 && ldyb % 4 == 0 && ldxo % 4 == 0 && ldy % 4 == 0,
+                  "layernorm_fwd_res: strides must be multiples of 4");
+  if (M == 0) return VITMI_OK;
+  VITMI_CHECK_ARG(x && yb && gamma && beta && xo && y && mean && rstd, "layernorm_fwd_res: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((M + 3) / 4));
+  const int nv = (D + 255) / 256;
+  const double by = (double)M * D * (4 + 2 + 4 + (y_dtype == VITMI_BF16 ? 2 : 4)) + 8.0 * M;
+#define LNFR(NV)                                                                                  \
+  if (y_dtype == VITMI_BF16) {                                                                    \
+    hipLaunchKernelGGL((ln_fwd_res_kernel<NV, bf16>), grid, dim3(256), 0, s, M, D, x, ldx, (const bf16*)yb, ldyb, \
+                       gamma, beta, eps, xo, ldxo, (bf16*)y, ldy, mean, rstd);                    \
+    VITMI_STAT((ln_fwd_res_kernel<NV, bf16>), 0, by);                                             \
+  } else {                                                                                        \
+    hipLaunchKernelGGL((ln_fwd_res_kernel<NV, float>), grid, dim3(256), 0, s, M, D, x, ldx, (const bf16*)yb, ldyb, \
+                       gamma, beta, eps, xo, ldxo, (float*)y, ldy, mean, rstd);                   \
+    VITMI_STAT((ln_fwd_res_kernel<NV, float>), 0, by);                                            \
+  }
+  switch (nv) {
+    case 1: LNFR(1) break;
+    case 2: LNFR(2) break;
+    case 3: LNFR(3) break;
+    case 4: LNFR(4) break;
+    default: LNFR(8) break;
+  }
+#undef LNFR
+  VITMI_LAUNCH_CHECK("layernorm_fwd_res");
   return VITMI_OK;
 }

@@ -50,6 +50,7 @@ SIGNATURES = {
     "vitmi_layernorm_fwd": (I, [L, I, P, L, P, P, F, P, I, L, P, P, P]),
     "vitmi_layernorm_bwd": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, P, P, P, S, P]),
     "vitmi_layernorm_bwd_workspace_size": (S, [L, I]),
+    "vitmi_layernorm_fwd_res": (I, [L, I, P, L, P, L, P, P, F, P, L, P, I, L, P, P, P]),
     "vitmi_layernorm_fwd_t": (I, [L, I, P, L, P, P, F, P, L, P, L, P, P, P]),
     "vitmi_layernorm_bwd_t": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, L, P, P, P, P, S, P]),
     "vitmi_attention_fwd": (I, [I, I, I, I, I, F, P, P, P, P]),

@@ -48,6 +48,10 @@ _LP_ATTR = "_vitmi_lp"
 # tools/wgrad_layout.py predicts (-1.1 ms per step) but writing the transposed copies from the
 # LayerNorm kernels costs as much
 WGRAD_T = os.environ.get("VITMI_WGRAD_T", "0") == "1"
+# bf16 with VITMI_RES_IN_LN=1: the out-projection stores a bf16 output and the LayerNorm after it
+# adds the residual (ops.layernorm_fwd_res).  Off by default: the GEMM saves what the LayerNorm
+# then spends (proj 105 -> 71 us, LN2 40 -> 74 us per layer)
+RES_IN_LN = os.environ.get("VITMI_RES_IN_LN", "0") == "1"
 LP_STATS = {"hit": 0, "miss": 0}     # test hook: how often the handed-over copy was used
 
 
@@ -346,12 +350,19 @@ class _BlockFn(torch.autograd.Function):
         if drop is not None:
             seed, rate, site0 = drop
             dr = [(seed, site0 + j, rate) for j in range(3)]
-        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
-        if xt:
-            h2, m2, r2, h2s = ops.layernorm_fwd_t(x1, n2.weight, n2.bias, blk.eps)
-        else:
-            h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
+        if T != F32 and dr[0] is None and not xt and RES_IN_LN:
+            # bf16: the out-projection stores its output as bf16 and LN2 adds the residual
+            # (ops.layernorm_fwd_res) instead of an fp32 load + store in the GEMM epilogue
+            y = ops.linear_fwd(o, wo, a_.proj.bias, T)
+            x1, h2, m2, r2 = ops.layernorm_fwd_res(x2, y, n2.weight, n2.bias, blk.eps, T)
             h2s = h2
+        else:
+            x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
+            if xt:
+                h2, m2, r2, h2s = ops.layernorm_fwd_t(x1, n2.weight, n2.bias, blk.eps)
+            else:
+                h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
+                h2s = h2
         # gelu' stays in the tile-native layout between fc1's epilogue and fc2's dgrad (bf16)
         act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1], aux_tiled=T != F32)
         out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])

@@ -231,6 +231,21 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.
     return y, mean, rstd
 
 
+def layernorm_fwd_res(x: Tensor, yb: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.dtype):
+    """xo = x (fp32) + yb (bf16), y = LayerNorm(xo): returns (xo fp32 [M, D], y [M, D], mean, rstd)."""
+    assert x.dtype == torch.float32 and yb.dtype == torch.bfloat16
+    M, ldx = _rows(x)
+    _, ldyb = _rows(yb)
+    D = x.shape[-1]
+    xo = torch.empty(M, D, dtype=torch.float32, device=x.device)
+    y = torch.empty(M, D, dtype=out_dtype, device=x.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    check(lib().vitmi_layernorm_fwd_res(M, D, _p(x), ldx, _p(yb), ldyb, _p(w), _p(b), float(eps), _p(xo), D,
+                                        _p(y), dt(out_dtype), D, _p(mean), _p(rstd), _s()), "layernorm_fwd_res")
+    return xo, y, mean, rstd
+
+
 def layernorm_fwd_t(x: Tensor, w: Tensor, b: Tensor, eps: float):
     """layernorm_fwd to bf16 that also returns the output transposed: (y [M, D], mean, rstd,
     yt [D, M]) -- yt is the token-contiguous operand of linear_wgrad_xt."""
