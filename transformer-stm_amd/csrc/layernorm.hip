@@ -16,6 +16,10 @@ namespace vitmi {
 #ifndef VITMI_NT_LN
 #define VITMI_NT_LN 1
 #endif
+// backward: the next row's loads issued before this row is reduced (A/B builds)
+#ifndef VITMI_LN_BWD_PIPE
+#define VITMI_LN_BWD_PIPE 0
+#endif
 template <typename V>
 __device__ __forceinline__ void put(V* p, V v) {
   if constexpr (VITMI_NT_LN) __builtin_nontemporal_store(v, p);
@@ -107,6 +111,42 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     db[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     ds[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+#if VITMI_LN_BWD_PIPE
+  // software-pipelined rows: the wave's next row (x, dy, the residual gradient, its statistics)
+  // is loaded before this row is reduced, so two rows' loads are in flight per wave
+  const int64_t rstep = (int64_t)gridDim.x * 4;
+  f32x4 cx[NV], cd[NV], cr[NV];
+  float cmu = 0.f, crs = 0.f;
+  auto load_row = [&](int64_t r, f32x4 (&lx)[NV], f32x4 (&ld)[NV], f32x4 (&lr)[NV], float& lmu, float& lrs) {
+    lmu = mean[r];
+    lrs = rstd[r];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 4;
+      const bool ok = c < D;
+      lr[i] = (dres && ok) ? *(const f32x4*)(dres + r * ldres + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      lx[i] = ok ? *(const f32x4*)(x + r * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      ld[i] = ok ? load4<TDY>(dy + r * lddy + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row < M) load_row(row, cx, cd, cr, cmu, crs);
+  for (; row < M; row += rstep) {
+    const int64_t nrow = row + rstep;
+    f32x4 nx[NV], nd[NV], nr[NV];
+    float nmu = 0.f, nrs = 0.f;
+    if (nrow < M) load_row(nrow, nx, nd, nr, nmu, nrs);
+    const float mu = cmu, rs = crs;
+    f32x4 xh[NV], gy[NV];
+    f32x4* rv = cr;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (lane + 64 * i) * 4;
+      if (c < D) {
+        const f32x4 xv = cx[i];
+        const f32x4 dyv = cd[i];
+#else
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < M; row += (int64_t)gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
     f32x4 xh[NV], gy[NV], rv[NV];
@@ -123,6 +163,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       if (c < D) {
         const f32x4 xv = *(const f32x4*)(x + row * ldx + c);
         const f32x4 dyv = load4<TDY>(dy + row * lddy + c);
+#endif
         xh[i] = (xv - mu) * rs;
         gy[i] = dyv * g[i];
         dg[i] += dyv * xh[i];
@@ -146,6 +187,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         if (LP) store4<bf16>(dx_lp + row * lddx_lp + c, o);
       }
     }
+#if VITMI_LN_BWD_PIPE
+    if (nrow < M) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        cx[i] = nx[i];
+        cd[i] = nd[i];
+        cr[i] = nr[i];
+      }
+      cmu = nmu;
+      crs = nrs;
+    }
+#endif
   }
   // block-reduce dgamma / dbeta / colsum(dx) partials over the 4 waves
 #pragma unroll
