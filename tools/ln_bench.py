@@ -41,3 +41,13 @@ tft = t(lambda: ops.layernorm_fwd_t(x, w, b, 1e-6))
 tbt = t(lambda: ops.layernorm_bwd_t(dy, x, mean, rstd, w, dw, db, dres=dres, dxsum=ds))
 print(f"ln fwd_t {tft:7.1f} us ({(fb + M * D * 2) / tft / 1e3:6.0f} GB/s)   "
       f"ln bwd_t {tbt:7.1f} us ({(bb + M * D * 2) / tbt / 1e3:6.0f} GB/s)", flush=True)
+
+# the fused Adam step over a ViT-B/16-sized arena (86.6 M fp32 parameters, bf16 shadow)
+n = 86_567_656
+p, gr = torch.randn(n, device="cuda", generator=g), torch.randn(n, device="cuda", generator=g)
+m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+sh = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+from vitmi._lib import lib  # noqa: E402
+ta = t(lambda: lib().vitmi_adam_step(n, ops._p(p), ops._p(gr), ops._p(m), ops._p(v), ops._p(sh), 1e-3, 0.9, 0.999,
+                                     1e-7, 1.0, ops._s()), 20)
+print(f"adam {ta:7.1f} us ({n * 30 / ta / 1e3:6.0f} GB/s)", flush=True)
