@@ -26,6 +26,11 @@
 namespace vitmi {
 
 static constexpr int DH = 64;
+// backward kernels: dP - delta formed by the MFMA chain (accumulator initialised to
+// -delta) instead of a subtraction per element (0: the subtraction; A/B builds)
+#ifndef VITMI_ATT_DPINIT
+#define VITMI_ATT_DPINIT 1
+#endif
 static constexpr float LOG2E = 1.4426950408889634f;
 static constexpr float LN2 = 0.6931471805599453f;
 
@@ -423,22 +428,29 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_bf16(
 #pragma unroll 1
       for (int u = 0; u < 2; ++u) {  // 32-query sub-tile
         if (t * 64 + 32 * u >= N) break;   // all 32 queries padding: P = 0, dS = 0 there
-        f32x16 sa = zero16(), dp = zero16();
+        f32x16 sa = zero16(), dp;
+        f32x4 L2[4];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {   // row constants first: dP - delta from the MFMA chain
+          const int q4 = 32 * u + 8 * g4 + 4 * h;           // rows acc_row(4*g4 + i, h) = q4 + i
+          L2[g4] = *(const f32x4*)(rl + q4);
+          const f32x4 dl = *(const f32x4*)(rl + 64 + q4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dp[4 * g4 + i] = VITMI_ATT_DPINIT ? -dl[i] : 0.f;
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           sa = mfma32(frag_row(qt, 32 * u, s, lane), kf[s], sa);   // S[q][key]
-          dp = mfma32(frag_row(dt_, 32 * u, s, lane), vf[s], dp);  // dP[q][key]
+          dp = mfma32(frag_row(dt_, 32 * u, s, lane), vf[s], dp);  // dP[q][key] - delta[q]
         }
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const int q4 = 32 * u + 8 * g4 + 4 * h;           // rows acc_row(4*g4 + i, h) = q4 + i
-          const f32x4 L2 = *(const f32x4*)(rl + q4);
-          const f32x4 dl = *(const f32x4*)(rl + 64 + q4);
+          [[maybe_unused]] const f32x4 dl = VITMI_ATT_DPINIT ? f32x4{} : *(const f32x4*)(rl + 64 + 32 * u + 8 * g4 + 4 * h);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = fexp2(sa[4 * g4 + i] * c2 - L2[i]);
+            const float p = fexp2(sa[4 * g4 + i] * c2 - L2[g4][i]);
             sa[4 * g4 + i] = p;
-            dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
+            dp[4 * g4 + i] = VITMI_ATT_DPINIT ? p * dp[4 * g4 + i] : p * (dp[4 * g4 + i] - dl[i]);
           }
         }
         // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
@@ -543,11 +555,15 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq_bf16(
 #pragma unroll
       for (int u = 0; u < 2; ++u) {  // 32-key sub-tile
         if (t * 64 + 32 * u >= N) break;   // all 32 keys padding: dS = 0 there
-        f32x16 st = zero16(), dp = zero16();
+        f32x16 st = zero16(), dp;
+        float ndl = VITMI_ATT_DPINIT ? -dl : 0.f;   // dP^T - delta from the MFMA chain
+        asm volatile("" : "+v"(ndl));                // (splat formed here, not hoisted)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[r] = ndl;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           st = mfma32(frag_row(kt, 32 * u, s, lane), qf[s], st);  // S^T[key][q]
-          dp = mfma32(frag_row(vt, 32 * u, s, lane), df[s], dp);  // dP^T[key][q]
+          dp = mfma32(frag_row(vt, 32 * u, s, lane), df[s], dp);  // dP^T[key][q] (- delta)
         }
         if (last) {
 #pragma unroll
@@ -557,7 +573,7 @@ __global__ __launch_bounds__(256, 4) void attn_bwd_dq_bf16(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = fexp2(fmaf(st[r], c2, -L2));   // q >= N: L2 = +inf -> p = 0
-          dp[r] = p * (dp[r] - dl);
+          dp[r] = VITMI_ATT_DPINIT ? p * dp[r] : p * (dp[r] - dl);
         }
         // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
 #pragma unroll
@@ -818,16 +834,24 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   const float c2 = scale * LOG2E;
   f32x16 dqt[2] = {zero16(), zero16()};
   auto kblock = [&](const int k0) {
-    f32x16 st = zero16(), dp = zero16();
+    f32x16 st = zero16(), dp;
+    // dP^T - delta straight from the MFMA chain: the accumulator starts at -delta (one row
+    // constant per lane), so dS = P (dP - delta) is one multiply per element
+    // (the opaque copy keeps the 16-register splat inside the block: hoisted out of the
+    // unrolled key loop it stays live across it and pushes the kernel past 128 VGPRs)
+    float ndl = VITMI_ATT_DPINIT ? -dl : 0.f;
+    asm volatile("" : "+v"(ndl));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] = ndl;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       st = mfma32(frag_row(kt, k0, s, lane), qf[s], st);   // S^T[key][q]
-      dp = mfma32(frag_row(vt, k0, s, lane), df[s], dp);   // dP^T[key][q]
+      dp = mfma32(frag_row(vt, k0, s, lane), df[s], dp);   // dP^T[key][q] (- delta)
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float p = fexp2(fmaf(st[r], c2, -L2));
-      dp[r] = p * (dp[r] - dl);
+      dp[r] = VITMI_ATT_DPINIT ? p * dp[r] : p * (dp[r] - dl);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -940,22 +964,31 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
     const char* dt_ = qt + NP * 128;
     f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
     auto qblock = [&](const int q0) {
-      f32x16 sa = zero16(), dp = zero16();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
-        dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key]
-      }
+      f32x16 sa = zero16(), dp;
+      // the row constants first: dP - delta straight from the MFMA chain (accumulator started
+      // at -delta of each query row), so dS = P (dP - delta) is one multiply per element
+      f32x4 L2[4];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int q4 = q0 + 8 * g4 + 4 * h;   // rows acc_row(4*g4 + i, h) = q4 + i
-        const f32x4 L2 = *(const f32x4*)(l2s + q4);
+        L2[g4] = *(const f32x4*)(l2s + q4);
         const f32x4 dl = *(const f32x4*)(dls + q4);
 #pragma unroll
+        for (int i = 0; i < 4; ++i) dp[4 * g4 + i] = VITMI_ATT_DPINIT ? -dl[i] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
+        dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key] - delta[q]
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        [[maybe_unused]] const f32x4 dl = VITMI_ATT_DPINIT ? f32x4{} : *(const f32x4*)(dls + q0 + 8 * g4 + 4 * h);
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = fexp2(fmaf(sa[4 * g4 + i], c2, -L2[i]));
+          const float p = fexp2(fmaf(sa[4 * g4 + i], c2, -L2[g4][i]));
           sa[4 * g4 + i] = p;
-          dp[4 * g4 + i] = p * (dp[4 * g4 + i] - dl[i]);
+          dp[4 * g4 + i] = VITMI_ATT_DPINIT ? p * dp[4 * g4 + i] : p * (dp[4 * g4 + i] - dl[i]);
         }
       }
 #pragma unroll
