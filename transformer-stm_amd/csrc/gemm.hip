@@ -882,7 +882,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand.
       // Returns the fragment of the second output (gelu') for BIAS_GELU.
       auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) -> bf16x4 {
-        [[maybe_unused]] bf16x4 u;
+        [[maybe_unused]] bf16x4 u{};   // (gelu' of the GELU epilogues; unused otherwise)
         f32x4 v = acc[mi][ni] + bv[ni];
         const int soff = mi * rstride;
         [[maybe_unused]] f32x4 df;   // dropout factors of the 4 columns
@@ -1297,11 +1297,17 @@ static int grid256(int nwg, int splits) {
 // Tail split: when the last round of a persistent launch would leave more than half of the
 // blocks idle (ViT N=768 GEMMs: 591 tiles on 256 CUs), its tiles are split into S K-ranges
 // (S <= 4, >= 2 K-steps each) so that round takes ~1/S of the time.
+#ifndef VITMI_TAIL_SMAX
+#define VITMI_TAIL_SMAX 4
+#endif
+#ifndef VITMI_TAIL_MINK
+#define VITMI_TAIL_MINK 16
+#endif
 static bool tail_plan(int nwg, int gx, int nk, int& S, int& ks, int& ntail) {
   ntail = nwg % gx;
   if (nwg < gx || ntail == 0 || 2 * ntail > gx || nk < 4) return false;
   S = gx / ntail;
-  if (S > 4) S = 4;
+  if (S > VITMI_TAIL_SMAX) S = VITMI_TAIL_SMAX;
   if (S < 2) return false;
   ks = (nk + S - 1) / S;
   if (ks < 2) ks = 2;
@@ -1357,7 +1363,7 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       g.ksplit = 0;
       // measured: pays off for long reductions (>= 16 K-steps) and for the DGELU epilogue
       // (whose partial units skip its aux loads); a wash or a loss for K = 768 otherwise
-      const bool tail_ok = g.k_per_split / 64 >= 16 || EPI == VITMI_EPI_DGELU;
+      const bool tail_ok = g.k_per_split / 64 >= VITMI_TAIL_MINK || EPI == VITMI_EPI_DGELU;
       if (splits == 1 && tail_ok && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM && g.tail_ws &&
           tail_plan(nwg, gx, (int)(g.k_per_split / 64), S, ks, ntail) &&
           g.tail_ws_bytes >= (size_t)ntail * S * 256 * 256 * sizeof(float)) {
