@@ -1030,6 +1030,215 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
   }
 }
 
+// Column sums of two consecutive 32-row tiles (rows row0.., row0+32..) that store_tile32 just wrote
+// into the images s0 and s1, folded over the workgroup's waves in wave order into colpart[0..63]
+// (tile32_colsum for a wave that owns 64 rows; fixed summation order).
+__device__ __forceinline__ void tile32x2_colsum(const char* s0, const char* s1, int row0, int nvalid, float* colpart,
+                                                float (*red)[64], int wave, int nw, int lane) {
+  const int rr = lane >> 3, cc = lane & 7;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const char* scr = t ? s1 : s0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (row0 + 32 * t + 8 * j + rr < nvalid) {
+        const bf16x8 b = *(const bf16x8*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += (float)b[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] += __shfl_xor(cs[e], 8, 64);
+    cs[e] += __shfl_xor(cs[e], 16, 64);
+    cs[e] += __shfl_xor(cs[e], 32, 64);
+  }
+  __syncthreads();                       // red is free (an earlier call's fold is done)
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wave][lane * 8 + e] = cs[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+    for (int w = 0; w < nw; ++w) t += red[w][threadIdx.x];
+    colpart[threadIdx.x] = t;
+  }
+}
+
+// dK/dV with TWO 32-key blocks per wave and one wave per SIMD (4 waves, up to 512 VGPRs): wave w
+// owns keys 64w..64w+63.  Each Q | dO fragment read from LDS feeds both blocks' MFMAs (half the
+// LDS reads per MFMA of attn_bwd_dkv_seq_bf16), and the two blocks' chains are independent, so
+// one block's MFMAs can run under the other's exp / dS VALU inside the wave instead of relying
+// on a co-resident wave.  Otherwise as attn_bwd_dkv_seq_bf16: persistent over the (batch, head)
+// pairs, the next pair's Q | dO by LDS-DMA under this pair's loop, K / V rows, lse and delta in
+// registers.  Key blocks past ceil(N/32) run on zero K / V rows and are never stored (rows >= N
+// fall outside the store descriptor).  N <= 256; NQC > 0: ceil(N/32) as a compile-time constant.
+template <int NPMAX, int NQC = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_dkv_seq2_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale,
+    float* __restrict__ colsum, int npairs) {
+  constexpr int NW = 4;
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * NPMAX * 128];   // [buffer][Q | dO]
+  __shared__ __attribute__((aligned(16))) float l2s[NPMAX];
+  __shared__ __attribute__((aligned(16))) float dls[NPMAX];
+  __shared__ float red[NW][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nq = NQC > 0 ? NQC : (N + 31) / 32, NP = nq * 32;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  const int key0 = wave * 64 + (lane & 31);   // block j: key0 + 32 j
+  const float c2 = scale * LOG2E;
+  auto stage_pair = [&](int bh, int buf) {
+    const int b = bh / H, hd = bh - b * H;
+    const bf16* base = qkv + (int64_t)b * N * ld;
+    stage_seq_dma(smem[buf], make_rsrc(base + hd * DH, bytes - hd * DH * 2), ldb, NP, NW, wave, lane);
+    stage_seq_dma(smem[buf] + NP * 128, make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2), ldo,
+                  NP, NW, wave, lane);
+  };
+  auto load_regs = [&](int bh, bf16x8 (&kf)[2][4], bf16x8 (&vf)[2][4], float& ls, float& dv) {
+    const int b = bh / H, hd = bh - b * H;
+    const bf16* base = qkv + (int64_t)b * N * ld;
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t kvoff = (uint32_t)((int64_t)(key0 + 32 * j) * ldb + 16 * h);   // 0 past N
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        kf[j][s] = __builtin_bit_cast(bf16x8, asm_load16(rk, kvoff, 32 * s));
+        vf[j][s] = __builtin_bit_cast(bf16x8, asm_load16(rv, kvoff, 32 * s));
+      }
+    }
+    const uint32_t ioff = (uint32_t)threadIdx.x * 4;
+    ls = asm_load4(make_rsrc(lse + (int64_t)bh * N, (uint32_t)N * 4), ioff);
+    dv = asm_load4(make_rsrc(delta + (int64_t)bh * N, (uint32_t)N * 4), ioff);
+  };
+
+  int bh = blockIdx.x;
+  if (bh >= npairs) return;
+  bf16x8 kf[2][4], vf[2][4];
+  float ls, dv;
+  stage_pair(bh, 0);
+  load_regs(bh, kf, vf, ls, dv);
+  int buf = 0;
+  bool first = true;
+  for (;;) {
+    // everything but the previous pair's dK/dV stores (16 per wave, + 2 column-sum stores on
+    // wave 0), which are younger; see attn_bwd_dkv_seq_bf16 for the inline-asm loads and the pin
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (colsum && wave == 0) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    first = false;
+    asm volatile("" : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[0][2]), "+v"(kf[0][3]), "+v"(vf[0][0]), "+v"(vf[0][1]),
+                 "+v"(vf[0][2]), "+v"(vf[0][3]), "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[1][2]), "+v"(kf[1][3]),
+                 "+v"(vf[1][0]), "+v"(vf[1][1]), "+v"(vf[1][2]), "+v"(vf[1][3]), "+v"(ls), "+v"(dv));
+    if (threadIdx.x < NP) {
+      const int i = threadIdx.x;
+      l2s[i] = i < N ? ls * LOG2E : INFINITY;
+      dls[i] = i < N ? dv : 0.f;
+    }
+    __syncthreads();   // Q | dO and l2s / dls visible; every wave is done with the other buffer
+    const int nbh = bh + gridDim.x;
+    const bool more = nbh < npairs;
+    if (more) stage_pair(nbh, buf ^ 1);
+    const char* qt = smem[buf];
+    const char* dt_ = qt + NP * 128;
+    f32x16 dvt[2][2] = {{zero16(), zero16()}, {zero16(), zero16()}};
+    f32x16 dkt[2][2] = {{zero16(), zero16()}, {zero16(), zero16()}};
+    auto qblock = [&](const int q0) {
+      f32x16 sa[2], dp[2];
+      f32x4 L2[4];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {   // row constants: dP - delta straight from the MFMA chain
+        const int q4 = q0 + 8 * g4 + 4 * h;   // rows acc_row(4*g4 + i, h) = q4 + i
+        L2[g4] = *(const f32x4*)(l2s + q4);
+        const f32x4 dl = *(const f32x4*)(dls + q4);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dp[j][4 * g4 + i] = -dl[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) sa[j] = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 qa = frag_row(qt, q0, s, lane), da = frag_row(dt_, q0, s, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          sa[j] = mfma32(qa, kf[j][s], sa[j]);    // S[q][key]
+          dp[j] = mfma32(da, vf[j][s], dp[j]);    // dP[q][key] - delta[q]
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = fexp2(fmaf(sa[j][4 * g4 + i], c2, -L2[g4][i]));
+            sa[j][4 * g4 + i] = p;
+            dp[j][4 * g4 + i] = p * dp[j][4 * g4 + i];
+          }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 td[2], tq[2];
+#pragma unroll
+        for (int d2 = 0; d2 < 2; ++d2) {
+          td[d2] = frag_tr(dt_, q0 + 16 * s, 32 * d2, lane);
+          tq[d2] = frag_tr(qt, q0 + 16 * s, 32 * d2, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 pb = pack8(sa[j], s), sb = pack8(dp[j], s);
+#pragma unroll
+          for (int d2 = 0; d2 < 2; ++d2) {
+            dvt[j][d2] = mfma32(td[d2], pb, dvt[j][d2]);
+            dkt[j][d2] = mfma32(tq[d2], sb, dkt[j][d2]);
+          }
+        }
+      }
+    };
+    if constexpr (NQC > 0) {
+#pragma unroll
+      for (int q0 = 0; q0 < NQC * 32; q0 += 32) qblock(q0);
+    } else {
+#pragma unroll 1
+      for (int q0 = 0; q0 < NP; q0 += 32) qblock(q0);
+    }
+    if (more) load_regs(nbh, kf, vf, ls, dv);   // (kf / vf are dead until the next pair)
+    // dK, dV through this pair's (now free) Q | dO image: every wave must be done reading it
+    __syncthreads();
+    {
+      const int b = bh / H, hd = bh - b * H;
+      const bf16* db = dqkv + (int64_t)b * N * ld;
+      const __amdgpu_buffer_rsrc_t rdk = make_rsrc(db + D + hd * DH, bytes - (D + hd * DH) * 2);
+      const __amdgpu_buffer_rsrc_t rdv = make_rsrc(db + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+      char* s0 = smem[buf] + (2 * wave) * ST_BYTES;
+      char* s1 = s0 + ST_BYTES;
+      float* part = colsum + (int64_t)b * 3 * D + hd * DH;   // the k- and v-bias gradient partials
+      const int ln = lane_here();
+      store_tile32(s0, dkt[0], scale, rdk, ldb, wave * 64, ln);
+      store_tile32(s1, dkt[1], scale, rdk, ldb, wave * 64 + 32, ln);
+      if (colsum) tile32x2_colsum(s0, s1, wave * 64, N, part + D, red, wave, NW, ln);
+      else asm volatile("" ::: "memory");
+      store_tile32(s0, dvt[0], 1.f, rdv, ldb, wave * 64, ln);
+      store_tile32(s1, dvt[1], 1.f, rdv, ldb, wave * 64 + 32, ln);
+      if (colsum) tile32x2_colsum(s0, s1, wave * 64, N, part + 2 * D, red, wave, NW, ln);
+    }
+    if (!more) break;
+    bh = nbh;
+    buf ^= 1;
+  }
+}
+
 // ---------------------------------------------- fused single-pass backward (N <= NPMAX)
 // One workgroup per (batch, head), NW = ceil(N/32) waves; wave w owns keys 32w..32w+31 exactly
 // as in attn_bwd_dkv_seq_bf16 (dK, dV accumulate in registers), and S, P, dP and dS of every
@@ -1715,7 +1924,8 @@ using namespace vitmi;
 
 // whole-sequence kernels for N <= SEQ_MAX (8 waves, 2 workgroups of <= 64 KiB LDS per CU).
 // Kernel policy (vitmi_attention_set_policy; tests / A-B timing): 0 = auto, 1 = always the
-// streamed kernels, 2 = auto with the single-pass fused backward for N <= SEQ_MAX.
+// streamed kernels, 2 = auto with the single-pass fused backward for N <= SEQ_MAX, 3 = auto with
+// the two-key-blocks-per-wave dK/dV kernel.
 static constexpr int SEQ_MAX = 256;
 
 static int device_cus() {   // compute units of the current device (the persistent dK/dV grid)
@@ -1733,9 +1943,15 @@ static int device_cus() {   // compute units of the current device (the persiste
 static int g_attn_policy = 0;
 static bool seq_path(int N) { return N <= SEQ_MAX && g_attn_policy != 1; }
 static bool fused_bwd() { return g_attn_policy == 2; }
+// 3 = auto with the two-key-blocks-per-wave dK/dV kernel (attn_bwd_dkv_seq2_bf16); a build with
+// VITMI_ATT_DKV2=1 makes it the auto choice (A/B timing)
+#ifndef VITMI_ATT_DKV2
+#define VITMI_ATT_DKV2 0
+#endif
+static bool dkv2() { return g_attn_policy == 3 || (VITMI_ATT_DKV2 && g_attn_policy == 0); }
 
 extern "C" int vitmi_attention_set_policy(int policy) {
-  VITMI_CHECK_ARG(policy >= 0 && policy <= 2, "attention_set_policy: policy must be 0..2");
+  VITMI_CHECK_ARG(policy >= 0 && policy <= 3, "attention_set_policy: policy must be 0..3");
   const int prev = g_attn_policy;
   g_attn_policy = policy;
   return prev;
@@ -1807,17 +2023,25 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     } else {
       const int npairs = B * H, cus = device_cus();
       const dim3 gkv(npairs < cus ? npairs : cus);
-      if ((N + 31) / 32 == 7) {   // N in (192, 224]: the ViT-B/ViT-S shape, N = 197
+      const bool n7 = (N + 31) / 32 == 7;   // N in (192, 224]: the ViT-B/ViT-S shape, N = 197
+      if (n7)
         hipLaunchKernelGGL((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), dim3(B * H), block, 0, s, (const bf16*)qkv,
                            (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
-        hipLaunchKernelGGL((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), gkv, block, 0, s, (const bf16*)qkv, (const bf16*)dout,
-                           lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
-      } else {
+      else
         hipLaunchKernelGGL((attn_bwd_dq_seq_bf16<SEQ_MAX>), dim3(B * H), block, 0, s, (const bf16*)qkv,
                            (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
+      if (dkv2() && n7)
+        hipLaunchKernelGGL((attn_bwd_dkv_seq2_bf16<SEQ_MAX, 7>), gkv, dim3(256), 0, s, (const bf16*)qkv,
+                           (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
+      else if (dkv2())
+        hipLaunchKernelGGL((attn_bwd_dkv_seq2_bf16<SEQ_MAX>), gkv, dim3(256), 0, s, (const bf16*)qkv,
+                           (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
+      else if (n7)
+        hipLaunchKernelGGL((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), gkv, block, 0, s, (const bf16*)qkv, (const bf16*)dout,
+                           lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
+      else
         hipLaunchKernelGGL((attn_bwd_dkv_seq_bf16<SEQ_MAX>), gkv, block, 0, s, (const bf16*)qkv, (const bf16*)dout,
                            lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
-      }
       if (colsum_rows) *colsum_rows = colsum ? B : 0;   // one partial row per batch
     }
   } else if (dtype == VITMI_BF16) {
@@ -1857,7 +2081,11 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
       } else {
         if ((N + 31) / 32 == 7) {
           VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
-          VITMI_STAT((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+          if (dkv2()) VITMI_STAT((attn_bwd_dkv_seq2_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+          else VITMI_STAT((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+        } else if (dkv2()) {
+          VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+          VITMI_STAT(attn_bwd_dkv_seq2_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
         } else {
           VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
           VITMI_STAT(attn_bwd_dkv_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);

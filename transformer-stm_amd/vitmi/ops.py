@@ -313,8 +313,9 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
 
 # ---------------------------------------------------------------- attention
 def attention_set_policy(policy: int) -> int:
-    """0 = auto, 1 = always the streamed kernels, 2 = single-pass fused backward for N <= 256
-    (tests / A-B timing).  Returns the previous policy."""
+    """0 = auto, 1 = always the streamed kernels, 2 = single-pass fused backward for N <= 256,
+    3 = auto with the two-key-blocks-per-wave dK/dV kernel (tests / A-B timing).  Returns the
+    previous policy."""
     return lib().vitmi_attention_set_policy(int(policy))
 
 
