@@ -147,6 +147,10 @@ __global__ void colsum_kernel(int64_t M, int64_t N, const T* __restrict__ dy, in
 }
 
 // db[n] += sum_z part[z][n]; 16 waves x 64 columns per block, fixed summation order
+// loads in flight per thread of the column-sum fold (A/B builds; the fold is latency-bound)
+#ifndef VITMI_CSF_UNROLL
+#define VITMI_CSF_UNROLL 4
+#endif
 __global__ __launch_bounds__(1024) void colsum_finish_kernel(int64_t N, int Z, const float* __restrict__ part,
                                                              float* __restrict__ db) {
   __shared__ float red[16][64];
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(1024) void colsum_finish_kernel(int64_t N, int Z, c
   const int64_t n = (int64_t)blockIdx.x * 64 + lane;
   float s = 0.f;
   if (n < N) {
-#pragma unroll 4
+#pragma unroll VITMI_CSF_UNROLL
     for (int z = w; z < Z; z += 16) s += part[(int64_t)z * N + n];
   }
   red[w][lane] = s;

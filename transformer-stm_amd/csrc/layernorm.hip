@@ -488,6 +488,10 @@ __global__ __launch_bounds__(512) void ln_bwd_t_kernel(
 
 // out[d] += sum_b part[b][d] for dgamma (rows 0..G-1), dbeta (G..2G-1), colsum(dx) (2G..3G-1),
 // in a fixed order (deterministic).
+// loads in flight per thread of the partial folds (A/B builds; the fold is latency-bound)
+#ifndef VITMI_LNR_UNROLL
+#define VITMI_LNR_UNROLL 2
+#endif
 __global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int G, int D,
                                                         float* __restrict__ dgamma,
                                                         float* __restrict__ dbeta,
@@ -500,7 +504,7 @@ __global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict_
   const int d = blockIdx.x * 16 + c;
   float a = 0.f, b = 0.f, e = 0.f;
   if (d < D) {
-#pragma unroll 2
+#pragma unroll VITMI_LNR_UNROLL
     for (int i = gi; i < G; i += 64) {
       a += part[(int64_t)i * D + d];
       b += part[(int64_t)(G + i) * D + d];
