@@ -149,7 +149,7 @@ __global__ void colsum_kernel(int64_t M, int64_t N, const T* __restrict__ dy, in
 // db[n] += sum_z part[z][n]; 16 waves x 64 columns per block, fixed summation order
 // loads in flight per thread of the column-sum fold (A/B builds; the fold is latency-bound)
 #ifndef VITMI_CSF_UNROLL
-#define VITMI_CSF_UNROLL 4
+#define VITMI_CSF_UNROLL 8
 #endif
 __global__ __launch_bounds__(1024) void colsum_finish_kernel(int64_t N, int Z, const float* __restrict__ part,
                                                              float* __restrict__ db) {

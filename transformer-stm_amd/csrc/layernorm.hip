@@ -490,7 +490,7 @@ __global__ __launch_bounds__(512) void ln_bwd_t_kernel(
 // in a fixed order (deterministic).
 // loads in flight per thread of the partial folds (A/B builds; the fold is latency-bound)
 #ifndef VITMI_LNR_UNROLL
-#define VITMI_LNR_UNROLL 2
+#define VITMI_LNR_UNROLL 8
 #endif
 __global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int G, int D,
                                                         float* __restrict__ dgamma,
