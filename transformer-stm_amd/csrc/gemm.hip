@@ -1203,9 +1203,46 @@ __global__ __launch_bounds__(256) void gemm_tail_fixup_kernel(GemmArgs g, int nt
     const int64_t row = (int64_t)tm * 256 + rl;
     const int64_t col = (int64_t)tn * 256 + cl;
     if (row >= g.M || col >= g.N) continue;
+    const float* pw = g.tail_ws + ((int64_t)t * g.nsplit * 256 + rl) * 256 + cl;   // split z at + z * 65536
     f32x4 a = {0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < g.nsplit; ++z)
-      a += *(const f32x4*)(g.tail_ws + ((int64_t)(t * g.nsplit + z) * 256 + rl) * 256 + cl);
+    if (g.nsplit <= 4) {
+      // every split's partial in flight at once (S <= 4 is the tail plan's cap), added in split order
+      f32x4 pz[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        if (z < g.nsplit) pz[z] = *(const f32x4*)(pw + (int64_t)z * 65536);
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        if (z < g.nsplit) a += pz[z];
+    } else {
+      for (int z = 0; z < g.nsplit; ++z) a += *(const f32x4*)(pw + (int64_t)z * 65536);
+    }
+    if constexpr ((EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_DGELU) && std::is_same<TC, bf16>::value &&
+                  std::is_same<T, bf16>::value) {
+      // the store-only and DGELU bf16 outputs leave as 8-B vectors (4 columns; N % 8 == 0 is a
+      // gemm256 precondition, and 4 aligned columns are contiguous in the tile-native gelu' too),
+      // element for element the arithmetic of epi_store
+      f32x4 v = a;
+      if constexpr (EPI == VITMI_EPI_STORE) {
+        if (g.bias) v += *(const f32x4*)(g.bias + col);
+      } else {
+        const bf16x4 gp = *(const bf16x4*)((const bf16*)g.aux + aux_at(g, row, col));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] *= (float)gp[j];
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+      *(bf16x4*)((bf16*)g.C + row * g.ldc + col) = o;
+      continue;
+    }
+    if constexpr (EPI == VITMI_EPI_RESIDUAL) {
+      // fp32 residual in and out as 16-B vectors ((residual + acc) + bias, as epi_store)
+      const f32x4 r = *(const f32x4*)(g.residual + row * g.ldr + col);
+      const f32x4 bv = g.bias ? *(const f32x4*)(g.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      *(f32x4*)((float*)g.C + row * g.ldc + col) = (r + a) + bv;
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (col + j >= g.N) break;
