@@ -344,6 +344,7 @@ def main():
         except (RuntimeError, TypeError):
             opt = torch.optim.Adam(model.parameters(), lr=1e-3, foreach=True)
     arena = model.arena()
+    params = list(arena.params)
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     img = torch.rand(B, cfg.in_chans, cfg.img_size, cfg.img_size, device=dev, generator=g)
@@ -356,7 +357,8 @@ def main():
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if timed else None
         if timed:
             ev[0].record()
-        arena.grad.zero_()
+        for p in params:                      # zero_grad(set_to_none=True): the forward zeroes the
+            p.grad = None                     # arena once and AccumulateGrad keeps its views as .grad
         red.start()
         with trace.range("vitmi:forward"):
             logits = model(img)
@@ -451,11 +453,19 @@ def main():
         "loss": round(float(loss.item()), 5),
         "build_id": _lib.lib().vitmi_build_id().decode(),
     }
+    if world > 1:
+        # the multi-rank run verifies itself: what the exchange ran on (ranks and library as the
+        # communicator reports them, the bucket plan, the tail launched after the backward), the
+        # compute-stream time the step waited for it, and whether every rank ends with the same
+        # parameters (MAX == MIN over ranks of the arena checksums)
+        out["rccl"] = dp.comm_report(red)
+        out["allreduce_exposed_ms"] = phases_ms.get("allreduce_wait")
+        out.update(dp.replica_report(arena.flat))
     red.close()                               # the comm watchdog thread (the step loop is over)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps, model, dev)
     if rank == 0 and world == 1 and not args.no_evidence and args.config == "c3" and not args.stats_out:
-        del model, opt, arena, red
+        del model, opt, arena, red, params
         torch.cuda.empty_cache()
         tmp = tempfile.mkdtemp(prefix="vitmi_bench_")
         tr, err = traffic_evidence(tmp, M)

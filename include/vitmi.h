@@ -129,16 +129,6 @@ int vitmi_linear_dgrad_bias(int dtype, int64_t M, int64_t N, int64_t K, const vo
                             vitmi_stream_t stream);
 
 size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
-/* The same dW[N,K] += dy^T x with one operand given token-contiguous (transposed copies that the
- * LayerNorm kernels below write beside their row-major outputs), so the GEMM reads only one
- * operand with transposing LDS reads (models/CvT(Par).py:132-134,254,256: the Dense kernels'
- * gradients).  _xt: x given as xt[K][ldxt] (ldxt >= M); _dyt: dy given as dyt[N][lddyt].
- * Workspaces: vitmi_linear_wgrad_xt_workspace_size / vitmi_linear_wgrad_workspace_size. */
-int vitmi_linear_wgrad_xt(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* xt,
-                          int64_t ldxt, float* dw, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
-size_t vitmi_linear_wgrad_xt_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
-int vitmi_linear_wgrad_dyt(int dtype, int64_t M, int64_t N, int64_t K, const void* dyt, int64_t lddyt,
-                           const void* x, float* dw, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 /* db[N] (f32) += sum_m dy[m, n]  (dy [M][ldy] of `dtype`) */
 int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, int64_t ldy, float* db,
                     void* workspace, size_t ws_bytes, vitmi_stream_t stream);
@@ -160,25 +150,6 @@ int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtype, int64_t 
                         int64_t lddx, void* dx_lp, int64_t lddx_lp, float* dgamma, float* dbeta,
                         float* dxsum, void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D);
-/* Residual add fused into the forward: xo = x + yb (fp32 residual stream + a bf16 branch output,
- * [M][ldyb]), then y = LN(xo) (models/CvT(Par).py:261-289: the out-projection's residual add
- * followed by the second LayerNorm).  xo fp32 [M][ldxo]. */
-int vitmi_layernorm_fwd_res(int64_t M, int D, const float* x, int64_t ldx, const void* yb, int64_t ldyb,
-                            const float* gamma, const float* beta, float eps, float* xo, int64_t ldxo, void* y,
-                            int y_dtype, int64_t ldy, float* mean, float* rstd, vitmi_stream_t stream);
-/* The same with the bf16 output also written transposed (yt / dxt [D][ldt], ldt >= M and a
- * multiple of 8): the token-contiguous operand of the weight-gradient GEMMs
- * (vitmi_linear_wgrad_xt / _dyt).  bf16 only; D <= 1024.  _bwd_t needs dx_lp. */
-int vitmi_layernorm_fwd_t(int64_t M, int D, const float* x, int64_t ldx, const float* gamma,
-                          const float* beta, float eps, void* y, int64_t ldy, void* yt, int64_t ldt,
-                          float* mean, float* rstd, vitmi_stream_t stream);
-int vitmi_layernorm_bwd_t(int64_t M, int D, const void* dy, int dy_dtype, int64_t lddy,
-                          const float* x, int64_t ldx, const float* mean, const float* rstd,
-                          const float* gamma, const float* dres, int64_t ldres, float* dx,
-                          int64_t lddx, void* dx_lp, int64_t lddx_lp, void* dxt, int64_t ldt,
-                          float* dgamma, float* dbeta, float* dxsum, void* workspace, size_t ws_bytes,
-                          vitmi_stream_t stream);
-
 /* ---------------------------------------------------------------------------
  * Multi-head scaled-dot-product attention (layers.MultiHeadAttention called (q, v, k),
  * models/CvT(Par).py:137,185; einsum-softmax-einsum old_codes/MS_CvT.py:202-207).
@@ -192,9 +163,8 @@ int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, con
                         const void* o, const void* dout, const float* lse, void* dqkv,
                         void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_attention_bwd_workspace_size(int B, int N, int H);
-/* Kernel selection (process-wide; tests / A-B timing): 0 = auto, 1 = always the streamed
- * (64-key LDS-tiled) kernels, 2 = auto with the single-pass fused backward for N <= 256,
- * 3 = auto with the two-key-blocks-per-wave dK/dV kernel.  Returns the previous policy. */
+/* Kernel selection (process-wide; tests): 0 = auto, 1 = always the streamed (64-key LDS-tiled)
+ * kernels.  Returns the previous policy. */
 int vitmi_attention_set_policy(int policy);
 /* vitmi_attention_bwd plus the qkv bias gradient: dbias[3*H*dh] += column sums of dqkv (the
  * q/k/v Dense biases, models/CvT(Par).py:132-134).  On the bf16 paths the sums come from the
@@ -264,7 +234,7 @@ int vitmi_head_fwd(int B, int D, int C, const float* y, int64_t ldy, const float
                    const float* b, float* logits, vitmi_stream_t stream);
 int vitmi_head_bwd(int B, int D, int C, const float* dlogits, const float* y, int64_t ldy,
                    const float* w, float* dy, float* dw, float* db, vitmi_stream_t stream);
-/* loss = mean over batch; dlogits = d loss / d logits.  target: int64 [B] (CE) or f32 [B] (MSE).
+/* loss = mean over batch; dlogits = d loss / d logits.  target: int64 [B] (CE) or f32 [B][C] (MSE).
  * Either output may be NULL (not both). */
 int vitmi_loss_fwd_bwd(int kind, int B, int C, const float* logits, const void* target,
                        float* loss, float* dlogits, vitmi_stream_t stream);

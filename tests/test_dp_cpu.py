@@ -50,10 +50,15 @@ def _worker(rank, world, port, q):
         arena = m.arena()
         arena.grad.copy_(torch.full_like(arena.grad, float(rank + 1)))
         r2.start()
-        m._head_ready_hook()
-        for blk in reversed(m.blocks):
-            blk._grad_ready_hook(blk)
-        m.patch_embed._grad_ready_hook(m.patch_embed)
+        # AccumulateGrad's post hooks, in backward (= arena) order; one parameter's gradient
+        # arrives in a tensor of its own and must be copied into its arena view
+        stray = arena.params[3]
+        for p in arena.params:
+            if p is stray:
+                p.grad = torch.full_like(p, float(rank + 1))
+            for h in list(p._post_accumulate_grad_hooks.values()):
+                h(p)
+        out["stray_bound"] = stray.grad.data_ptr() == arena.view(arena.grad, stray).data_ptr()
         r2.finish()
         out["arena_mean"] = arena.grad.clone().numpy()
         out["arena_order"] = [b for _, b in r2.launch_log]
@@ -105,6 +110,7 @@ def test_grad_reducer_gloo_world2():
         assert o["launched"] == list(range(o["nbuckets"]))
         assert torch.allclose(o["arena_mean"], torch.full_like(o["arena_mean"], 1.5))
         assert o["arena_order"] == sorted(o["arena_order"])    # front-to-back readiness
+        assert res[r]["stray_bound"]
         assert (res[r]["param0"] == res[0]["param0"]).all()     # broadcast from rank 0
         assert (res[r]["lin_w"] == res[0]["lin_w"]).all() and (res[r]["bn_mean"] == 1.0).all()
         assert res[r]["lin_buckets"] > 1
@@ -174,3 +180,137 @@ def test_comm_binds_the_rccl_torch_loaded():
     assert mapped, "torch did not map an RCCL"
     bound = VitmiComm.library()
     assert os.path.realpath(bound) in {os.path.realpath(m) for m in mapped}, (bound, mapped)
+
+
+# ------------------------------------------------------------------ the N>1 bench line's fields
+class _FakeComm(dp.VitmiComm):
+    """The vitmi communicator's interface with the exchange done by gloo on the host: the RCCL
+    id still travels through the job's TCPStore (VitmiComm.from_store), only ncclCommInitRank
+    and ncclAllReduce are replaced."""
+
+    def _init(self, rank, world):
+        self.calls = 0
+
+    def allreduce_async(self, buf, side, ready=None, op=dp.REDUCE_AVG):
+        self.calls += 1
+        dist.all_reduce(buf)
+        if op == dp.REDUCE_AVG:
+            buf.div_(self.world)
+
+    def info(self):
+        return self.rank, self.world
+
+    def check(self):
+        pass
+
+    @staticmethod
+    def library():
+        return "fake-rccl"
+
+
+def _report_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vitmi.modules import VisionTransformer
+        out = {}
+        comm = _FakeComm.from_store(rank, world)
+        out["uid"] = comm._uid.raw
+        torch.manual_seed(0)
+        m = VisionTransformer(ViTConfig(img_size=32, patch_size=8, embed_dim=128, depth=4, num_heads=2,
+                                        dtype="fp32"))
+        red = dp.attach(m, bucket_mb=0.3, comm=comm, timeout_s=0)
+        arena = m.arena()
+        for step in range(2):
+            arena.grad.fill_(float(rank + 1))
+            red.start()
+            for p in arena.params:              # AccumulateGrad's post hooks, backward order
+                for h in list(p._post_accumulate_grad_hooks.values()):
+                    h(p)
+            in_backward = comm.calls
+            red.finish()
+        out["mean_ok"] = bool(torch.allclose(arena.grad, torch.full_like(arena.grad, 1.5)))
+        out["in_backward"] = in_backward
+        out["report"] = dp.comm_report(red)
+        out["same"] = dp.replica_report(arena.flat)
+        if rank == 1:
+            with torch.no_grad():
+                arena.flat[7] += 1e-3
+        out["diff"] = dp.replica_report(arena.flat)
+        cuts = red.bounds
+        out["ends"] = [e for _, e in cuts]
+        out["block_ends"] = sorted(max(arena.offsets[id(p)] + p.numel() for p in blk.parameters()) for blk in m.blocks)
+        out["numel"] = arena.numel
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_multirank_report_fields_gloo_world2():
+    """What bench.py adds to its line at N > 1 (dp.comm_report / dp.replica_report), driven
+    through GradReducer, the parameters' post-accumulate hooks and VitmiComm.from_store's id
+    exchange with a fake communicator: ranks and library as the communicator reports them, the
+    block-aligned bucket plan with the tail that finish() launches, and a replica check that
+    passes on identical parameters and fails when one rank's parameters differ."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[0]["uid"] == res[1]["uid"]
+    for r in range(world):
+        o = res[r]
+        rep = o["report"]
+        assert o["mean_ok"]
+        assert rep["ranks"] == 2 and rep["rank"] == r and rep["library"] == "fake-rccl"
+        assert rep["bucket_count"] == len(rep["buckets_mib"]) > 2
+        assert rep["tail_buckets"] == [rep["bucket_count"] - 1]      # only the embedding's bucket
+        assert rep["tail_bucket_mib"] == rep["buckets_mib"][-1]
+        assert o["in_backward"] >= rep["bucket_count"] - 1           # the rest launched from hooks
+        assert set(o["block_ends"]) <= set(o["ends"]) and o["ends"][-1] == o["numel"]
+        assert o["same"]["replicas_identical"] is True
+        assert o["diff"]["replicas_identical"] is False
+    assert res[0]["same"]["param_checksum_bits"] == res[1]["same"]["param_checksum_bits"]
+
+
+def test_watchdog_abort_serialises_with_an_allreduce_enqueue():
+    """the watchdog thread's abort must not free the communicator while the
+    training thread is inside an all-reduce enqueue.  Every library comm call of VitmiComm
+    holds its lock (and comm.cpp holds a mutex): an abort fired mid-enqueue runs after it, and
+    the abort path leaves the CU reservation (a training-thread global) alone."""
+    import threading
+    import time
+
+    ev = []
+
+    class SlowComm(dp.VitmiComm):
+        def _init(self, rank, world):
+            pass
+
+        def _call(self, name, *args):
+            with self._lock:
+                ev.append(("enter", name, time.monotonic()))
+                time.sleep(0.3)
+                ev.append(("exit", name, time.monotonic()))
+                return 0
+
+    comm = SlowComm(0, 1, bytes(dp.UID_BYTES))
+    red = dp.GradReducer(torch.zeros(256), bucket_mb=0.001, comm=comm, timeout_s=0)
+    red._prev_reserve = 7                       # a reservation in force (training thread)
+    t = threading.Thread(target=lambda: comm._call("vitmi_comm_allreduce_async"))
+    t.start()
+    time.sleep(0.05)
+    t0 = time.monotonic()
+    red._abort_comm()                           # what CommWatchdog calls on a timeout
+    t1 = time.monotonic()
+    t.join()
+    exit_t = [e[2] for e in ev if e[0] == "exit"][0]
+    assert t1 >= exit_t > t0                   # the abort waited for the enqueue to leave
+    assert not comm.live
+    assert red._prev_reserve == 7              # untouched by the watchdog path

@@ -47,34 +47,6 @@ def compare(cfg, params, img, tgt, logit_tol, grad_tol, loss_tol=1e-5):
     return err, worst
 
 
-def test_wgrad_transposed_operands_path_matches_oracle(monkeypatch):
-    """The opt-in bf16 weight-gradient path from token-contiguous operand copies
-    (VITMI_WGRAD_T: layernorm_fwd_t / _bwd_t -> linear_wgrad_xt / _dyt; needs B*N % 64 == 0:
-    64 images of 17 tokens) against the oracle, and against the default token-major path."""
-    from vitmi import modules
-    cfg = config_c1(dtype="bf16")
-    params = vit_ref.init_params(cfg, seed=0)
-    img, tgt = vit_ref.synthetic_batch(cfg, 64)
-    monkeypatch.setattr(modules, "WGRAD_T", True)
-    compare(cfg, params, img, tgt, logit_tol=BF16_C1_LOGITS, grad_tol=BF16_GRADS, loss_tol=2e-2)
-    _, _, g_t = gpu_step(cfg, params, img, tgt)
-    monkeypatch.setattr(modules, "WGRAD_T", False)
-    _, _, g_tn = gpu_step(cfg, params, img, tgt)
-    worst = max(vit_ref.rel_err(g_t[k], g_tn[k]) for k in g_tn)
-    assert worst < 1e-3, worst
-
-
-def test_residual_in_layernorm_path_matches_oracle(monkeypatch):
-    """The opt-in bf16 path with the out-projection's residual add in LN2 (VITMI_RES_IN_LN:
-    linear_fwd bf16 store + layernorm_fwd_res) against the oracle, at the C1 bounds."""
-    from vitmi import modules
-    monkeypatch.setattr(modules, "RES_IN_LN", True)
-    cfg = config_c1(dtype="bf16")
-    params = vit_ref.init_params(cfg, seed=0)
-    img, tgt = vit_ref.synthetic_batch(cfg, 8)
-    compare(cfg, params, img, tgt, logit_tol=BF16_C1_LOGITS, grad_tol=BF16_GRADS, loss_tol=2e-2)
-
-
 def test_c1_fp32_matches_oracle():
     cfg = config_c1()                           # ViT-Ti/16 64x64 bs8 (BASELINE config 1)
     params = vit_ref.init_params(cfg, seed=0)

@@ -266,67 +266,6 @@ def test_layernorm_fwd_bwd(D, T):
     assert rel(dsum, 2.0 + (xx.grad + dres).sum(0)) < 1e-5   # fused bias-grad column sums
 
 
-@pytest.mark.parametrize("D", [64, 384, 768, 1024])
-@pytest.mark.parametrize("T", [BF, torch.float32])
-def test_layernorm_fwd_residual(D, T):
-    """layernorm_fwd_res: xo = x + y (bf16 branch output) bit for bit, and LN(xo) == the plain
-    LayerNorm kernel on xo bit for bit."""
-    M = 197 * 2 + 3
-    x = (rnd(M, D, seed=81) * 2 + 0.5).to(DEV)
-    yb = rnd(M, D, seed=82).to(BF).to(DEV)
-    w, b = (1 + 0.1 * rnd(D, seed=83)).to(DEV), (0.1 * rnd(D, seed=84)).to(DEV)
-    xo, h, mean, rstd = ops.layernorm_fwd_res(x, yb, w, b, 1e-6, T)
-    assert torch.equal(xo, x + yb.float())
-    h2, mean2, rstd2 = ops.layernorm_fwd(xo, w, b, 1e-6, T)
-    assert torch.equal(h, h2) and torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
-
-
-@pytest.mark.parametrize("M,D", [(197 * 3, 768), (64, 384), (33, 64), (256 * 197, 768)])
-def test_layernorm_transposed_outputs(M, D):
-    """layernorm_fwd_t / layernorm_bwd_t (32-row tiles through LDS) == the row-kernels' bf16
-    outputs bit for bit, with the transposed copies equal to their transposes (M not a multiple
-    of 32 included); the parameter-gradient partials sum in another order (1e-5)."""
-    x = (rnd(M, D, seed=71) * 2 + 0.5).to(DEV)
-    w, b = (1 + 0.1 * rnd(D, seed=72)).to(DEV), (0.1 * rnd(D, seed=73)).to(DEV)
-    y, mean, rstd = ops.layernorm_fwd(x, w, b, 1e-6, BF)
-    y2, mean2, rstd2, yt = ops.layernorm_fwd_t(x, w, b, 1e-6)
-    assert torch.equal(y, y2) and torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
-    assert torch.equal(yt, y.t())
-    dy = rnd(M, D, seed=74).to(BF).to(DEV)
-    dres = rnd(M, D, seed=75).to(DEV)
-    grads = []
-    for _ in range(2):
-        dg, dbb, dsum = (torch.full((D,), v, device=DEV) for v in (0.5, -0.5, 2.0))
-        grads.append((dg, dbb, dsum))
-    dx, dx_lp = ops.layernorm_bwd(dy, x, mean, rstd, w, *grads[0][:2], dres=dres, lp_dtype=BF, dxsum=grads[0][2])
-    dx2, dx_lp2, dxt = ops.layernorm_bwd_t(dy, x, mean, rstd, w, *grads[1][:2], dres=dres, dxsum=grads[1][2])
-    assert torch.equal(dx, dx2) and torch.equal(dx_lp, dx_lp2) and torch.equal(dxt, dx_lp.t())
-    for a, c in zip(grads[0], grads[1]):
-        assert rel(c, a) < 1e-5
-
-
-@pytest.mark.parametrize("M,N,K", [(64 * 9, 384, 192), (1024, 256, 320), (256 * 197, 2304, 768),
-                                   (256 * 197, 768, 3072)])
-def test_linear_wgrad_transposed_operands(M, N, K):
-    """dW += dy^T x with x given transposed (linear_wgrad_xt: the product dW^T through a
-    transposing split-K fold) or dy given transposed (linear_wgrad_dyt) == the token-major
-    linear_wgrad up to fp32 summation order.  (The transposed operand is read k-major: the token
-    count must be a multiple of 64, which the module path checks before taking it.)"""
-    g = torch.Generator(device=DEV).manual_seed(7)
-    dy = (torch.rand(M, N, device=DEV, generator=g) * 2 - 1).to(BF)
-    x = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(BF)
-    base = torch.rand(N, K, device=DEV, generator=g)
-    ref = base.clone()
-    ops.linear_wgrad(dy, x, ref)
-    a = base.clone()
-    ops.linear_wgrad_xt(dy, x.t().contiguous(), a)
-    c = base.clone()
-    ops.linear_wgrad_dyt(dy.t().contiguous(), x, c)
-    assert rel(a, ref) < 1e-6 and rel(c, ref) < 1e-6
-    exact = base.double() + dy.double().t() @ x.double()
-    assert rel(a, exact) < 1e-5
-
-
 def test_layernorm_strided_rows():
     B, N, D = 5, 17, 192
     x = rnd(B, N, D, seed=20)
@@ -426,71 +365,6 @@ def test_attention_persistent_many_pairs(B, N, H):
     d = dqkv.float().cpu().view(B * N, 3, D)
     for i, name in enumerate("qkv"):
         assert rel(d[:, i], g[:, i]) < 2e-2, name
-
-
-@pytest.mark.parametrize("B,N,H", [(2, 197, 2), (1, 17, 3), (3, 1, 2), (1, 130, 1), (1, 256, 1),
-                                   (2, 255, 1), (1, 33, 2), (1, 96, 1), (4, 197, 12)])
-def test_attention_bwd_single_pass(B, N, H):
-    """The single-pass backward (attention policy 2: S/P/dS formed once, dQ summed over the
-    key waves in a fixed order through LDS) vs the fp32 reference, vs the dQ + dK/dV kernel
-    pair, and bitwise equal across runs (deterministic: no atomics)."""
-    D = 64 * H
-    scale = 64 ** -0.5
-    qkv = rnd(B * N, 3 * D, dtype=BF, seed=31)
-    do = rnd(B * N, D, dtype=BF, seed=32)
-    o, lse = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
-    prev = ops.attention_set_policy(0)
-    pair = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-    ops.attention_set_policy(2)
-    try:
-        one = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-        again = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-    finally:
-        ops.attention_set_policy(prev)
-    assert torch.equal(one, again)
-    qq = qkv.float().clone().requires_grad_()
-    o2, _ = attn_ref(qq, B, N, H, scale)
-    o2.backward(do.float())
-    g = qq.grad.view(B * N, 3, D)
-    d1 = one.float().cpu().view(B * N, 3, D)
-    d2 = pair.float().cpu().view(B * N, 3, D)
-    for i, name in enumerate("qkv"):
-        assert rel(d1[:, i], g[:, i]) < 2e-2, name
-        assert rel(d1[:, i], d2[:, i]) < 1e-2, name
-
-
-@pytest.mark.parametrize("B,N,H", [(2, 197, 2), (48, 197, 12), (3, 197, 1), (1, 17, 3), (3, 1, 2),
-                                   (1, 130, 1), (1, 256, 1), (2, 255, 1), (40, 193, 9), (24, 224, 12)])
-def test_attention_dkv_two_blocks_per_wave(B, N, H):
-    """The dK/dV kernel with two 32-key blocks per wave and one wave per SIMD (attention policy
-    3) vs the fp32 reference and the 7-wave kernel, bitwise equal across runs, with the fused
-    k/v bias-gradient column sums equal to a column-sum pass over its own output."""
-    D = 64 * H
-    scale = 64 ** -0.5
-    qkv = rnd(B * N, 3 * D, dtype=BF, seed=51)
-    do = rnd(B * N, D, dtype=BF, seed=52)
-    o, lse = ops.attention_fwd(qkv.to(DEV), B, N, H, scale)
-    prev = ops.attention_set_policy(0)
-    pair = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-    ops.attention_set_policy(3)
-    try:
-        two = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-        again = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale)
-        db = torch.full((3 * D,), 0.25, device=DEV)
-        fused = ops.attention_bwd(qkv.to(DEV), o, do.to(DEV), lse, B, N, H, scale, bias_grad=db, fused_bias=True)
-    finally:
-        ops.attention_set_policy(prev)
-    assert torch.equal(two, again) and torch.equal(fused, two)
-    assert rel(db - 0.25, two.float().sum(0)) < 1e-5
-    qq = qkv.float().clone().requires_grad_()
-    o2, _ = attn_ref(qq, B, N, H, scale)
-    o2.backward(do.float())
-    g = qq.grad.view(B * N, 3, D)
-    d1 = two.float().cpu().view(B * N, 3, D)
-    d2 = pair.float().cpu().view(B * N, 3, D)
-    for i, name in enumerate("qkv"):
-        assert rel(d1[:, i], g[:, i]) < 2e-2, name
-        assert rel(d1[:, i], d2[:, i]) < 1e-2, name
 
 
 @pytest.mark.parametrize("B,N,H,T", [(2, 197, 2, BF), (3, 17, 1, BF), (1, 256, 3, BF), (2, 1, 2, BF),

@@ -55,17 +55,3 @@ def test_fp32_is_passthrough(monkeypatch):
     casts = _patch(monkeypatch)
     g = torch.randn(3, 3)
     assert modules._take_lp(g, torch.float32) is g and not casts
-
-
-def test_transposed_copy_travels_with_the_copy(monkeypatch):
-    casts = _patch(monkeypatch)
-    g = torch.randn(6, 4)
-    lp, lpt = g.to(BF), g.to(BF).t().contiguous()
-    modules._handover(g, lp, lpt)
-    got, got_t = modules._take_lp2(g, BF)
-    assert got.data_ptr() == lp.data_ptr() and got_t is lpt and not casts
-    # a stale hand-over yields neither
-    modules._handover(g, lp, lpt)
-    g.mul_(2.0)
-    got, got_t = modules._take_lp2(g, BF)
-    assert got_t is None and torch.equal(got, g.to(BF)) and len(casts) == 1

@@ -37,10 +37,6 @@ tf = t(lambda: ops.layernorm_fwd(x, w, b, 1e-6, torch.bfloat16))
 tb = t(lambda: ops.layernorm_bwd(dy, x, mean, rstd, w, dw, db, dres=dres, lp_dtype=torch.bfloat16, dxsum=ds))
 fb, bb = M * D * (4 + 2) + M * 8, M * D * (2 + 4 + 4 + 4 + 2)
 print(f"ln fwd {tf:7.1f} us ({fb / tf / 1e3:6.0f} GB/s)   ln bwd {tb:7.1f} us ({bb / tb / 1e3:6.0f} GB/s)", flush=True)
-tft = t(lambda: ops.layernorm_fwd_t(x, w, b, 1e-6))
-tbt = t(lambda: ops.layernorm_bwd_t(dy, x, mean, rstd, w, dw, db, dres=dres, dxsum=ds))
-print(f"ln fwd_t {tft:7.1f} us ({(fb + M * D * 2) / tft / 1e3:6.0f} GB/s)   "
-      f"ln bwd_t {tbt:7.1f} us ({(bb + M * D * 2) / tbt / 1e3:6.0f} GB/s)", flush=True)
 
 # the fused Adam step over a ViT-B/16-sized arena (86.6 M fp32 parameters, bf16 shadow)
 n = 86_567_656

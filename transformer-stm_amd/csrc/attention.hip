@@ -1030,424 +1030,6 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
   }
 }
 
-// Column sums of two consecutive 32-row tiles (rows row0.., row0+32..) that store_tile32 just wrote
-// into the images s0 and s1, folded over the workgroup's waves in wave order into colpart[0..63]
-// (tile32_colsum for a wave that owns 64 rows; fixed summation order).
-__device__ __forceinline__ void tile32x2_colsum(const char* s0, const char* s1, int row0, int nvalid, float* colpart,
-                                                float (*red)[64], int wave, int nw, int lane) {
-  const int rr = lane >> 3, cc = lane & 7;
-  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const char* scr = t ? s1 : s0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (row0 + 32 * t + 8 * j + rr < nvalid) {
-        const bf16x8 b = *(const bf16x8*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) cs[e] += (float)b[e];
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    cs[e] += __shfl_xor(cs[e], 8, 64);
-    cs[e] += __shfl_xor(cs[e], 16, 64);
-    cs[e] += __shfl_xor(cs[e], 32, 64);
-  }
-  __syncthreads();                       // red is free (an earlier call's fold is done)
-  if (lane < 8) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[wave][lane * 8 + e] = cs[e];
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    float t = 0.f;
-    for (int w = 0; w < nw; ++w) t += red[w][threadIdx.x];
-    colpart[threadIdx.x] = t;
-  }
-}
-
-// dK/dV with TWO 32-key blocks per wave and one wave per SIMD (4 waves, up to 512 VGPRs): wave w
-// owns keys 64w..64w+63.  Each Q | dO fragment read from LDS feeds both blocks' MFMAs (half the
-// LDS reads per MFMA of attn_bwd_dkv_seq_bf16), and the two blocks' chains are independent, so
-// one block's MFMAs can run under the other's exp / dS VALU inside the wave instead of relying
-// on a co-resident wave.  Otherwise as attn_bwd_dkv_seq_bf16: persistent over the (batch, head)
-// pairs, the next pair's Q | dO by LDS-DMA under this pair's loop, K / V rows, lse and delta in
-// registers.  Key blocks past ceil(N/32) run on zero K / V rows and are never stored (rows >= N
-// fall outside the store descriptor).  N <= 256; NQC > 0: ceil(N/32) as a compile-time constant.
-template <int NPMAX, int NQC = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_dkv_seq2_bf16(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H, float scale,
-    float* __restrict__ colsum, int npairs) {
-  constexpr int NW = 4;
-  __shared__ __attribute__((aligned(16))) char smem[2][2 * NPMAX * 128];   // [buffer][Q | dO]
-  __shared__ __attribute__((aligned(16))) float l2s[NPMAX];
-  __shared__ __attribute__((aligned(16))) float dls[NPMAX];
-  __shared__ float red[NW][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nq = NQC > 0 ? NQC : (N + 31) / 32, NP = nq * 32;
-  const int D = H * DH;
-  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
-  const int h = lane >> 5;
-  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
-  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
-  const int key0 = wave * 64 + (lane & 31);   // block j: key0 + 32 j
-  const float c2 = scale * LOG2E;
-  auto stage_pair = [&](int bh, int buf) {
-    const int b = bh / H, hd = bh - b * H;
-    const bf16* base = qkv + (int64_t)b * N * ld;
-    stage_seq_dma(smem[buf], make_rsrc(base + hd * DH, bytes - hd * DH * 2), ldb, NP, NW, wave, lane);
-    stage_seq_dma(smem[buf] + NP * 128, make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2), ldo,
-                  NP, NW, wave, lane);
-  };
-  auto load_regs = [&](int bh, bf16x8 (&kf)[2][4], bf16x8 (&vf)[2][4], float& ls, float& dv) {
-    const int b = bh / H, hd = bh - b * H;
-    const bf16* base = qkv + (int64_t)b * N * ld;
-    const __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
-    const __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const uint32_t kvoff = (uint32_t)((int64_t)(key0 + 32 * j) * ldb + 16 * h);   // 0 past N
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        kf[j][s] = __builtin_bit_cast(bf16x8, asm_load16(rk, kvoff, 32 * s));
-        vf[j][s] = __builtin_bit_cast(bf16x8, asm_load16(rv, kvoff, 32 * s));
-      }
-    }
-    const uint32_t ioff = (uint32_t)threadIdx.x * 4;
-    ls = asm_load4(make_rsrc(lse + (int64_t)bh * N, (uint32_t)N * 4), ioff);
-    dv = asm_load4(make_rsrc(delta + (int64_t)bh * N, (uint32_t)N * 4), ioff);
-  };
-
-  int bh = blockIdx.x;
-  if (bh >= npairs) return;
-  bf16x8 kf[2][4], vf[2][4];
-  float ls, dv;
-  stage_pair(bh, 0);
-  load_regs(bh, kf, vf, ls, dv);
-  int buf = 0;
-  bool first = true;
-  for (;;) {
-    // everything but the previous pair's dK/dV stores (16 per wave, + 2 column-sum stores on
-    // wave 0), which are younger; see attn_bwd_dkv_seq_bf16 for the inline-asm loads and the pin
-    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (colsum && wave == 0) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    first = false;
-    asm volatile("" : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[0][2]), "+v"(kf[0][3]), "+v"(vf[0][0]), "+v"(vf[0][1]),
-                 "+v"(vf[0][2]), "+v"(vf[0][3]), "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[1][2]), "+v"(kf[1][3]),
-                 "+v"(vf[1][0]), "+v"(vf[1][1]), "+v"(vf[1][2]), "+v"(vf[1][3]), "+v"(ls), "+v"(dv));
-    if (threadIdx.x < NP) {
-      const int i = threadIdx.x;
-      l2s[i] = i < N ? ls * LOG2E : INFINITY;
-      dls[i] = i < N ? dv : 0.f;
-    }
-    __syncthreads();   // Q | dO and l2s / dls visible; every wave is done with the other buffer
-    const int nbh = bh + gridDim.x;
-    const bool more = nbh < npairs;
-    if (more) stage_pair(nbh, buf ^ 1);
-    const char* qt = smem[buf];
-    const char* dt_ = qt + NP * 128;
-    f32x16 dvt[2][2] = {{zero16(), zero16()}, {zero16(), zero16()}};
-    f32x16 dkt[2][2] = {{zero16(), zero16()}, {zero16(), zero16()}};
-    auto qblock = [&](const int q0) {
-      f32x16 sa[2], dp[2];
-      f32x4 L2[4];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {   // row constants: dP - delta straight from the MFMA chain
-        const int q4 = q0 + 8 * g4 + 4 * h;   // rows acc_row(4*g4 + i, h) = q4 + i
-        L2[g4] = *(const f32x4*)(l2s + q4);
-        const f32x4 dl = *(const f32x4*)(dls + q4);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) dp[j][4 * g4 + i] = -dl[i];
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) sa[j] = zero16();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 qa = frag_row(qt, q0, s, lane), da = frag_row(dt_, q0, s, lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          sa[j] = mfma32(qa, kf[j][s], sa[j]);    // S[q][key]
-          dp[j] = mfma32(da, vf[j][s], dp[j]);    // dP[q][key] - delta[q]
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float p = fexp2(fmaf(sa[j][4 * g4 + i], c2, -L2[g4][i]));
-            sa[j][4 * g4 + i] = p;
-            dp[j][4 * g4 + i] = p * dp[j][4 * g4 + i];
-          }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 td[2], tq[2];
-#pragma unroll
-        for (int d2 = 0; d2 < 2; ++d2) {
-          td[d2] = frag_tr(dt_, q0 + 16 * s, 32 * d2, lane);
-          tq[d2] = frag_tr(qt, q0 + 16 * s, 32 * d2, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const bf16x8 pb = pack8(sa[j], s), sb = pack8(dp[j], s);
-#pragma unroll
-          for (int d2 = 0; d2 < 2; ++d2) {
-            dvt[j][d2] = mfma32(td[d2], pb, dvt[j][d2]);
-            dkt[j][d2] = mfma32(tq[d2], sb, dkt[j][d2]);
-          }
-        }
-      }
-    };
-    if constexpr (NQC > 0) {
-#pragma unroll
-      for (int q0 = 0; q0 < NQC * 32; q0 += 32) qblock(q0);
-    } else {
-#pragma unroll 1
-      for (int q0 = 0; q0 < NP; q0 += 32) qblock(q0);
-    }
-    if (more) load_regs(nbh, kf, vf, ls, dv);   // (kf / vf are dead until the next pair)
-    // dK, dV through this pair's (now free) Q | dO image: every wave must be done reading it
-    __syncthreads();
-    {
-      const int b = bh / H, hd = bh - b * H;
-      const bf16* db = dqkv + (int64_t)b * N * ld;
-      const __amdgpu_buffer_rsrc_t rdk = make_rsrc(db + D + hd * DH, bytes - (D + hd * DH) * 2);
-      const __amdgpu_buffer_rsrc_t rdv = make_rsrc(db + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
-      char* s0 = smem[buf] + (2 * wave) * ST_BYTES;
-      char* s1 = s0 + ST_BYTES;
-      float* part = colsum + (int64_t)b * 3 * D + hd * DH;   // the k- and v-bias gradient partials
-      const int ln = lane_here();
-      store_tile32(s0, dkt[0], scale, rdk, ldb, wave * 64, ln);
-      store_tile32(s1, dkt[1], scale, rdk, ldb, wave * 64 + 32, ln);
-      if (colsum) tile32x2_colsum(s0, s1, wave * 64, N, part + D, red, wave, NW, ln);
-      else asm volatile("" ::: "memory");
-      store_tile32(s0, dvt[0], 1.f, rdv, ldb, wave * 64, ln);
-      store_tile32(s1, dvt[1], 1.f, rdv, ldb, wave * 64 + 32, ln);
-      if (colsum) tile32x2_colsum(s0, s1, wave * 64, N, part + 2 * D, red, wave, NW, ln);
-    }
-    if (!more) break;
-    bh = nbh;
-    buf ^= 1;
-  }
-}
-
-// ---------------------------------------------- fused single-pass backward (N <= NPMAX)
-// One workgroup per (batch, head), NW = ceil(N/32) waves; wave w owns keys 32w..32w+31 exactly
-// as in attn_bwd_dkv_seq_bf16 (dK, dV accumulate in registers), and S, P, dP and dS of every
-// 32x32 block are formed ONCE (the two-kernel path forms them in both kernels: 28 MFMAs + two
-// exp passes per block, here 20 + one).  dQ needs a sum over keys, i.e. over waves:
-//   * the wave's dS block (accumulator: key on the lane) goes to a per-wave LDS scratch as
-//     dS^T[key][q] with 8-B writes, and comes back with ds_read_b64_tr_b16 as the B operand
-//     with q on the lane;
-//   * dQ^T[d][q] += K^T[d][key] dS^T[key][q], with the wave's K^T fragments in registers;
-//   * the partial goes into an fp32 dQ image in LDS by read-add-write.  At step t wave w works
-//     on query tile (w + t) mod NW and adds only after the tile's turn counter says step t-1's
-//     add is in, so every tile has one writer at a time and its sum order (w = tile, tile-1, ...)
-//     is fixed: deterministic, no atomics, no workgroup barrier inside the loop.
-// Delta = rowsum(dO * O) is formed in the prologue (each wave its own 32 query rows).
-// LDS (NPMAX = 256): Q | dO images 64 KiB + dQ fp32 [256][68] 68 KiB + L2 | delta 2 KiB +
-// scratch 8 x 2 KiB = 150 KiB: one workgroup per CU.
-__device__ __forceinline__ int scr_off(int key, int chunk) { return key * 64 + ((chunk ^ (key & 7)) << 3); }
-
-template <int NPMAX>
-__global__ __launch_bounds__(NPMAX * 2) void attn_bwd_fused_seq_bf16(
-    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
-    const float* __restrict__ lse, bf16* __restrict__ dqkv, int N, int H, float scale) {
-  constexpr int DQP = 68;                                  // dQ image row pitch (floats)
-  constexpr int OFF_DQ = 2 * NPMAX * 128;
-  constexpr int OFF_ROW = OFF_DQ + NPMAX * DQP * 4;
-  constexpr int OFF_SCR = OFF_ROW + 2 * NPMAX * 4;
-  constexpr int OFF_TURN = OFF_SCR + (NPMAX / 32) * 2048;
-  __shared__ __attribute__((aligned(16))) char smem[OFF_TURN + (NPMAX / 32) * 4];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = blockDim.x >> 6, NP = nw * 32;
-  const int bh = blockIdx.x, b = bh / H, hd = bh % H;
-  const int D = H * DH;
-  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
-  const int h = lane >> 5;
-  const bf16* base = qkv + (int64_t)b * N * ld;
-  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
-  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
-  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
-  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
-  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
-  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
-  __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
-  char* qt = smem;
-  char* dt_ = smem + NPMAX * 128;
-  float* dqs = (float*)(smem + OFF_DQ);
-  float* l2s = (float*)(smem + OFF_ROW);
-  float* dls = l2s + NPMAX;
-  char* scr = smem + OFF_SCR + wave * 2048;
-
-  // prologue: Q, dO images; the K image (128-B rows) parked in the dQ area for the K^T fragments
-  stage_seq(qt, rq, ldb, NP, nw, wave, lane);
-  stage_seq(dt_, rdo, ldo, NP, nw, wave, lane);
-  stage_seq(smem + OFF_DQ, rk, ldb, NP, nw, wave, lane);
-  const int r32 = wave * 32 + (lane & 31);   // this lane's key (dK/dV) and query (delta) row
-  bf16x8 kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = load_row16(rk, (uint32_t)((int64_t)r32 * ldb + (16 * s + 8 * h) * 2));
-    vf[s] = load_row16(rv, (uint32_t)((int64_t)r32 * ldb + (16 * s + 8 * h) * 2));
-  }
-  float dl;
-  {
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const uint32_t off = (uint32_t)((int64_t)r32 * ldo + (16 * s + 8 * h) * 2);
-      const bf16x8 dv = load_row16(rdo, off), ov = load_row16(ro, off);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) part += (float)ov[j] * (float)dv[j];
-    }
-    dl = part + __shfl_xor(part, 32, 64);
-  }
-  const bool rok = r32 < N;
-  const float l2v = rok ? lse[(int64_t)bh * N + r32] * LOG2E : INFINITY;   // q >= N -> P = 0
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (h == 0) {
-    l2s[r32] = l2v;
-    dls[r32] = rok ? dl : 0.f;
-  }
-  __syncthreads();
-  // K^T[d][key] fragments of this wave's keys (A operands of dQ^T = K^T dS^T)
-  bf16x8 ktf[2][2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int d2 = 0; d2 < 2; ++d2) ktf[s][d2] = frag_tr(smem + OFF_DQ, wave * 32 + 16 * s, 32 * d2, lane);
-  __syncthreads();   // (the barrier's fence retires the reads before the area is zeroed)
-  for (int i = threadIdx.x; i < NP * DQP / 4; i += blockDim.x) ((f32x4*)dqs)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int* turn = (int*)(smem + OFF_TURN);   // turn[tile] = steps whose dQ add into the tile is done
-  if (threadIdx.x < nw) turn[threadIdx.x] = 0;
-  __syncthreads();
-
-  const float c2 = scale * LOG2E;
-  const int g16 = lane >> 4, tl = lane & 15, qq = tl >> 2, pp = tl & 3;
-  f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
-#pragma unroll 1
-  for (int t = 0; t < nw; ++t) {
-    int qi = wave + t;
-    if (qi >= nw) qi -= nw;
-    const int q0 = qi * 32;
-    f32x16 sa = zero16(), dp = zero16();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
-      dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key]
-    }
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int q4 = q0 + 8 * g4 + 4 * h;
-      const f32x4 L2 = *(const f32x4*)(l2s + q4);
-      const f32x4 d4 = *(const f32x4*)(dls + q4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = fexp2(fmaf(sa[4 * g4 + i], c2, -L2[i]));
-        sa[4 * g4 + i] = p;
-        dp[4 * g4 + i] = p * (dp[4 * g4 + i] - d4[i]);
-      }
-    }
-    // dS^T[key][q] into the scratch: rows q = 8*g4 + 4h + 0..3 of this lane's key column
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      bf16x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (bf16)dp[4 * g4 + i];
-      *(bf16x4*)(scr + scr_off(lane & 31, 2 * g4 + h)) = v;
-    }
-    asm volatile("" ::: "memory");   // scratch writes stay ahead of the transposed reads
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
-#pragma unroll
-      for (int d2 = 0; d2 < 2; ++d2) {
-        dvt[d2] = mfma32(frag_tr(dt_, q0 + 16 * s, 32 * d2, lane), pb, dvt[d2]);
-        dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
-      }
-    }
-    // dQ^T[d][q] partial of this wave's 32 keys; B = dS^T with q on the lane (transposed read
-    // of the scratch: element j <-> key 16s + 8(j>>2) + 4h + (j&3), the frag_tr k order)
-    f32x16 dqp[2] = {zero16(), zero16()};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 sbt;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = 16 * s + 8 * i + 4 * (g16 >> 1) + qq;
-        s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, scr + scr_off(row, 4 * (g16 & 1) + pp)));
-        bf16x4 bv = __builtin_bit_cast(bf16x4, v);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sbt[4 * i + j] = bv[j];
-      }
-#pragma unroll
-      for (int d2 = 0; d2 < 2; ++d2) dqp[d2] = mfma32(ktf[s][d2], sbt, dqp[d2]);
-    }
-    // this step's only writer of query tile qi: dQ[q][d] += partial (lane q, d = 32d2 + acc_row).
-    // Step t-1 of tile qi belonged to wave w+1; wait for its add (turn[qi] == t) instead of a
-    // workgroup barrier, so the waves drift apart and one wave's MFMAs overlap another's softmax.
-    // The waits form a chain (w waits on w+1 one step earlier), so they always resolve; the
-    // bound only guards against a logic error hanging the device.  Should it ever be hit, the
-    // tile's dQ is poisoned with NaN (the parity tests then fail loudly) instead of being
-    // summed out of order.
-    bool late;
-    {
-      volatile int* tp = turn + qi;
-      for (int spin = 0; *tp != t && spin < (1 << 22); ++spin) __builtin_amdgcn_s_sleep(1);
-      late = *tp != t;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    float* dq_row = dqs + (q0 + (lane & 31)) * DQP;
-    const float poison = late ? __builtin_nanf("") : 0.f;
-#pragma unroll
-    for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        f32x4* pq = (f32x4*)(dq_row + 32 * d2 + 8 * g4 + 4 * h);
-        f32x4 a = *pq;
-        a[0] += dqp[d2][4 * g4] + poison;
-        a[1] += dqp[d2][4 * g4 + 1] + poison;
-        a[2] += dqp[d2][4 * g4 + 2] + poison;
-        a[3] += dqp[d2][4 * g4 + 3] + poison;
-        *pq = a;
-      }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    *(volatile int*)(turn + qi) = t + 1;
-  }
-  __syncthreads();   // every tile's last add is in
-  // dK, dV of the wave's keys
-  if (rok) {
-    bf16* row = dqkv + ((int64_t)b * N + r32) * ld;
-#pragma unroll
-    for (int d2 = 0; d2 < 2; ++d2)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * d2 + 8 * g4 + 4 * h;
-        store4(row + D + hd * DH + d, dkt[d2][4 * g4] * scale, dkt[d2][4 * g4 + 1] * scale,
-               dkt[d2][4 * g4 + 2] * scale, dkt[d2][4 * g4 + 3] * scale);
-        store4(row + 2 * D + hd * DH + d, dvt[d2][4 * g4], dvt[d2][4 * g4 + 1], dvt[d2][4 * g4 + 2],
-               dvt[d2][4 * g4 + 3]);
-      }
-    // dQ of query row r32 (all writers finished at the loop's last barrier): half h = d 32h..
-    bf16* qrow = row + hd * DH + 32 * h;
-    const float* src = dqs + r32 * DQP + 32 * h;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const f32x4 a = *(const f32x4*)(src + 4 * c);
-      store4(qrow + 4 * c, a[0] * scale, a[1] * scale, a[2] * scale, a[3] * scale);
-    }
-  }
-}
 
 // =============================================================== fp32 path (MFMA, N <= NPMAX)
 // The fp32 parity configuration on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: full fp32
@@ -1923,9 +1505,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_f32(const float* __restrict_
 using namespace vitmi;
 
 // whole-sequence kernels for N <= SEQ_MAX (8 waves, 2 workgroups of <= 64 KiB LDS per CU).
-// Kernel policy (vitmi_attention_set_policy; tests / A-B timing): 0 = auto, 1 = always the
-// streamed kernels, 2 = auto with the single-pass fused backward for N <= SEQ_MAX, 3 = auto with
-// the two-key-blocks-per-wave dK/dV kernel.
+// Kernel policy (vitmi_attention_set_policy; tests): 0 = auto, 1 = always the streamed kernels.
 static constexpr int SEQ_MAX = 256;
 
 static int device_cus() {   // compute units of the current device (the persistent dK/dV grid)
@@ -1942,16 +1522,9 @@ static int device_cus() {   // compute units of the current device (the persiste
 }
 static int g_attn_policy = 0;
 static bool seq_path(int N) { return N <= SEQ_MAX && g_attn_policy != 1; }
-static bool fused_bwd() { return g_attn_policy == 2; }
-// 3 = auto with the two-key-blocks-per-wave dK/dV kernel (attn_bwd_dkv_seq2_bf16); a build with
-// VITMI_ATT_DKV2=1 makes it the auto choice (A/B timing)
-#ifndef VITMI_ATT_DKV2
-#define VITMI_ATT_DKV2 0
-#endif
-static bool dkv2() { return g_attn_policy == 3 || (VITMI_ATT_DKV2 && g_attn_policy == 0); }
 
 extern "C" int vitmi_attention_set_policy(int policy) {
-  VITMI_CHECK_ARG(policy >= 0 && policy <= 3, "attention_set_policy: policy must be 0..3");
+  VITMI_CHECK_ARG(policy == 0 || policy == 1, "attention_set_policy: policy must be 0 or 1");
   const int prev = g_attn_policy;
   g_attn_policy = policy;
   return prev;
@@ -2017,10 +1590,7 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
   if (dtype == VITMI_BF16 && seq_path(N)) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
     const dim3 block(64 * ((N + 31) / 32));
-    if (!colsum && fused_bwd()) {
-      hipLaunchKernelGGL(attn_bwd_fused_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv,
-                         (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, N, H, scale);
-    } else {
+    {
       const int npairs = B * H, cus = device_cus();
       const dim3 gkv(npairs < cus ? npairs : cus);
       const bool n7 = (N + 31) / 32 == 7;   // N in (192, 224]: the ViT-B/ViT-S shape, N = 197
@@ -2030,13 +1600,7 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
       else
         hipLaunchKernelGGL((attn_bwd_dq_seq_bf16<SEQ_MAX>), dim3(B * H), block, 0, s, (const bf16*)qkv,
                            (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
-      if (dkv2() && n7)
-        hipLaunchKernelGGL((attn_bwd_dkv_seq2_bf16<SEQ_MAX, 7>), gkv, dim3(256), 0, s, (const bf16*)qkv,
-                           (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
-      else if (dkv2())
-        hipLaunchKernelGGL((attn_bwd_dkv_seq2_bf16<SEQ_MAX>), gkv, dim3(256), 0, s, (const bf16*)qkv,
-                           (const bf16*)dout, lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
-      else if (n7)
+      if (n7)
         hipLaunchKernelGGL((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), gkv, block, 0, s, (const bf16*)qkv, (const bf16*)dout,
                            lse, (const float*)delta, (bf16*)dqkv, N, H, scale, colsum, npairs);
       else
@@ -2076,20 +1640,12 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     const double es = dtype == VITMI_BF16 ? 2 : 4, bh = (double)B * H, t = bh * N * DH;
     const double fl = 4.0 * bh * N * N * DH;
     if (dtype == VITMI_BF16 && seq_path(N)) {
-      if (!colsum && fused_bwd()) {
-        VITMI_STAT(attn_bwd_fused_seq_bf16<SEQ_MAX>, 2 * fl, t * 8 * es + bh * N * 4);
+      if ((N + 31) / 32 == 7) {
+        VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+        VITMI_STAT((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
       } else {
-        if ((N + 31) / 32 == 7) {
-          VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
-          if (dkv2()) VITMI_STAT((attn_bwd_dkv_seq2_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
-          else VITMI_STAT((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
-        } else if (dkv2()) {
-          VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
-          VITMI_STAT(attn_bwd_dkv_seq2_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
-        } else {
-          VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
-          VITMI_STAT(attn_bwd_dkv_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
-        }
+        VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
+        VITMI_STAT(attn_bwd_dkv_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
       }
     } else if (dtype == VITMI_BF16) {
       VITMI_STAT(attn_bwd_dq_bf16, fl, t * 6 * es + bh * N * 8);

@@ -11,8 +11,13 @@
 // process: PyTorch-ROCm loads its own librccl.so, and two RCCL instances in one process
 // would each start their own proxy threads and IPC state.  No RCCL symbol is linked, so
 // the library still loads (and every other entry point works) where RCCL is absent.
+//
+// Thread safety: every entry point that touches the communicator holds g_mu, so the DP
+// watchdog's abort (vitmi_comm_destroy(1) from its own thread, vitmi/dp.py CommWatchdog) never
+// frees the communicator between another thread's null check and its ncclAllReduce.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <string.h>
@@ -34,6 +39,7 @@ struct Rccl {
 };
 
 Rccl g_rccl;
+std::mutex g_mu;   // guards g_rccl loading, g_comm, g_rank, g_world
 ncclComm_t g_comm = nullptr;
 int g_rank = -1, g_world = 0;
 
@@ -84,6 +90,7 @@ using namespace vitmi;
 
 extern "C" int vitmi_comm_get_unique_id(char* uid) {
   VITMI_CHECK_ARG(uid != nullptr, "comm_get_unique_id: uid is null");
+  std::lock_guard<std::mutex> lk(g_mu);
   if (int rc = load_rccl()) return rc;
   ncclUniqueId id;
   if (ncclResult_t r = g_rccl.get_unique_id(&id)) return nccl_fail("ncclGetUniqueId", r);
@@ -95,13 +102,22 @@ extern "C" int vitmi_comm_get_unique_id(char* uid) {
 extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
   VITMI_CHECK_ARG(world >= 1 && rank >= 0 && rank < world, "comm_init: rank %d / world %d", rank, world);
   VITMI_CHECK_ARG(uid != nullptr, "comm_init: uid is null");
-  VITMI_CHECK_ARG(g_comm == nullptr, "comm_init: a communicator already exists (vitmi_comm_destroy first)");
-  if (int rc = load_rccl()) return rc;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    VITMI_CHECK_ARG(g_comm == nullptr, "comm_init: a communicator already exists (vitmi_comm_destroy first)");
+    if (int rc = load_rccl()) return rc;
+  }
   ncclUniqueId id;
   memcpy(id.internal, uid, VITMI_COMM_UID_BYTES);
   ncclComm_t c = nullptr;
-  // the communicator binds to the calling thread's current HIP device
+  // the communicator binds to the calling thread's current HIP device; the rendezvous with the
+  // other ranks runs without the lock held
   if (ncclResult_t r = g_rccl.init_rank(&c, world, id, rank)) return nccl_fail("ncclCommInitRank", r);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_comm != nullptr) {
+    g_rccl.destroy(c);
+    return fail(VITMI_ERR_INVALID, "comm_init: a communicator was created concurrently");
+  }
   g_comm = c;
   g_rank = rank;
   g_world = world;
@@ -110,6 +126,7 @@ extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
 
 extern "C" int vitmi_comm_library(char* path, int len) {
   VITMI_CHECK_ARG(path != nullptr && len > 0, "comm_library: bad buffer");
+  std::lock_guard<std::mutex> lk(g_mu);
   if (int rc = load_rccl()) return rc;
   Dl_info info;
   if (!dladdr(reinterpret_cast<void*>(g_rccl.all_reduce), &info) || !info.dli_fname)
@@ -119,6 +136,7 @@ extern "C" int vitmi_comm_library(char* path, int len) {
 }
 
 extern "C" int vitmi_comm_info(int* rank, int* world) {
+  std::lock_guard<std::mutex> lk(g_mu);
   if (rank) *rank = g_rank;
   if (world) *world = g_world;
   return g_comm ? VITMI_OK : fail(VITMI_ERR_INVALID, "comm_info: no communicator");
@@ -126,7 +144,8 @@ extern "C" int vitmi_comm_info(int* rank, int* world) {
 
 extern "C" int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, int op, vitmi_stream_t side,
                                           void* ready_event) {
-  VITMI_CHECK_ARG(g_comm != nullptr, "comm_allreduce_async: vitmi_comm_init first");
+  std::lock_guard<std::mutex> lk(g_mu);
+  VITMI_CHECK_ARG(g_comm != nullptr, "comm_allreduce_async: no communicator (never initialised, or aborted)");
   VITMI_CHECK_ARG(count >= 0, "comm_allreduce_async: negative count");
   VITMI_CHECK_ARG(op == VITMI_REDUCE_SUM || op == VITMI_REDUCE_AVG, "comm_allreduce_async: bad op %d", op);
   ncclDataType_t t;
@@ -144,6 +163,7 @@ extern "C" int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, i
 }
 
 extern "C" int vitmi_comm_broadcast(void* ptr, int64_t count, int dtype, int root, vitmi_stream_t stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
   VITMI_CHECK_ARG(g_comm != nullptr, "comm_broadcast: vitmi_comm_init first");
   VITMI_CHECK_ARG(root >= 0 && root < g_world, "comm_broadcast: bad root %d", root);
   ncclDataType_t t;
@@ -155,6 +175,7 @@ extern "C" int vitmi_comm_broadcast(void* ptr, int64_t count, int dtype, int roo
 }
 
 extern "C" int vitmi_comm_check(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
   if (!g_comm) return VITMI_OK;
   ncclResult_t a = ncclSuccess;
   if (ncclResult_t r = g_rccl.async_err(g_comm, &a)) return nccl_fail("ncclCommGetAsyncError", r);
@@ -163,6 +184,7 @@ extern "C" int vitmi_comm_check(void) {
 }
 
 extern "C" int vitmi_comm_destroy(int abort) {
+  std::lock_guard<std::mutex> lk(g_mu);
   if (!g_comm) return VITMI_OK;
   ncclComm_t c = g_comm;
   g_comm = nullptr;

@@ -14,6 +14,7 @@
 // fp32 (exact fp32 products).  For fp32 each lane reads 8 consecutive k and the
 // j-th MFMA consumes element j from every lane group: both operands use the same
 // k permutation, so the sum is unchanged.
+#include <atomic>
 #include "common.h"
 #include <stdlib.h>
 #include <type_traits>
@@ -95,7 +96,6 @@ struct GemmArgs {
   float* colsum;
   unsigned long long* stamps;        // DIAGNOSTIC build only (VITMI_GEMM_STAMPS)
   int aux_tiled;                     // gelu' in the tile-native layout (VITMI_EPI_AUX_TILED)
-  int ct;                            // EPI_PARTIAL: slabs hold C^T ([N][M], row stride ldc)
 };
 
 // Element (row, col) of a tile-native gelu' buffer (VITMI_EPI_AUX_TILED; bf16 elements): 256x256
@@ -274,7 +274,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_
   } else if constexpr (EPI == EPI_RESIDUAL_DROP) {
     ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + (acc + biasv) * drop_factor(g, row, col);
   } else if constexpr (EPI == EPI_PARTIAL) {
-    ((float*)g.C)[blockIdx.z * g.split_stride + (g.ct ? col * g.ldc + row : row * g.ldc + col)] = acc;
+    ((float*)g.C)[blockIdx.z * g.split_stride + row * g.ldc + col] = acc;
   } else if constexpr (EPI == VITMI_EPI_STORE) {
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(acc + biasv);
   } else if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
@@ -811,9 +811,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       if constexpr (EPI == EPI_PARTIAL) zoff = (int64_t)(blockIdx.z + zs) * g.split_stride;
       char* cbase = (char*)g.C + (zoff + m0 * g.ldc + n0) * CES;
       const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, clamp_bytes(((g.M - m0) * g.ldc - n0) * CES));
-      // (EPI_PARTIAL with ct: the C^T slab from its element (n0, m0))
-      [[maybe_unused]] const __amdgpu_buffer_rsrc_t rct =
-          make_rsrc((char*)g.C + (zoff + n0 * g.ldc + m0) * 4, clamp_bytes(((g.N - n0) * g.ldc - m0) * 4));
       const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
       const uint32_t vbase = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldc + wn * 64 + lc4) * CES);
       // Branch-free ragged N (straight-line epilogue code schedules far better): lanes past
@@ -911,21 +908,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         }
         if constexpr (CES == 4) {
           if constexpr (EPI == EPI_PARTIAL) {
-            if (g.ct) {
-              // C^T slab [N][M]: each of the lane's 4 columns is a slab row; the 16 lanes of a
-              // column group store 16 consecutive m (64 B) per instruction.  Rows >= M dropped.
-              const bool mok = m0 + wm * 128 + mi * 16 + lr < g.M;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const uint32_t vo = cok[ni] && mok ? (uint32_t)(((int64_t)(wn * 64 + ni * 16 + lc4 + e) * g.ldc +
-                                                                 wm * 128 + mi * 16 + lr) * 4) : 0x80000000u;
-                asm volatile(VMEM_SGPR_GUARD "buffer_store_dword %0, %1, %2, 0 offen" VITMI_ST_PART "\n\ts_nop 1"
-                             :: "v"(v[e]), "v"(vo), "s"(rct) : "memory");
-              }
-            } else {
-              asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_PART "\n\ts_nop 1"
-                           :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
-            }
+            asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_PART "\n\ts_nop 1"
+                         :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
           } else
             asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4" VITMI_ST_C32 "\n\ts_nop 1"
                          :: "v"(v), "v"(vb[ni]), "s"(rc), "s"(soff), "i"(ni * 64) : "memory");
@@ -1156,7 +1140,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       constexpr int EP = CES2 ? (EB == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU ? 32 : 16)
                               : (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ? 64
                                  : EPI == VITMI_EPI_DGELU ? 48 : 32);
-      ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : (EPI == EPI_PARTIAL && g.ct ? 128 : EP);
+      ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : EP;
     }
     if (!has_next) break;
     it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
@@ -1289,7 +1273,9 @@ __global__ __launch_bounds__(256) void tail_colsum_kernel(GemmArgs g) {
 static int g_policy = 0;
 static int g_cus = 256;   // compute units of the current device (set on first use)
 
-static int g_reserved = 0;        // CUs the persistent grid leaves free (vitmi_gemm_set_reserved_cus)
+// CUs the persistent grid leaves free (vitmi_gemm_set_reserved_cus).  Atomic: the DP reducer may
+// change it from a thread other than the one launching GEMMs.
+static std::atomic<int> g_reserved{0};
 #ifdef VITMI_GEMM_STAMPS
 static unsigned long long* g_stamps = nullptr;
 #endif
@@ -1326,7 +1312,7 @@ static bool use256(int dtype, int64_t M, int64_t N, int64_t K = 0, bool split = 
 
 // persistent grid of the gemm256 launch for nwg tiles and `splits` K-slabs
 static int grid256(int nwg, int splits) {
-  int gx = (g_cus - g_reserved) / splits;
+  int gx = (g_cus - g_reserved.load(std::memory_order_relaxed)) / splits;
   if (gx < 8 || g_policy == 3) gx = 8;   // policy 3: force many tiles per block (tests)
   return gx > nwg ? nwg : gx;
 }
@@ -1486,8 +1472,10 @@ static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits
 static int bk_of(int dtype) { return dtype == VITMI_BF16 ? 64 : 32; }
 
 // split count for a reduction-heavy GEMM (wgrad): about one full round of blocks
-// (1 block/CU for gemm256, ~2 for the 128 kernel), at least 4 k-tiles per split.
-static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K) {
+// (1 block/CU for gemm256, ~2 for the 128 kernel), at least 4 k-tiles per split.  `reserved`:
+// the CUs left free; the workspace queries size for 0 (the most splits), so a workspace sized
+// while CUs were reserved is never short after the reservation ends, or the reverse.
+static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K, int reserved) {
   const bool big = use256(dtype, M, N, K, true);
   const int64_t t = big ? 256 : 128;
   const int64_t tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
@@ -1495,7 +1483,7 @@ static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K) {
   // about one round of the CUs the persistent grid may use: with reserved CUs (DP overlap) a
   // fixed 256 left a few units for a second full round (fc1 wgrad 262 -> 440 us at 8 reserved)
   init_cus();
-  const int avail = g_cus - g_reserved > 8 ? g_cus - g_reserved : 8;
+  const int avail = g_cus - reserved > 8 ? g_cus - reserved : 8;
   return (int)splits_for(tiles, ktiles, big ? avail : 2 * avail);
 }
 
@@ -1503,10 +1491,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
                      int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
                      int epi, const float* bias, void* aux, int64_t ldaux, const float* residual,
                      int64_t ldr, void* ws, size_t ws_bytes, hipStream_t s, bool allow_split,
-                     const GemmArgs* drop = nullptr, float* colsum = nullptr, bool* colsum_done = nullptr,
-                     bool tc = false) {
-  // tc: C^T += A B (EPI_ACCUM only): the split-K slabs are written transposed (EPI_PARTIAL with
-  // ct) and folded into the dense C[N][M] by the plain reduction, whatever the split count
+                     const GemmArgs* drop = nullptr, float* colsum = nullptr, bool* colsum_done = nullptr) {
   if (colsum_done) *colsum_done = false;
   const bool aux_tiled = (epi & VITMI_EPI_AUX_TILED) != 0;
   epi &= ~VITMI_EPI_AUX_TILED;
@@ -1522,7 +1507,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   VITMI_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "gemm: A/B must be 16-byte aligned");
   VITMI_CHECK_ARG(ak ? lda >= K : lda >= M, "gemm: lda too small");
   VITMI_CHECK_ARG(bk ? ldb >= K : ldb >= N, "gemm: ldb too small");
-  VITMI_CHECK_ARG(ldc >= (tc ? M : N), "gemm: ldc too small");
+  VITMI_CHECK_ARG(ldc >= N, "gemm: ldc too small");
   const int eb = epi_base(epi);
   if (eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_DGELU)
     VITMI_CHECK_ARG(aux != nullptr && ldaux >= N, "gemm: epilogue needs aux");
@@ -1557,15 +1542,13 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
     g.drop_thresh = drop->drop_thresh; g.drop_scale = drop->drop_scale;
   }
   int splits = 1;
-  if (allow_split && epi == VITMI_EPI_ACCUM) splits = choose_splits(dtype, M, N, K);
+  if (allow_split && epi == VITMI_EPI_ACCUM) splits = choose_splits(dtype, M, N, K, g_reserved.load(std::memory_order_relaxed));
   const int64_t ktiles = (K + BK - 1) / BK;
   g.k_per_split = ((ktiles + splits - 1) / splits) * BK;
   if (K == 0) g.k_per_split = BK;
   splits = (int)((K + g.k_per_split - 1) / g.k_per_split);
   if (splits < 1) splits = 1;
-  if (tc) VITMI_CHECK_ARG(epi == VITMI_EPI_ACCUM && ws && ws_bytes >= (size_t)splits * M * N * sizeof(float),
-                         "gemm: transposed accumulate needs the split workspace");
-  if (splits > 1 && !tc) {
+  if (splits > 1) {
     const size_t need = (size_t)splits * M * N * sizeof(float);
     if (ws == nullptr || ws_bytes < need) splits = 1, g.k_per_split = ktiles * BK;
   }
@@ -1586,7 +1569,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
     }
   }
   const bool big_ok = big2;
-  if (splits == 1 && !tc) {
+  if (splits == 1) {
     g.k_per_split = (K > 0 ? ktiles : 1) * BK;
     g.tail_ws = (float*)ws;   // tail split of the persistent gemm256 launch (if it fits)
     g.tail_ws_bytes = ws ? ws_bytes : 0;
@@ -1599,12 +1582,11 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   }
   // split-K: partial slabs then one reduction pass into C (+=)
   GemmArgs gp = g;
-  gp.C = ws; gp.ldc = tc ? M : N; gp.split_stride = M * N;
-  gp.ct = tc;
+  gp.C = ws; gp.ldc = N; gp.split_stride = M * N;
   int rc = dtype == VITMI_BF16 ? dispatch<bf16>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big_ok, s)
                                : dispatch<float>(ak, bk, VITMI_F32, EPI_PARTIAL, gp, splits, big_ok, s);
   if (rc) return rc;
-  VITMI_CHECK_ARG(ldc == (tc ? M : N), "gemm: split-K accumulate needs a dense C");
+  VITMI_CHECK_ARG(ldc == N, "gemm: split-K accumulate needs a dense C");
   const int64_t n = M * N;
   int blocks = (int)((n / 4 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
@@ -1629,9 +1611,7 @@ extern "C" int vitmi_gemm_set_stamps(void* buf) {
 
 extern "C" int vitmi_gemm_set_reserved_cus(int n) {
   init_cus();
-  const int prev = g_reserved;
-  g_reserved = n < 0 ? 0 : (n > g_cus - 8 ? g_cus - 8 : n);
-  return prev;
+  return g_reserved.exchange(n < 0 ? 0 : (n > g_cus - 8 ? g_cus - 8 : n));
 }
 
 extern "C" int vitmi_gemm_set_policy(int policy) {
@@ -1653,7 +1633,7 @@ extern "C" size_t vitmi_gemm_workspace_size(int dtype, int a_kmajor, int b_kmajo
                                             int64_t N, int64_t K, int epilogue) {
   (void)a_kmajor; (void)b_kmajor;
   if (epilogue != VITMI_EPI_ACCUM) return use256(dtype, M, N) ? tail_ws_bytes(M, N, K) : 0;
-  const int splits = choose_splits(dtype, M, N, K);
+  const int splits = choose_splits(dtype, M, N, K, 0);
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
@@ -1743,32 +1723,8 @@ extern "C" int vitmi_linear_dgrad_bias(int dtype, int64_t M, int64_t N, int64_t 
 
 extern "C" size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
   // dW[N,K]: GEMM rows N, cols K, reduction M
-  const int splits = choose_splits(dtype, N, K, M);
+  const int splits = choose_splits(dtype, N, K, M, 0);
   return splits > 1 ? (size_t)splits * N * K * sizeof(float) : 0;
-}
-
-extern "C" size_t vitmi_linear_wgrad_xt_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
-  // the transposed product dW^T[K,N]: GEMM rows K, cols N, reduction M; at least one slab
-  const int splits = choose_splits(dtype, K, N, M);
-  return (size_t)(splits > 1 ? splits : 1) * N * K * sizeof(float);
-}
-
-extern "C" int vitmi_linear_wgrad_xt(int dtype, int64_t M, int64_t N, int64_t K, const void* dy, const void* xt,
-                                     int64_t ldxt, float* dw, void* workspace, size_t ws_bytes,
-                                     vitmi_stream_t stream) {
-  // dW[N,K] += sum_m dy[m][n] xt[k][m], formed as the product dW^T = xt dy: A(k,m) = xt (m
-  // contiguous: k-major in GEMM terms), B(m,n) = dy (n contiguous); the slabs are written transposed
-  return gemm_impl(dtype, 1, 0, K, N, M, xt, ldxt, dy, N, dw, K, VITMI_F32, VITMI_EPI_ACCUM, nullptr, nullptr, 0,
-                   nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, true, nullptr, nullptr, nullptr, true);
-}
-
-extern "C" int vitmi_linear_wgrad_dyt(int dtype, int64_t M, int64_t N, int64_t K, const void* dyt, int64_t lddyt,
-                                      const void* x, float* dw, void* workspace, size_t ws_bytes,
-                                      vitmi_stream_t stream) {
-  // dW[N,K] += sum_m dyt[n][m] x[m][k]: A(n,m) = dyt (m contiguous), B(m,k) = x (k contiguous);
-  // workspace: vitmi_linear_wgrad_workspace_size
-  return gemm_impl(dtype, 1, 0, N, K, M, dyt, lddyt, x, K, dw, K, VITMI_F32, VITMI_EPI_ACCUM, nullptr, nullptr, 0,
-                   nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, true);
 }
 
 extern "C" int vitmi_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, const void* dy,

@@ -32,58 +32,12 @@ __device__ __forceinline__ void adam1(const AdamArgs& a, float& p, float g, floa
   p = __fsub_rn(p, __fdiv_rn(__fmul_rn(m, a.alpha), den));
 }
 
-// streaming form (A/B builds): two float4 groups per thread and iteration (8 loads in flight per
-// lane) and non-temporal stores (p, m, v are next read by the next step's Adam; the bf16 shadow
-// by the next forward's GEMMs, from the MALL at best)
-#ifndef VITMI_ADAM_V2
-#define VITMI_ADAM_V2 0
-#endif
-template <typename V>
-__device__ __forceinline__ void st_stream(V* p, V v) {
-  if constexpr (VITMI_ADAM_V2) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-
-template <bool LP>
-__device__ __forceinline__ void adam4(const AdamArgs& a, int64_t i, float* __restrict__ p, const float* __restrict__ g,
-                                      float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ lp,
-                                      f32x4 pv, f32x4 gv, f32x4 mv, f32x4 vv) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float pe = pv[e], me = mv[e], ve = vv[e];
-    adam1(a, pe, gv[e], me, ve);
-    pv[e] = pe;
-    mv[e] = me;
-    vv[e] = ve;
-  }
-  st_stream((f32x4*)p + i, pv);
-  st_stream((f32x4*)m + i, mv);
-  st_stream((f32x4*)v + i, vv);
-  if constexpr (LP) {
-    bf16x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = from_f32<bf16>(pv[e]);
-    st_stream((bf16x4*)lp + i, o);
-  }
-}
-
 template <bool LP>
 __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16* __restrict__ lp, AdamArgs a) {
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-#if VITMI_ADAM_V2
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + stride < n4; i += 2 * stride) {
-    const f32x4 p0 = ((const f32x4*)p)[i], g0 = ((const f32x4*)g)[i], m0 = ((const f32x4*)m)[i], v0 = ((const f32x4*)v)[i];
-    const int64_t j = i + stride;
-    const f32x4 p1 = ((const f32x4*)p)[j], g1 = ((const f32x4*)g)[j], m1 = ((const f32x4*)m)[j], v1 = ((const f32x4*)v)[j];
-    adam4<LP>(a, i, p, g, m, v, lp, p0, g0, m0, v0);
-    adam4<LP>(a, j, p, g, m, v, lp, p1, g1, m1, v1);
-  }
-  if (i < n4) adam4<LP>(a, i, p, g, m, v, lp, ((const f32x4*)p)[i], ((const f32x4*)g)[i], ((const f32x4*)m)[i], ((const f32x4*)v)[i]);
-#else
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pv = ((const f32x4*)p)[i], gv = ((const f32x4*)g)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
 #pragma unroll
@@ -104,7 +58,6 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
       ((bf16x4*)lp)[i] = o;
     }
   }
-#endif
   // tail (n % 4) by the first threads
   const int64_t t = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n && t < n4 * 4 + 4) {

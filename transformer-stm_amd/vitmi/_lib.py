@@ -42,17 +42,11 @@ SIGNATURES = {
     "vitmi_linear_dgrad_workspace_size": (S, [I, L, L, L]),
     "vitmi_linear_wgrad": (I, [I, L, L, L, P, P, P, P, S, P]),
     "vitmi_linear_wgrad_workspace_size": (S, [I, L, L, L]),
-    "vitmi_linear_wgrad_xt": (I, [I, L, L, L, P, P, L, P, P, S, P]),
-    "vitmi_linear_wgrad_xt_workspace_size": (S, [I, L, L, L]),
-    "vitmi_linear_wgrad_dyt": (I, [I, L, L, L, P, L, P, P, P, S, P]),
     "vitmi_bias_grad": (I, [I, L, L, P, L, P, P, S, P]),
     "vitmi_bias_grad_workspace_size": (S, [L, L]),
     "vitmi_layernorm_fwd": (I, [L, I, P, L, P, P, F, P, I, L, P, P, P]),
     "vitmi_layernorm_bwd": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, P, P, P, S, P]),
     "vitmi_layernorm_bwd_workspace_size": (S, [L, I]),
-    "vitmi_layernorm_fwd_res": (I, [L, I, P, L, P, L, P, P, F, P, L, P, I, L, P, P, P]),
-    "vitmi_layernorm_fwd_t": (I, [L, I, P, L, P, P, F, P, L, P, L, P, P, P]),
-    "vitmi_layernorm_bwd_t": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, L, P, P, P, P, S, P]),
     "vitmi_attention_fwd": (I, [I, I, I, I, I, F, P, P, P, P]),
     "vitmi_attention_bwd": (I, [I, I, I, I, I, F, P, P, P, P, P, P, S, P]),
     "vitmi_attention_bwd_workspace_size": (S, [I, I, I]),

@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .modules import F32, LayerNorm, Linear, _check_cuda, _drop_args, _grad, _lp, cross_entropy, mse_loss  # noqa: F401
+from .modules import F32, LayerNorm, Linear, _check_cuda, _drop_args, _lp, _sink, cross_entropy, mse_loss  # noqa: F401
 
 Tensor = torch.Tensor
 
@@ -143,18 +143,21 @@ class _ConvEmbedFn(torch.autograd.Function):
         T = patches.dtype
         C, D, k = mod.cin, mod.dim, mod.k
         K = k * k * C
+        gs = _sink(ctx, 7, (mod.weight, mod.bias))
         dy = dy.contiguous().float()
         dy_lp = dy if T == F32 else ops.cast_bf16(dy)
-        dwm = torch.zeros(D, wm.shape[1], dtype=torch.float32, device=dy.device)
-        ops.linear_wgrad(dy_lp, patches, dwm)
-        _grad(mod.weight).add_(dwm[:, :K].view(D, k, k, C).permute(0, 3, 1, 2))
-        ops.bias_grad(dy_lp, _grad(mod.bias))
+        if gs.wants(mod.weight):
+            dwm = torch.zeros(D, wm.shape[1], dtype=torch.float32, device=dy.device)
+            ops.linear_wgrad(dy_lp, patches, dwm)
+            gs(mod.weight).add_(dwm[:, :K].view(D, k, k, C).permute(0, 3, 1, 2))
+        if gs.wants(mod.bias):
+            ops.bias_grad(dy_lp, gs(mod.bias))
         dx = None
         if ctx.needs_input_grad[0]:
             dp = ops.linear_dgrad(dy_lp, wm, F32)
             dx = torch.zeros_like(x)
             ops.conv_col2im(dp, B, H, H, C, k, mod.s, geo, dx, img_stride, row_off)
-        return (dx,) + (None,) * 8
+        return (dx,) + (None,) * 6 + gs.grads((mod.weight, mod.bias))
 
 
 # ======================================================================= dw_bn projection
@@ -295,6 +298,8 @@ class _CvTBlockFn(torch.autograd.Function):
         off = 1 if with_cls else 0
         a_, mlp = blk.attn, blk.mlp
         n1, n2 = blk.norm1, blk._norm2
+        ps = list(blk.parameters())
+        gs = _sink(ctx, 6, ps)
         g2 = dout.contiguous().view(M, D).float()
         drop = ctx.drop
         if drop is None:
@@ -302,13 +307,16 @@ class _CvTBlockFn(torch.autograd.Function):
         else:   # the fc2 branch was dropped: its dgrad/wgrad/bias see g2 * mask / (1 - p)
             g2_lp = ops.dropout_apply(g2, drop[0], drop[2] + 2, drop[1], T)
         # MLP
-        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias),
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=gs(mlp.fc1.bias),
                               aux_tiled=T == torch.bfloat16)
-        ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
-        ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
+        if gs.wants(mlp.fc2.weight):
+            ops.linear_wgrad(g2_lp, act, gs(mlp.fc2.weight))
+        if gs.wants(mlp.fc2.bias):
+            ops.bias_grad(g2_lp, gs(mlp.fc2.bias))
         dh2 = ops.linear_dgrad(du, w1, T)
-        ops.linear_wgrad(du, h2, _grad(mlp.fc1.weight))
-        dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias), dres=g2,
+        if gs.wants(mlp.fc1.weight):
+            ops.linear_wgrad(du, h2, gs(mlp.fc1.weight))
+        dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, gs(n2.weight), gs(n2.bias), dres=g2,
                                         lp_dtype=lpT if drop is None else None)
         if drop is not None:   # the out-projection branch was dropped
             dx1_lp = ops.dropout_apply(dx1, drop[0], drop[2], drop[1], T)
@@ -316,8 +324,10 @@ class _CvTBlockFn(torch.autograd.Function):
             dx1_lp = dx1
         # attention + out-projection
         do = ops.linear_dgrad(dx1_lp, wo, T)
-        ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
-        ops.bias_grad(dx1_lp, _grad(a_.proj.bias))
+        if gs.wants(a_.proj.weight):
+            ops.linear_wgrad(dx1_lp, o, gs(a_.proj.weight))
+        if gs.wants(a_.proj.bias):
+            ops.bias_grad(dx1_lp, gs(a_.proj.bias))
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, scale)
         # q/k/v GEMMs, the cls rows, dw_bn: all into the LN1-output gradient dh
         dh = torch.zeros(M, D, dtype=torch.float32, device=g2.device)
@@ -326,9 +336,10 @@ class _CvTBlockFn(torch.autograd.Function):
             lin = getattr(a_, f"proj_{c}")
             dq = dqkv[:, c_i * D:(c_i + 1) * D].contiguous()
             dinp = ops.linear_dgrad(dq, wl, F32)
-            ops.linear_wgrad(dq, inp, _grad(lin.weight))
-            if lin.bias is not None:
-                ops.bias_grad(dq, _grad(lin.bias))
+            if gs.wants(lin.weight):
+                ops.linear_wgrad(dq, inp, gs(lin.weight))
+            if gs.wants(lin.bias):
+                ops.bias_grad(dq, gs(lin.bias))
             if meth == "linear":
                 dh.add_(dinp)
                 continue
@@ -340,11 +351,17 @@ class _CvTBlockFn(torch.autograd.Function):
                 continue
             cp = getattr(a_, f"conv_proj_{c}")
             dw9 = torch.zeros(9, D, dtype=torch.float32, device=g2.device)
+            # (the BN parameter gradients always have a destination: the kernel writes them)
+            dg = gs(cp.bn.weight)
+            db = gs(cp.bn.bias)
+            dg = dg if dg is not None else torch.zeros(D, device=g2.device)
+            db = db if db is not None else torch.zeros(D, device=g2.device)
             ops.dwconv_bn_bwd(dinp, h, B, H, W, cp.w9(), cp.bn.weight, z, mean, rstd, dh, dw9,
-                              _grad(cp.bn.weight), _grad(cp.bn.bias), x_img=N, x_off=off, dy_img=N, dy_off=off)
-            _grad(cp.weight).add_(dw9.t().reshape(D, 1, 3, 3))
-        dx, _ = ops.layernorm_bwd(dh, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias), dres=dx1, lp_dtype=None)
-        return (dx.view(B, N, D), None, None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 6)
+                              dg, db, x_img=N, x_off=off, dy_img=N, dy_off=off)
+            if gs.wants(cp.weight):
+                gs(cp.weight).add_(dw9.t().reshape(D, 1, 3, 3))
+        dx, _ = ops.layernorm_bwd(dh, x2, m1, r1, n1.weight, gs(n1.weight), gs(n1.bias), dres=dx1, lp_dtype=None)
+        return (dx.view(B, N, D), None, None, None, None, None) + gs.grads(ps)
 
 
 class ProcMlp(nn.Module):
@@ -375,12 +392,18 @@ class _ProcMlpFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, h, y = ctx.saved_tensors
         mod = ctx.mod
+        ps = list(mod.parameters())
+        gs = _sink(ctx, 2, ps)
+
+        def dst(w):   # dense_f32_bwd always writes dW: a scratch buffer for a frozen weight
+            d = gs(w)
+            return d if d is not None else torch.zeros_like(w)
         dy = dy.contiguous().float()
-        dh = ops.dense_f32_bwd(dy, y, h, mod.fc2.weight.detach(), _grad(mod.fc2.weight), _grad(mod.fc2.bias),
+        dh = ops.dense_f32_bwd(dy, y, h, mod.fc2.weight.detach(), dst(mod.fc2.weight), gs(mod.fc2.bias),
                                ops.ACT_RELU)
-        dx = ops.dense_f32_bwd(dh, h, x, mod.fc1.weight.detach(), _grad(mod.fc1.weight), _grad(mod.fc1.bias),
+        dx = ops.dense_f32_bwd(dh, h, x, mod.fc1.weight.detach(), dst(mod.fc1.weight), gs(mod.fc1.bias),
                                ops.ACT_RELU, want_dx=ctx.needs_input_grad[0])
-        return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+        return (dx, None) + gs.grads(ps)
 
 
 class _CvTHeadFn(torch.autograd.Function):
@@ -397,9 +420,11 @@ class _CvTHeadFn(torch.autograd.Function):
     def backward(ctx, dlogits):
         (y,) = ctx.saved_tensors
         head = ctx.head
-        dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), _grad(head.weight),
-                          _grad(head.bias) if head.bias is not None else None)
-        return dy, None, None, None
+        gs = _sink(ctx, 2, (head.weight, head.bias))
+        dw = gs(head.weight)
+        dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), dw if dw is not None else torch.zeros_like(head.weight),
+                          gs(head.bias))
+        return (dy, None) + gs.grads((head.weight, head.bias))
 
 
 # ======================================================================= stages + model

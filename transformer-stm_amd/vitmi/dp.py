@@ -16,9 +16,9 @@ cross-replica mean of every gradient once per step.  MI355X design:
   the backward finishes them (head, norm, block L-1 ... block 0, patch-embed), so
   fixed-size buckets (default 64 MiB: few, large collectives suit per-link-bound
   xGMI rings) become ready front to back;
-* each block's backward calls its ``_grad_ready_hook`` when its grads are final;
-  every bucket wholly inside the finished prefix is all-reduced at once, overlapping the
-  rest of the backward;
+* a post-accumulate-grad hook on every parameter (torch's own signal that ``.grad`` is final,
+  the one DistributedDataParallel's reducer uses) advances the finished prefix of the arena;
+  every bucket wholly inside it is all-reduced at once, overlapping the rest of the backward;
 * ``grad_dtype="bf16"`` halves the bytes on the wire (ViT-L: 1.2 GB -> 607 MB per step):
   each bucket is cast to bf16 on the side stream, averaged, and cast back into the fp32
   arena (rounding each gradient to bf16 once, plus RCCL's bf16 partial sums);
@@ -44,16 +44,29 @@ REDUCE_SUM, REDUCE_AVG = 0, 1
 
 
 class VitmiComm:
-    """The library's RCCL communicator (one per process, bound to the current HIP device)."""
+    """The library's RCCL communicator (one per process, bound to the current HIP device).
+
+    Every call into the library's comm entry points holds ``self._lock`` (and the library holds
+    its own mutex around the communicator): the CommWatchdog thread's abort can never interleave
+    with the training thread's enqueue of an all-reduce on the same communicator."""
 
     def __init__(self, rank: int, world: int, uid: bytes):
-        from ._lib import check, lib
         if len(uid) != UID_BYTES:
             raise ValueError(f"vitmi comm: the RCCL id must be {UID_BYTES} bytes")
         self.rank, self.world = rank, world
+        self._lock = threading.Lock()
         self._uid = ctypes.create_string_buffer(uid, UID_BYTES)
-        check(lib().vitmi_comm_init(rank, world, self._uid), "comm_init")
+        self._init(rank, world)
         self._live = True
+
+    def _init(self, rank: int, world: int) -> None:
+        from ._lib import check, lib
+        check(lib().vitmi_comm_init(rank, world, self._uid), "comm_init")
+
+    def _call(self, name: str, *args) -> int:
+        from ._lib import lib
+        with self._lock:
+            return getattr(lib(), name)(*args)
 
     @staticmethod
     def unique_id() -> bytes:
@@ -68,22 +81,28 @@ class VitmiComm:
         return cls(rank, world, exchange_unique_id(rank, world, store, key))
 
     def allreduce_async(self, buf: torch.Tensor, side: "torch.cuda.Stream", ready=None, op: int = REDUCE_AVG) -> None:
-        from ._lib import check, lib
+        from ._lib import check
         assert buf.is_cuda and buf.is_contiguous() and buf.dtype in _DT
         dt = _DT[buf.dtype]
-        check(lib().vitmi_comm_allreduce_async(buf.data_ptr(), buf.numel(), dt, op, side.cuda_stream,
-                                               ready.cuda_event if ready is not None else None),
-              "comm_allreduce_async")
+        check(self._call("vitmi_comm_allreduce_async", buf.data_ptr(), buf.numel(), dt, op, side.cuda_stream,
+                         ready.cuda_event if ready is not None else None), "comm_allreduce_async")
 
     def broadcast(self, buf: torch.Tensor, root: int = 0) -> None:
-        from ._lib import check, lib
+        from ._lib import check
         dt = _F32 if buf.dtype == torch.float32 else _BF16
-        check(lib().vitmi_comm_broadcast(buf.data_ptr(), buf.numel(), dt, root,
-                                         torch.cuda.current_stream().cuda_stream), "comm_broadcast")
+        check(self._call("vitmi_comm_broadcast", buf.data_ptr(), buf.numel(), dt, root,
+                         torch.cuda.current_stream().cuda_stream), "comm_broadcast")
 
     def check(self) -> None:
-        from ._lib import check, lib
-        check(lib().vitmi_comm_check(), "comm_check")
+        from ._lib import check
+        check(self._call("vitmi_comm_check"), "comm_check")
+
+    def info(self) -> Tuple[int, int]:
+        """(rank, world) as the library's communicator holds them (vitmi_comm_info)."""
+        from ._lib import check
+        r, w = ctypes.c_int(-1), ctypes.c_int(0)
+        check(self._call("vitmi_comm_info", ctypes.byref(r), ctypes.byref(w)), "comm_info")
+        return r.value, w.value
 
     @property
     def live(self) -> bool:
@@ -98,10 +117,13 @@ class VitmiComm:
         return buf.value.decode()
 
     def destroy(self, abort: bool = False) -> None:
-        if self._live:
-            from ._lib import check, lib
+        from ._lib import check, lib
+        with self._lock:
+            if not self._live:
+                return
             self._live = False
-            check(lib().vitmi_comm_destroy(int(abort)), "comm_destroy")
+            rc = lib().vitmi_comm_destroy(int(abort))
+        check(rc, "comm_destroy")
 
 
 def exchange_unique_id(rank: int, world: int, store=None, key: str = "vitmi_comm_uid") -> bytes:
@@ -182,6 +204,43 @@ class CommWatchdog:
             time.sleep(self.poll_s)
 
 
+def plan_buckets(n: int, per: int, cuts: Optional[Sequence[int]] = None, solo_tail: int = 2) -> List[Tuple[int, int]]:
+    """Bucket bounds over a flat buffer of n elements, at most ``per`` elements each.
+
+    Without ``cuts``: fixed-size buckets.  With ``cuts`` (the offsets at which the backward's
+    finished prefix can end: one per block, head and embedding, in order), buckets end on cuts,
+    packed greedily up to ``per``, except that the last ``solo_tail`` segments get buckets of
+    their own.  A bucket's all-reduce can only start when the backward has passed its end, so
+    whatever the last bucket holds is exchanged after the backward, exposed: with the ViT-B
+    arena in 64 MiB fixed buckets that is 64 MiB launched at block 0's end plus 7.3 MiB at
+    finish(); with solo tail segments it is block 0's 28 MB, overlapped with the patch
+    embedding's backward, plus the embedding's 3 MB."""
+    if not cuts:
+        return [(s, min(n, s + per)) for s in range(0, n, per)]
+    cuts = sorted({c for c in cuts if 0 < c < n} | {n})
+    segs, prev = [], 0
+    for c in cuts:
+        segs.append((prev, c))
+        prev = c
+    tail = segs[len(segs) - solo_tail:] if solo_tail > 0 else []
+    head = segs[:len(segs) - len(tail)]
+    out: List[Tuple[int, int]] = []
+    start = 0
+    for a, b in head:
+        if b - start > per and a > start:           # close the bucket before this segment
+            out.append((start, a))
+            start = a
+        while b - start > per:                      # a segment larger than a bucket: split it
+            out.append((start, start + per))
+            start += per
+    if head and head[-1][1] > start:
+        out.append((start, head[-1][1]))
+    for a, b in tail:
+        for s0 in range(a, b, per):
+            out.append((s0, min(b, s0 + per)))
+    return out
+
+
 class GradReducer:
     """Bucketed, overlapped all-reduce (mean) over one flat gradient buffer.
 
@@ -191,7 +250,7 @@ class GradReducer:
 
     def __init__(self, flat_grad: torch.Tensor, bucket_mb: float = 64.0, group=None,
                  comm: Optional[VitmiComm] = None, grad_dtype: str = "fp32", reserve_cus: int = 0,
-                 timeout_s: float = 600.0):
+                 timeout_s: float = 600.0, cuts: Optional[Sequence[int]] = None):
         self.flat = flat_grad
         self.group = group
         self.comm = comm
@@ -209,18 +268,25 @@ class GradReducer:
         self.reserve_cus = int(reserve_cus)
         n = flat_grad.numel()
         per = max(64, int(bucket_mb * (1 << 20) / flat_grad.element_size()) // 64 * 64)
-        self.bounds: List[Tuple[int, int]] = [(s, min(n, s + per)) for s in range(0, n, per)]
+        self.bounds: List[Tuple[int, int]] = plan_buckets(n, per, cuts)
         self._next = 0
         self._ready = 0
         self._handles: list = []
         self._active = comm is not None or self.world > 1
-        self._side = torch.cuda.Stream(device=flat_grad.device) if comm is not None else None
+        self._side = torch.cuda.Stream(device=flat_grad.device) if comm is not None and flat_grad.is_cuda else None
         self._lp = (torch.empty(n, dtype=torch.bfloat16, device=flat_grad.device)
                     if comm is not None and grad_dtype == "bf16" else None)
         self._prev_reserve: Optional[int] = None
         self.launch_log: List[Tuple[int, int]] = []   # (ready prefix, bucket index) for tests
-        self.watchdog = (CommWatchdog(timeout_s, self.abort)
+        self.readiness: Optional["ArenaReadiness"] = None   # set by attach()
+        # the watchdog thread only aborts the communicator (whose entry points are locked); the CU
+        # reservation is a training-thread global, restored by finish()/start()/abort()
+        self.watchdog = (CommWatchdog(timeout_s, self._abort_comm)
                          if comm is not None and timeout_s and timeout_s > 0 else None)
+        # the step's tail: the buckets launched by the last readiness event of the backward (the
+        # embedding's parameters) and by finish(): exchanged after the backward's compute
+        self.tail_launched: List[int] = []
+        self._burst: List[int] = []
 
     def _restore_reserve(self) -> None:
         if self._prev_reserve is not None:
@@ -228,12 +294,17 @@ class GradReducer:
             lib().vitmi_gemm_set_reserved_cus(self._prev_reserve)
             self._prev_reserve = None
 
-    def abort(self) -> None:
-        """Tear down after a failure: give the persistent GEMM its CUs back and abort the RCCL
-        communicator without waiting for peers (vitmi_comm_destroy(1) -> ncclCommAbort)."""
-        self._restore_reserve()
+    def _abort_comm(self) -> None:
+        """Abort the RCCL communicator without waiting for peers (vitmi_comm_destroy(1) ->
+        ncclCommAbort), so its stuck kernels exit.  Safe from the watchdog thread."""
         if self.comm is not None and self.comm.live:
             self.comm.destroy(abort=True)
+
+    def abort(self) -> None:
+        """Tear down after a failure (training thread): give the persistent GEMM its CUs back and
+        abort the communicator."""
+        self._restore_reserve()
+        self._abort_comm()
 
     def close(self) -> None:
         if self.watchdog is not None:
@@ -242,9 +313,16 @@ class GradReducer:
     def start(self) -> None:
         """Call before the backward of every step."""
         if self.watchdog is not None:
-            self.watchdog.check()
+            try:
+                self.watchdog.check()
+            except RuntimeError:
+                self._restore_reserve()
+                raise
         self._next, self._ready, self._handles = 0, 0, []
+        self._burst = []
         self.launch_log = []
+        if self.readiness is not None:
+            self.readiness.reset()
         if self._active and self.reserve_cus > 0 and self._prev_reserve is None:
             from ._lib import lib
             self._prev_reserve = lib().vitmi_gemm_set_reserved_cus(self.reserve_cus)
@@ -252,7 +330,9 @@ class GradReducer:
     def _launch(self) -> None:
         s, e = self.bounds[self._next]
         buf = self.flat[s:e]
-        if self.comm is not None:
+        if self.comm is not None and self._side is None:
+            self.comm.allreduce_async(buf, None, None, REDUCE_AVG)      # a host-side comm (tests)
+        elif self.comm is not None:
             ready = torch.cuda.Event()
             ready.record(torch.cuda.current_stream(buf.device))
             if self._lp is None:
@@ -277,8 +357,12 @@ class GradReducer:
         if not self._active:
             return
         self._ready = max(self._ready, end)
+        burst = []
         while self._next < len(self.bounds) and self.bounds[self._next][1] <= self._ready:
+            burst.append(self._next)
             self._launch()
+        if burst:
+            self._burst = burst
 
     def finish(self) -> None:
         if not self._active:
@@ -286,9 +370,11 @@ class GradReducer:
         try:
             if self.watchdog is not None:
                 self.watchdog.check()
+            rest = list(range(self._next, len(self.bounds)))
+            self.tail_launched = (self._burst if self._ready >= self.flat.numel() else []) + rest
             while self._next < len(self.bounds):
                 self._launch()
-            if self.comm is not None:
+            if self._side is not None:
                 # the optimizer (on the compute stream) runs after every bucket's exchange
                 torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
                 if self.watchdog is not None:
@@ -372,27 +458,125 @@ def broadcast_module(model: torch.nn.Module, src: int = 0, group=None, comm: Opt
                 dist.broadcast(t.data, src, group=group)
 
 
+class ArenaReadiness:
+    """Tracks which parameters of a ParamArena hold their final gradient in this backward and
+    feeds the finished prefix (arena order = backward order) to the reducer.
+
+    One ``register_post_accumulate_grad_hook`` per parameter fires once AccumulateGrad has
+    written ``.grad`` (after the Function that produced it, and after every other Function
+    contributing to that parameter).  If ``.grad`` is not the parameter's arena view (a gradient
+    accumulated into a tensor of its own), the hook copies it into the view and rebinds it, so
+    the bucket that all-reduces the flat buffer sees it.  Frozen parameters count as done."""
+
+    def __init__(self, arena, red: GradReducer):
+        self.arena, self.red = arena, red
+        ps = arena.params
+        self.index = {id(p): i for i, p in enumerate(ps)}
+        self.starts = [arena.offsets[id(p)] for p in ps] + [arena.numel]
+        self.done = [False] * len(ps)
+        self.k = 0
+        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in ps]
+
+    def reset(self) -> None:
+        self.done = [not p.requires_grad for p in self.arena.params]
+        self.k = 0
+        self._advance()
+
+    def _hook(self, p: torch.Tensor) -> None:
+        i = self.index[id(p)]
+        v = self.arena.view(self.arena.grad, p)
+        if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+            with torch.no_grad():
+                v.copy_(p.grad)
+            p.grad = v
+        self.done[i] = True
+        self._advance()
+
+    def _advance(self) -> None:
+        k, n = self.k, len(self.done)
+        while k < n and self.done[k]:
+            k += 1
+        if k != self.k:
+            self.k = k
+            self.red.mark_ready(self.starts[k])
+
+    def remove(self) -> None:
+        for h in self.handles:
+            h.remove()
+        self.handles = []
+
+
 def attach(model, bucket_mb: float = 64.0, group=None, comm: Optional[VitmiComm] = None,
            grad_dtype: str = "fp32", reserve_cus: int = 0, timeout_s: float = 600.0) -> GradReducer:
-    """Wire a GradReducer to a vitmi VisionTransformer's arena and backward hooks."""
+    """Wire a GradReducer to a vitmi VisionTransformer's arena: buckets launch from the
+    parameters' post-accumulate-grad hooks (ArenaReadiness) as the backward finishes them."""
     arena = model.arena()
+
+    def end_of(params) -> int:
+        return max(arena.offsets[id(p)] + p.numel() for p in params) if params else 0
+
+    # bucket ends on the prefixes the backward finishes (head, each block, the embedding)
+    cuts = [end_of(list(model.head.parameters()) + list(model.norm.parameters()))]
+    cuts += [end_of(list(blk.parameters())) for blk in reversed(model.blocks)]
+    cuts += [arena.numel]
     red = GradReducer(arena.grad, bucket_mb, group, comm=comm, grad_dtype=grad_dtype, reserve_cus=reserve_cus,
-                      timeout_s=timeout_s)
-
-    def end_of(params: Sequence[torch.nn.Parameter]) -> int:
-        return max(arena.offsets[id(p)] + p.numel() for p in params)
-
-    head_end = end_of(list(model.head.parameters()) + list(model.norm.parameters()))
-    object.__setattr__(model, "_head_ready_hook", lambda: red.mark_ready(head_end))
-    for blk in model.blocks:
-        e = end_of(list(blk.parameters()))
-        object.__setattr__(blk, "_grad_ready_hook", _hook(red, e))
-    object.__setattr__(model.patch_embed, "_grad_ready_hook", _hook(red, arena.numel))
+                      timeout_s=timeout_s, cuts=cuts)
+    red.readiness = ArenaReadiness(arena, red)
     return red
 
 
-def _hook(red: GradReducer, end: int) -> Callable:
-    return lambda _mod: red.mark_ready(end)
+def param_checksum(flat: torch.Tensor) -> Tuple[float, int]:
+    """(fp64 sum, exact bit checksum) of a flat fp32 buffer.  The bit checksum is
+    sum_i bits_i * (i mod 65521 + 1) over the int32 bit patterns in wrapping int64 arithmetic:
+    independent of the summation order, so equal on two replicas exactly when (barring a
+    collision) their bytes are."""
+    with torch.no_grad():
+        f = flat.detach().reshape(-1)
+        s64 = float(f.double().sum().item())
+        bits = f.view(torch.int32).to(torch.int64)
+        w = torch.arange(bits.numel(), device=f.device, dtype=torch.int64).remainder_(65521).add_(1)
+        exact = int(bits.mul_(w).sum().item())
+    return s64, exact
+
+
+def replica_report(flat: torch.Tensor, group=None) -> dict:
+    """Whether every rank holds the same parameters after the timed steps: MAX and MIN over the
+    ranks of the checksums must agree (synchronous data parallelism keeps the replicas
+    bit-identical, as MirroredStrategy does: old_codes/BayConvT(Par)(Muti).py:16-19)."""
+    s64, exact = param_checksum(flat)
+    out = {"param_checksum_fp64": s64, "param_checksum_bits": exact}
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        out["replicas_identical"] = True
+        return out
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    vals = {}
+    for name, v, dt in (("bits", exact, torch.int64), ("fp64", s64, torch.float64)):
+        mx = torch.tensor([v], dtype=dt, device=dev)
+        mn = mx.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
+        vals[name] = (mx.item(), mn.item())
+    out["replicas_identical"] = all(a == b for a, b in vals.values())
+    out["param_checksum_fp64_minmax"] = list(vals["fp64"])
+    return out
+
+
+def comm_report(red: GradReducer) -> dict:
+    """The exchange the reducer ran: communicator ranks and library (asked of the communicator
+    itself), the bucket plan and the tail the last finish() launched after the backward."""
+    es = red.flat.element_size()
+    mib = [(e - s) * es / 2 ** 20 for s, e in red.bounds]
+    out = {"buckets_mib": [round(m, 2) for m in mib], "bucket_count": len(mib),
+           "tail_buckets": list(red.tail_launched),
+           "tail_bucket_mib": round(sum(mib[i] for i in red.tail_launched), 2),
+           "grad_dtype": red.grad_dtype, "reserve_cus": red.reserve_cus}
+    if red.comm is not None:
+        rank, world = red.comm.info()
+        out.update(backend="vitmi RCCL communicator", ranks=world, rank=rank, library=type(red.comm).library())
+    else:
+        out.update(backend=f"torch.distributed {red.backend}", ranks=red.world,
+                   library=f"ProcessGroup {red.backend}" if red.backend else None)
+    return out
 
 
 def broadcast_parameters(model, src: int = 0, group=None, comm: Optional[VitmiComm] = None) -> None:

@@ -16,9 +16,11 @@ Every forward and backward runs the hand-written gfx950 kernels of libvitmi.so
 through fused ``torch.autograd.Function``s (one per block: LN1 -> QKV -> attention
 -> out-proj + residual -> LN2 -> fc1 + GELU -> fc2 + residual).  Parameters are
 ordinary fp32 ``nn.Parameter``s, so ``torch.optim``, ``state_dict`` and the DP
-reducer work unchanged.  Parameter gradients are accumulated (+=) by the kernels
-directly into ``param.grad`` (fp32); the autograd Functions return ``None`` for
-parameters.  In ``bf16`` mode GEMM/attention operands are bf16 (fp32 accumulate,
+reducer work unchanged.  The Functions RETURN their parameters' gradients to autograd
+(``vitmi/grads.py``: the kernels accumulate each into its final buffer, for a model with a
+ParamArena the arena view that AccumulateGrad then keeps as ``.grad``), so parameter hooks,
+DistributedDataParallel and ``torch.autograd.grad`` see them, and frozen parameters get
+none.  In ``bf16`` mode GEMM/attention operands are bf16 (fp32 accumulate,
 fp32 residual stream, LN statistics, softmax and head); in ``fp32`` mode every
 product is exact fp32 (f32-input MFMA).
 """
@@ -32,6 +34,7 @@ import torch.nn as nn
 
 from . import ops
 from .config import ViTConfig
+from .grads import GradSink
 
 Tensor = torch.Tensor
 F32 = torch.float32
@@ -43,15 +46,6 @@ F32 = torch.float32
 # and it is used only while the tensor is unmodified: autograd may accumulate another gradient
 # into it in place, which bumps its version counter.
 _LP_ATTR = "_vitmi_lp"
-# bf16 weight gradients from token-contiguous operand copies (ops.layernorm_fwd_t / _bwd_t ->
-# ops.linear_wgrad_xt / _dyt) with VITMI_WGRAD_T=1.  Off by default: the GEMMs gain what
-# tools/wgrad_layout.py predicts (-1.1 ms per step) but writing the transposed copies from the
-# LayerNorm kernels costs as much
-WGRAD_T = os.environ.get("VITMI_WGRAD_T", "0") == "1"
-# bf16 with VITMI_RES_IN_LN=1: the out-projection stores a bf16 output and the LayerNorm after it
-# adds the residual (ops.layernorm_fwd_res).  Off by default: the GEMM saves what the LayerNorm
-# then spends (proj 105 -> 71 us, LN2 40 -> 74 us per layer)
-RES_IN_LN = os.environ.get("VITMI_RES_IN_LN", "0") == "1"
 LP_STATS = {"hit": 0, "miss": 0}     # test hook: how often the handed-over copy was used
 
 
@@ -67,10 +61,10 @@ def _drop_args(mod: nn.Module, rate: float, site0: int):
     return (int(seed), float(rate), site0)
 
 
-def _grad(p: nn.Parameter) -> Tensor:
-    if p.grad is None:
-        p.grad = torch.zeros_like(p)
-    return p.grad
+def _sink(ctx, first: int, params, arena=None, extra=()) -> GradSink:
+    """GradSink over the Function inputs ``params`` starting at input index ``first`` (plus
+    ``extra`` (index, param) pairs)."""
+    return GradSink(ctx, [(first + i, q) for i, q in enumerate(params)] + list(extra), arena)
 
 
 def _lp(mod: nn.Module, p: Tensor, T: torch.dtype) -> Tensor:
@@ -89,32 +83,30 @@ def _take_lp(g: Tensor, T: torch.dtype, src: Optional[Tensor] = None) -> Tensor:
     current, otherwise ``g`` is cast."""
     if T == F32:
         return g
-    return _take_lp2(g, T, src)[0]
-
-
-def _take_lp2(g: Tensor, T: torch.dtype, src: Optional[Tensor] = None):
-    """(``g`` in the compute dtype, its transposed copy [D, rows] or None): as ``_take_lp``, plus
-    the token-contiguous copy a LayerNorm backward may have handed over with it (the operand of
-    ``ops.linear_wgrad_dyt``)."""
-    if T == F32:
-        return g, None
     src = g if src is None else src
     ent = src.__dict__.pop(_LP_ATTR, None)
     if ent is not None:
-        lp, version, ptr, lpt = ent
+        lp, version, ptr = ent
         if src._version == version and src.data_ptr() == ptr and lp.numel() == g.numel() and lp.dtype == T:
             LP_STATS["hit"] += 1
-            return lp.view(g.shape), lpt
+            return lp.view(g.shape)
     LP_STATS["miss"] += 1
-    return ops.cast_bf16(g.contiguous()), None
+    return ops.cast_bf16(g.contiguous())
 
 
-def _handover(g: Tensor, lp: Optional[Tensor], lpt: Optional[Tensor] = None) -> Tensor:
-    """Attach the bf16 copy ``lp`` of ``g`` (and its transpose ``lpt``) to the tensor object a
-    backward returns."""
+def _handover(g: Tensor, lp: Optional[Tensor]) -> Tensor:
+    """Attach the bf16 copy ``lp`` of ``g`` to the tensor object a backward returns."""
     if lp is not None:
-        g.__dict__[_LP_ATTR] = (lp, g._version, g.data_ptr(), lpt)
+        g.__dict__[_LP_ATTR] = (lp, g._version, g.data_ptr())
     return g
+
+
+def _is_vitmi_node(x: Tensor) -> bool:
+    """x was produced by a vitmi Function: its backward consumes the handed-over bf16 copy of
+    the gradient.  (A leaf or a torch op would keep the tensor object, e.g. as a leaf's .grad,
+    and the copy with it: ADVICE r03.)"""
+    fn = x.grad_fn
+    return fn is not None and getattr(type(fn), "_forward_cls", None) in _HANDOVER_FNS
 
 
 def _check_cuda(x: Tensor):
@@ -150,9 +142,10 @@ class _LayerNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         xs, mean, rstd = ctx.saved_tensors
         mod = ctx.mod
-        dx, _ = ops.layernorm_bwd(dy.contiguous().float(), xs, mean, rstd, mod.weight,
-                                  _grad(mod.weight), _grad(mod.bias))
-        return dx.view(xs.shape), None, None, None
+        ps = (mod.weight, mod.bias)
+        gs = _sink(ctx, 2, ps, getattr(mod, "_arena", None))
+        dx, _ = ops.layernorm_bwd(dy.contiguous().float(), xs, mean, rstd, mod.weight, gs(mod.weight), gs(mod.bias))
+        return (dx.view(xs.shape), None) + gs.grads(ps)
 
 
 class Linear(nn.Linear):
@@ -177,13 +170,16 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         (xs,) = ctx.saved_tensors
         mod = ctx.mod
+        ps = (mod.weight, mod.bias)
+        gs = _sink(ctx, 2, ps, getattr(mod, "_arena", None))
         dy2 = dy.contiguous().float().view(-1, dy.shape[-1])
         x2 = xs.view(-1, xs.shape[-1])
-        dx = ops.linear_dgrad(dy2, mod.weight.detach(), F32)
-        ops.linear_wgrad(dy2, x2, _grad(mod.weight))
-        if mod.bias is not None:
-            ops.bias_grad(dy2, _grad(mod.bias))
-        return dx.view(xs.shape), None, None, None
+        dx = ops.linear_dgrad(dy2, mod.weight.detach(), F32).view(xs.shape) if ctx.needs_input_grad[0] else None
+        if gs.wants(mod.weight):
+            ops.linear_wgrad(dy2, x2, gs(mod.weight))
+        if gs.wants(mod.bias):
+            ops.bias_grad(dy2, gs(mod.bias))
+        return (dx, None) + gs.grads(ps)
 
 
 # ======================================================================= attention / MLP
@@ -230,17 +226,21 @@ class _AttentionFn(torch.autograd.Function):
     def backward(ctx, dy):
         xo, qkv, o, lse, wq, wo = ctx.saved_tensors
         mod, (B, N, D) = ctx.mod, ctx.shape
+        ps = mod._params()
+        gs = _sink(ctx, 2, ps, getattr(mod, "_arena", None))
         T = xo.dtype
         g = dy.contiguous().float().view(B * N, D)
         g_lp = _take_lp(g, T, dy)
         do = ops.linear_dgrad(g_lp, wo, T)
-        ops.linear_wgrad(g_lp, o, _grad(mod.proj.weight))
-        ops.bias_grad(g_lp, _grad(mod.proj.bias))
-        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, mod.num_heads, mod.scale,
-                                 bias_grad=_grad(mod.qkv.bias) if mod.qkv.bias is not None else None)
+        if gs.wants(mod.proj.weight):
+            ops.linear_wgrad(g_lp, o, gs(mod.proj.weight))
+        if gs.wants(mod.proj.bias):
+            ops.bias_grad(g_lp, gs(mod.proj.bias))
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, mod.num_heads, mod.scale, bias_grad=gs(mod.qkv.bias))
         dx = ops.linear_dgrad(dqkv, wq, F32)
-        ops.linear_wgrad(dqkv, xo, _grad(mod.qkv.weight))
-        return (dx.view(B, N, D), None) + (None,) * len(mod._params())
+        if gs.wants(mod.qkv.weight):
+            ops.linear_wgrad(dqkv, xo, gs(mod.qkv.weight))
+        return (dx.view(B, N, D), None) + gs.grads(ps)
 
 
 class Mlp(nn.Module):
@@ -275,15 +275,20 @@ class _MlpFn(torch.autograd.Function):
     def backward(ctx, dy):
         xo, a, u, w1, w2 = ctx.saved_tensors
         mod = ctx.mod
+        ps = (mod.fc1.weight, mod.fc1.bias, mod.fc2.weight, mod.fc2.bias)
+        gs = _sink(ctx, 2, ps, getattr(mod, "_arena", None))
         T = xo.dtype
         g = dy.contiguous().float().view(-1, dy.shape[-1])
         g_lp = _take_lp(g, T, dy)
-        du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mod.fc1.bias), aux_tiled=T != F32)
-        ops.linear_wgrad(g_lp, a, _grad(mod.fc2.weight))
-        ops.bias_grad(g_lp, _grad(mod.fc2.bias))
+        du = ops.linear_dgrad(g_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=gs(mod.fc1.bias), aux_tiled=T != F32)
+        if gs.wants(mod.fc2.weight):
+            ops.linear_wgrad(g_lp, a, gs(mod.fc2.weight))
+        if gs.wants(mod.fc2.bias):
+            ops.bias_grad(g_lp, gs(mod.fc2.bias))
         dx = ops.linear_dgrad(du, w1, F32)
-        ops.linear_wgrad(du, xo, _grad(mod.fc1.weight))
-        return (dx.view(ctx.shape), None, None, None, None, None)
+        if gs.wants(mod.fc1.weight):
+            ops.linear_wgrad(du, xo, gs(mod.fc1.weight))
+        return (dx.view(ctx.shape), None) + gs.grads(ps)
 
 
 # ======================================================================= block
@@ -312,20 +317,23 @@ class Block(nn.Module):
 
     def forward(self, x: Tensor, h: Optional[int] = None, w: Optional[int] = None) -> Tensor:
         _check_cuda(x)
-        return _BlockFn.apply(x, self, None, False, _drop_args(self, self.drop_rate, 0), False, *self.parameters())
+        return _BlockFn.apply(x, self, None, False, _drop_args(self, self.drop_rate, 0), _is_vitmi_node(x),
+                              *self.parameters())
 
 
 class _BlockFn(torch.autograd.Function):
-    """Fused block.  ``first``: the block fed by the patch embedding (its input gradient is
-    not needed in bf16).  ``prev_fc2_bias``: the fc2 bias of the block feeding this one; its grad is
-    colsum(d input), produced for free by this block's LN1 backward.  ``fc2_bias_done``: this
-    block's own fc2 bias grad was already accumulated by its consumer (next block or head).
-    ``drop``: (seed, rate, site0) -> training-mode dropout (models/CvT(Par).py:189,255,257) at
-    sites site0 (out-projection), site0+1 (GELU output), site0+2 (fc2), fused into the GEMM
-    epilogues; the backward regenerates the masks (vitmi_dropout_apply)."""
+    """Fused block.  ``handover``: the input was produced by a vitmi Function whose backward
+    takes the bf16 copy of the input gradient (the LN1 backward writes it beside the fp32
+    gradient).  ``prev_fc2_bias``: the fc2 bias of the block feeding this one; its gradient is
+    colsum(d input), produced for free by this block's LN1 backward and returned for that input.
+    ``fc2_bias_done``: this block's own fc2 bias gradient is supplied by its consumer (next block
+    or head).  ``drop``: (seed, rate, site0) -> training-mode dropout
+    (models/CvT(Par).py:189,255,257) at sites site0 (out-projection), site0+1 (GELU output),
+    site0+2 (fc2), fused into the GEMM epilogues; the backward regenerates the masks
+    (vitmi_dropout_apply)."""
 
     @staticmethod
-    def forward(ctx, x, blk, prev_fc2_bias, fc2_bias_done, drop, first, *params):
+    def forward(ctx, x, blk, prev_fc2_bias, fc2_bias_done, drop, handover, *params):
         T = ops.torch_dtype(blk.dtype)
         B, N, D = x.shape
         M = B * N
@@ -335,58 +343,40 @@ class _BlockFn(torch.autograd.Function):
         a_ = blk.attn
         wq, wo = _lp(blk, a_.qkv.weight, T), _lp(blk, a_.proj.weight, T)
         w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
-        # bf16: the LayerNorm outputs are also written transposed (token-contiguous); the
-        # backward's qkv / fc1 weight gradients read those instead of h1 / h2 (linear_wgrad_xt)
-        # (the GEMM reads the transposed copies k-major: the token count must be a multiple of 64)
-        xt = T != F32 and WGRAD_T and M % 64 == 0
-        if xt:
-            h1, m1, r1, h1s = ops.layernorm_fwd_t(x2, n1.weight, n1.bias, blk.eps)
-        else:
-            h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
-            h1s = h1
+        h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
         qkv = ops.linear_fwd(h1, wq, a_.qkv.bias, T)
         o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
         dr = [None, None, None]
         if drop is not None:
             seed, rate, site0 = drop
             dr = [(seed, site0 + j, rate) for j in range(3)]
-        if T != F32 and dr[0] is None and not xt and RES_IN_LN:
-            # bf16: the out-projection stores its output as bf16 and LN2 adds the residual
-            # (ops.layernorm_fwd_res) instead of an fp32 load + store in the GEMM epilogue
-            y = ops.linear_fwd(o, wo, a_.proj.bias, T)
-            x1, h2, m2, r2 = ops.layernorm_fwd_res(x2, y, n2.weight, n2.bias, blk.eps, T)
-            h2s = h2
-        else:
-            x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
-            if xt:
-                h2, m2, r2, h2s = ops.layernorm_fwd_t(x1, n2.weight, n2.bias, blk.eps)
-            else:
-                h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
-                h2s = h2
+        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
+        h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, T)
         # gelu' stays in the tile-native layout between fc1's epilogue and fc2's dgrad (bf16)
         act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1], aux_tiled=T != F32)
         out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])
-        ctx.save_for_backward(x2, h1s, m1, r1, qkv, o, lse, x1, h2s, m2, r2, u, act, wq, wo, w1, w2)
-        ctx.blk, ctx.shape, ctx.xt = blk, (B, N, D), xt
+        ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
+        ctx.blk, ctx.shape = blk, (B, N, D)
         ctx.prev_bias, ctx.bias_done, ctx.drop = prev_fc2_bias, fc2_bias_done, drop
-        ctx.first = first
+        ctx.handover = handover
         return out.view(B, N, D)
 
     @staticmethod
     def backward(ctx, dout):
-        # h1s / h2s: the LayerNorm outputs, transposed [D, M] when ctx.xt
-        (x2, h1s, m1, r1, qkv, o, lse, x1, h2s, m2, r2, u, act, wq, wo, w1, w2) = ctx.saved_tensors
+        (x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2) = ctx.saved_tensors
         blk, (B, N, D) = ctx.blk, ctx.shape
         M = B * N
-        T = h1s.dtype
+        T = h1.dtype
         lpT = None if T == F32 else T
         n1, n2 = blk.norm1, blk._norm2
         a_, mlp = blk.attn, blk.mlp
+        ps = list(blk.parameters())
+        prev = ctx.prev_bias
+        gs = _sink(ctx, 6, ps, getattr(blk, "_arena", None), extra=[(2, prev)] if prev is not None else [])
         g2 = dout.contiguous().float().view(M, D)
         drop = ctx.drop
-        g2_lpt = None
         if drop is None:
-            g2_lp, g2_lpt = _take_lp2(g2, T, dout)
+            g2_lp = _take_lp(g2, T, dout)
         else:
             # the fc2 branch was dropped: its dgrad/wgrad/bias see g2 * mask / (1 - p)
             dout.__dict__.pop(_LP_ATTR, None)
@@ -394,58 +384,42 @@ class _BlockFn(torch.autograd.Function):
             g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
         # MLP branch
         # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
-        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=_grad(mlp.fc1.bias), aux_tiled=T != F32)
-        if g2_lpt is not None:
-            ops.linear_wgrad_dyt(g2_lpt, act, _grad(mlp.fc2.weight))
-        else:
-            ops.linear_wgrad(g2_lp, act, _grad(mlp.fc2.weight))
-        if not ctx.bias_done:
-            ops.bias_grad(g2_lp, _grad(mlp.fc2.bias))
-        if ctx.xt:
-            ops.linear_wgrad_xt(du, h2s, _grad(mlp.fc1.weight))
-        else:
-            ops.linear_wgrad(du, h2s, _grad(mlp.fc1.weight))
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=gs(mlp.fc1.bias), aux_tiled=T != F32)
+        if gs.wants(mlp.fc2.weight):
+            ops.linear_wgrad(g2_lp, act, gs(mlp.fc2.weight))
+        if not ctx.bias_done and gs.wants(mlp.fc2.bias):
+            ops.bias_grad(g2_lp, gs(mlp.fc2.bias))
+        if gs.wants(mlp.fc1.weight):
+            ops.linear_wgrad(du, h2, gs(mlp.fc1.weight))
         dh2 = ops.linear_dgrad(du, w1, T)
         # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
         if drop is None:
-            dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias),
-                                            dres=g2, lp_dtype=lpT, dxsum=_grad(a_.proj.bias))
+            dx1, dx1_lp = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, gs(n2.weight), gs(n2.bias),
+                                            dres=g2, lp_dtype=lpT, dxsum=gs(a_.proj.bias))
             if dx1_lp is None:
                 dx1_lp = dx1
         else:
-            dx1, _ = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, _grad(n2.weight), _grad(n2.bias),
+            dx1, _ = ops.layernorm_bwd(dh2, x1, m2, r2, n2.weight, gs(n2.weight), gs(n2.bias),
                                        dres=g2, lp_dtype=None)
             dx1_lp = ops.dropout_apply(dx1, seed, site0, rate, T)
-            ops.bias_grad(dx1_lp, _grad(a_.proj.bias))
+            if gs.wants(a_.proj.bias):
+                ops.bias_grad(dx1_lp, gs(a_.proj.bias))
         # attention branch
         do = ops.linear_dgrad(dx1_lp, wo, T)
-        ops.linear_wgrad(dx1_lp, o, _grad(a_.proj.weight))
+        if gs.wants(a_.proj.weight):
+            ops.linear_wgrad(dx1_lp, o, gs(a_.proj.weight))
         # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
-        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale,
-                                 bias_grad=_grad(a_.qkv.bias) if a_.qkv.bias is not None else None)
-        if ctx.xt:
-            ops.linear_wgrad_xt(dqkv, h1s, _grad(a_.qkv.weight))
-        else:
-            ops.linear_wgrad(dqkv, h1s, _grad(a_.qkv.weight))
+        dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale, bias_grad=gs(a_.qkv.bias))
+        if gs.wants(a_.qkv.weight):
+            ops.linear_wgrad(dqkv, h1, gs(a_.qkv.weight))
         dh1 = ops.linear_dgrad(dqkv, wq, T)
-        prev = ctx.prev_bias
         # the bf16 copy of dx is for a consumer that takes it (the block below); the patch
         # embedding's backward reads dx in fp32
-        want_lp = drop is None and not ctx.first
-        dx_lpt = None
-        if want_lp and lpT is not None and WGRAD_T and M % 64 == 0:
-            # with its transpose: the fc2 weight gradient of the block below (linear_wgrad_dyt)
-            dx, dx_lp, dx_lpt = ops.layernorm_bwd_t(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
-                                                    dres=dx1, dxsum=_grad(prev) if prev is not None else None)
-        else:
-            dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, _grad(n1.weight), _grad(n1.bias),
-                                          dres=dx1, lp_dtype=lpT if want_lp else None,
-                                          dxsum=_grad(prev) if prev is not None else None)
-        hook = getattr(blk, "_grad_ready_hook", None)
-        if hook is not None:
-            hook(blk)
-        out = _handover(dx.view(B, N, D), dx_lp, dx_lpt)
-        return (out, None, None, None, None, None) + (None,) * (len(ctx.needs_input_grad) - 6)
+        want_lp = drop is None and ctx.handover
+        dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, gs(n1.weight), gs(n1.bias),
+                                      dres=dx1, lp_dtype=lpT if want_lp else None, dxsum=gs(prev))
+        out = _handover(dx.view(B, N, D), dx_lp)
+        return (out, None, gs.grads([prev])[0], None, None, None) + gs.grads(ps)
 
 
 # ======================================================================= embedding
@@ -501,68 +475,70 @@ class _EmbedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx):
         emb, cls, pos, (B, np_, D) = ctx.emb, ctx.cls, ctx.pos, ctx.dims
+        ps = list(emb.parameters())
+        gs = _sink(ctx, 4, ps, getattr(emb, "_arena", None), extra=[(2, cls), (3, pos)])
         saved = ctx.saved_tensors
         patches = saved[0]
         T = patches.dtype
         lpT = None if T == F32 else T
         dx = dx.contiguous()
-        dcls = _grad(cls).view(-1) if cls is not None else None
-        dpos = _grad(pos).view(-1) if pos is not None else None
+        dcls, dpos = gs(cls), gs(pos)
+        dcls = dcls.view(-1) if dcls is not None else None
+        dpos = dpos.view(-1) if dpos is not None else None
+        dw = gs(emb.proj.weight)
+        dw = dw.view(D, -1) if dw is not None else None
         if emb.norm is not None:
             conv, mean, rstd = saved[1:]
             dy, _ = ops.tokens_assemble_bwd(dx, B, np_, True, None, dcls, dpos)
             dconv, dconv_lp = ops.layernorm_bwd(dy, conv, mean, rstd, emb.norm.weight,
-                                                _grad(emb.norm.weight), _grad(emb.norm.bias), lp_dtype=lpT)
+                                                gs(emb.norm.weight), gs(emb.norm.bias), lp_dtype=lpT)
             g = dconv_lp if dconv_lp is not None else dconv
-            ops.linear_wgrad(g, patches, _grad(emb.proj.weight).view(D, -1))
-            ops.bias_grad(g, _grad(emb.proj.bias))
+            if dw is not None:
+                ops.linear_wgrad(g, patches, dw)
+            if gs.wants(emb.proj.bias):
+                ops.bias_grad(g, gs(emb.proj.bias))
         else:
             Bi, C, S, P = ctx.img_shape
-            ops.patch_embed_bwd(dx, patches, Bi, C, S, P, _grad(emb.proj.weight).view(D, -1),
-                                _grad(emb.proj.bias), dcls, dpos)
-        hook = getattr(emb, "_grad_ready_hook", None)
-        if hook is not None:
-            hook(emb)
-        n_params = len(ctx.needs_input_grad) - 4
-        return (None, None, None, None) + (None,) * n_params
+            ops.patch_embed_bwd(dx, patches, Bi, C, S, P, dw, gs(emb.proj.bias), dcls, dpos)
+        return (None, None, gs.grads([cls])[0], gs.grads([pos])[0]) + gs.grads(ps)
 
 
 # ======================================================================= head + loss
 class _HeadFn(torch.autograd.Function):
-    """LN(cls) -> Dense(num_classes)  (models/CvT(Par).py:326-329,350)."""
+    """LN(cls) -> Dense(num_classes)  (models/CvT(Par).py:326-329,350).  ``last_fc2_bias``: the
+    fc2 bias of the last block, whose gradient (colsum of the head's input gradient) the LN
+    backward forms here."""
 
     @staticmethod
-    def forward(ctx, x, model, *params):
+    def forward(ctx, x, model, last_fc2_bias, *params):
         norm, head = model.norm, model.head
         xc = x[:, 0]                                      # strided rows [B, D]
         y, mean, rstd = ops.layernorm_fwd(xc, norm.weight, norm.bias, norm.eps, F32)
         logits = ops.head_fwd(y, head.weight.detach(), head.bias)
         ctx.save_for_backward(x, y, mean, rstd)
-        ctx.model = model
+        ctx.model, ctx.last_bias = model, last_fc2_bias
+        ctx.handover = _is_vitmi_node(x)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         x, y, mean, rstd = ctx.saved_tensors
-        model = ctx.model
+        model, last = ctx.model, ctx.last_bias
         norm, head = model.norm, model.head
-        dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), _grad(head.weight),
-                          _grad(head.bias) if head.bias is not None else None)
+        ps = list(norm.parameters()) + list(head.parameters())
+        gs = _sink(ctx, 3, ps, model._arena, extra=[(2, last)] if last is not None else [])
+        dy = ops.head_bwd(dlogits.float(), y, head.weight.detach(), gs(head.weight), gs(head.bias))
         dx = torch.zeros_like(x)
-        last_fc2_bias = model.blocks[-1].mlp.fc2.bias if len(model.blocks) and model._fc2_bias_fused else None
         # the last block's GEMMs take dx in the compute dtype: its zero rows are a fill and the
         # cls rows come from the LN backward (no cast pass over dx)
         T = ops.torch_dtype(model.cfg.dtype)
-        lp = torch.zeros(x.shape[0] * x.shape[1], x.shape[2], dtype=T, device=x.device) if T != F32 else None
-        ops.layernorm_bwd(dy, x[:, 0], mean, rstd, norm.weight, _grad(norm.weight), _grad(norm.bias),
-                          dx=dx[:, 0], dxsum=_grad(last_fc2_bias) if last_fc2_bias is not None else None,
-                          lp_dtype=None if lp is None else T,
+        lp = (torch.zeros(x.shape[0] * x.shape[1], x.shape[2], dtype=T, device=x.device)
+              if T != F32 and ctx.handover else None)
+        ops.layernorm_bwd(dy, x[:, 0], mean, rstd, norm.weight, gs(norm.weight), gs(norm.bias),
+                          dx=dx[:, 0], dxsum=gs(last), lp_dtype=None if lp is None else T,
                           dx_lp=None if lp is None else lp.view(x.shape[0], x.shape[1], x.shape[2])[:, 0])
         _handover(dx, lp)
-        hook = getattr(model, "_head_ready_hook", None)
-        if hook is not None:
-            hook()
-        return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+        return (dx, None, gs.grads([last])[0]) + gs.grads(ps)
 
 
 class _LossFn(torch.autograd.Function):
@@ -576,6 +552,10 @@ class _LossFn(torch.autograd.Function):
     def backward(ctx, g):
         (dl,) = ctx.saved_tensors
         return dl * g, None, None
+
+
+# the Functions whose backward takes a handed-over bf16 copy of their output gradient
+_HANDOVER_FNS = (_BlockFn, _AttentionFn, _MlpFn)
 
 
 def cross_entropy(logits: Tensor, target: Tensor) -> Tensor:
@@ -610,6 +590,8 @@ class ParamArena:
         self.grad = torch.zeros(n, dtype=F32, device=device)
         self.flat_lp = torch.empty(n, dtype=torch.bfloat16, device=device) if want_lp else None
         self._lp_version: Optional[int] = None
+        self._ids = frozenset(id(p) for p in ordered)
+        self._fresh: set = set()   # parameters whose gradient view is zero and not handed out
         with torch.no_grad():
             for p, o in zip(ordered, offs):
                 self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
@@ -650,7 +632,30 @@ class ParamArena:
         """The fused optimizer wrote params and shadow through raw pointers (no version bump)."""
         self._lp_version = self._stamp()
 
+    def begin_step(self) -> None:
+        """A forward that will be differentiated: when no parameter holds a gradient (the
+        set_to_none convention of torch's zero_grad), zero the flat gradient buffer once and
+        offer every parameter's view as its backward destination (``take``); AccumulateGrad
+        then keeps that view as ``.grad``.  Otherwise (gradients being accumulated across
+        backwards) the Functions allocate fresh buffers that autograd adds into ``.grad``."""
+        if all(p.grad is None for p in self.params):
+            self.grad.zero_()
+            self._fresh = set(self._ids)
+        else:
+            self._fresh = set()
+
+    def take(self, p: Tensor) -> Optional[Tensor]:
+        """p's zeroed gradient view, once per ``begin_step``, while ``p.grad`` is None."""
+        if id(p) in self._fresh and p.grad is None:
+            self._fresh.discard(id(p))
+            return self.view(self.grad, p)
+        return None
+
     def bind_grads(self) -> None:
+        """Make every ``.grad`` the parameter's view of the flat gradient buffer (copying a
+        gradient that lives elsewhere; a missing one counts as zero): the fused optimizer and
+        the DP buckets read the flat buffer.  After a backward from ``begin_step`` this only
+        checks pointers."""
         ps, views = self.params, self._grad_views
         if all(p.grad is None for p in ps):
             self.grad.zero_()
@@ -739,13 +744,14 @@ class VisionTransformer(nn.Module):
         return self._arena
 
     # -- forward
-    def forward_features(self, x: Tensor) -> Tensor:
-        """Token stream after the last block, [B, N, D] fp32."""
+    def forward_features(self, x: Tensor, _head_takes_bias: bool = False) -> Tensor:
+        """Token stream after the last block, [B, N, D] fp32.  (``_head_takes_bias``: forward()'s
+        head forms the last block's fc2 bias gradient.)"""
         _check_cuda(x)
         arena = self.arena()
         arena.refresh_lp()
         if torch.is_grad_enabled():
-            arena.bind_grads()
+            arena.begin_step()
         pe = self.patch_embed
         t = _EmbedFn.apply(x, pe, self.cls_token, self.pos_embed, *pe.parameters())
         # bias-grad fusion: block i's LN1 backward produces colsum(d input) = the fc2 bias grad
@@ -753,15 +759,19 @@ class VisionTransformer(nn.Module):
         drop = _drop_args(self, self.cfg.drop_rate, 0)
         # with dropout the fc2/proj bias grads are column sums of MASKED gradients: no fusion
         self._fc2_bias_fused = drop is None
+        L = len(self.blocks)
         for i, blk in enumerate(self.blocks):
             prev_bias = self.blocks[i - 1].mlp.fc2.bias if i > 0 and drop is None else None
+            done = drop is None and (i < L - 1 or _head_takes_bias)
             d = None if drop is None else (drop[0], drop[1], 3 * i)
-            t = _BlockFn.apply(t, blk, prev_bias, drop is None, d, i == 0, *blk.parameters())
+            # block 0's input gradient goes to the patch embedding's backward, which reads fp32
+            t = _BlockFn.apply(t, blk, prev_bias, done, d, i > 0, *blk.parameters())
         return t
 
     def forward(self, x: Tensor) -> Tensor:
-        t = self.forward_features(x)
-        return _HeadFn.apply(t, self, *self.norm.parameters(), *self.head.parameters())
+        t = self.forward_features(x, _head_takes_bias=True)
+        last = self.blocks[-1].mlp.fc2.bias if len(self.blocks) and self._fc2_bias_fused else None
+        return _HeadFn.apply(t, self, last, *self.norm.parameters(), *self.head.parameters())
 
 
 def build_model(cfg: ViTConfig, device="cuda") -> VisionTransformer:

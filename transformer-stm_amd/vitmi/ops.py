@@ -175,24 +175,6 @@ def linear_wgrad(dy: Tensor, x: Tensor, dw: Tensor) -> None:
                                    _s()), "linear_wgrad")
 
 
-def linear_wgrad_xt(dy: Tensor, xt: Tensor, dw: Tensor) -> None:
-    """dW[N,K] (fp32) += dy[M,N]^T x with x given transposed, xt [K][>=M] (token-contiguous)."""
-    M, N = dy.shape
-    K = xt.shape[0]
-    ws = _ws(lib().vitmi_linear_wgrad_xt_workspace_size(dt(dy.dtype), M, N, K), dy)
-    check(lib().vitmi_linear_wgrad_xt(dt(dy.dtype), M, N, K, _p(dy), _p(xt), xt.stride(0), _p(dw), _p(ws),
-                                      ws.numel(), _s()), "linear_wgrad_xt")
-
-
-def linear_wgrad_dyt(dyt: Tensor, x: Tensor, dw: Tensor) -> None:
-    """dW[N,K] (fp32) += dy^T x with dy given transposed, dyt [N][>=M] (token-contiguous)."""
-    M, K = x.shape
-    N = dyt.shape[0]
-    ws = _ws(lib().vitmi_linear_wgrad_workspace_size(dt(x.dtype), M, N, K), x)
-    check(lib().vitmi_linear_wgrad_dyt(dt(x.dtype), M, N, K, _p(dyt), dyt.stride(0), _p(x), _p(dw), _p(ws),
-                                       ws.numel(), _s()), "linear_wgrad_dyt")
-
-
 def bias_grad(dy: Tensor, db: Tensor) -> None:
     """db[N] (fp32) += sum over rows of dy[..., N]."""
     M, ld = _rows(dy)
@@ -231,57 +213,6 @@ def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.
     return y, mean, rstd
 
 
-def layernorm_fwd_res(x: Tensor, yb: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.dtype):
-    """xo = x (fp32) + yb (bf16), y = LayerNorm(xo): returns (xo fp32 [M, D], y [M, D], mean, rstd)."""
-    assert x.dtype == torch.float32 and yb.dtype == torch.bfloat16
-    M, ldx = _rows(x)
-    _, ldyb = _rows(yb)
-    D = x.shape[-1]
-    xo = torch.empty(M, D, dtype=torch.float32, device=x.device)
-    y = torch.empty(M, D, dtype=out_dtype, device=x.device)
-    mean = torch.empty(M, dtype=torch.float32, device=x.device)
-    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
-    check(lib().vitmi_layernorm_fwd_res(M, D, _p(x), ldx, _p(yb), ldyb, _p(w), _p(b), float(eps), _p(xo), D,
-                                        _p(y), dt(out_dtype), D, _p(mean), _p(rstd), _s()), "layernorm_fwd_res")
-    return xo, y, mean, rstd
-
-
-def layernorm_fwd_t(x: Tensor, w: Tensor, b: Tensor, eps: float):
-    """layernorm_fwd to bf16 that also returns the output transposed: (y [M, D], mean, rstd,
-    yt [D, M]) -- yt is the token-contiguous operand of linear_wgrad_xt."""
-    assert x.dtype == torch.float32
-    M, ldx = _rows(x)
-    D = x.shape[-1]
-    y = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
-    ldt = (M + 7) // 8 * 8             # 16-B aligned rows; yt is the [D, M] view
-    yt = torch.empty(D, ldt, dtype=torch.bfloat16, device=x.device)
-    mean = torch.empty(M, dtype=torch.float32, device=x.device)
-    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
-    check(lib().vitmi_layernorm_fwd_t(M, D, _p(x), ldx, _p(w), _p(b), float(eps), _p(y), D, _p(yt), ldt,
-                                      _p(mean), _p(rstd), _s()), "layernorm_fwd_t")
-    return y, mean, rstd, yt[:, :M]
-
-
-def layernorm_bwd_t(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
-                    dgamma: Optional[Tensor], dbeta: Optional[Tensor], dres: Optional[Tensor] = None,
-                    dxsum: Optional[Tensor] = None):
-    """layernorm_bwd with the bf16 copy of dx also written transposed: (dx fp32, dx_lp bf16
-    [M, D], dxt bf16 [D, M])."""
-    M, ldy = _rows(dy)
-    _, ldx = _rows(x)
-    D = x.shape[-1]
-    dx = torch.empty(M, D, dtype=torch.float32, device=x.device)
-    dx_lp = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
-    ldt = (M + 7) // 8 * 8
-    dxt = torch.empty(D, ldt, dtype=torch.bfloat16, device=x.device)
-    ldres = _rows(dres)[1] if dres is not None else 0
-    ws = _ws(lib().vitmi_layernorm_bwd_workspace_size(M, D), x)
-    check(lib().vitmi_layernorm_bwd_t(M, D, _p(dy), dt(dy.dtype), ldy, _p(x), ldx, _p(mean), _p(rstd), _p(w),
-                                      _p(dres), ldres, _p(dx), D, _p(dx_lp), D, _p(dxt), ldt, _p(dgamma), _p(dbeta),
-                                      _p(dxsum), _p(ws), ws.numel(), _s()), "layernorm_bwd_t")
-    return dx, dx_lp, dxt[:, :M]
-
-
 def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
                   dgamma: Optional[Tensor], dbeta: Optional[Tensor], dres: Optional[Tensor] = None,
                   dx: Optional[Tensor] = None, lp_dtype: Optional[torch.dtype] = None,
@@ -313,9 +244,7 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
 
 # ---------------------------------------------------------------- attention
 def attention_set_policy(policy: int) -> int:
-    """0 = auto, 1 = always the streamed kernels, 2 = single-pass fused backward for N <= 256,
-    3 = auto with the two-key-blocks-per-wave dK/dV kernel (tests / A-B timing).  Returns the
-    previous policy."""
+    """0 = auto, 1 = always the streamed kernels (tests).  Returns the previous policy."""
     return lib().vitmi_attention_set_policy(int(policy))
 
 

@@ -64,12 +64,15 @@ class Adam:
     def lr(self, v: float) -> None:
         self.learning_rate = float(v)
 
-    def zero_grad(self) -> None:
-        if self._arena is not None:
-            self._arena.grad.zero_()
-            return
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """torch's convention: drop the gradients (the next forward of an arena model zeroes the
+        flat buffer once and the backward writes into it again), or zero them in place."""
         for p in self.params:
-            if p.grad is not None:
+            if p.grad is None:
+                continue
+            if set_to_none:
+                p.grad = None
+            else:
                 p.grad.zero_()
 
     @torch.no_grad()
@@ -81,9 +84,9 @@ class Adam:
             if arena is not self._arena:
                 raise RuntimeError("vitmi Adam: the model's parameter arena was rebuilt after the optimizer "
                                    "was created (model moved?); create the optimizer after placing the model")
-            for p in (self.params[0], self.params[-1]):     # bind_grads binds all or none
-                if p.grad is None or p.grad.data_ptr() != arena.view(arena.grad, p).data_ptr():
-                    raise RuntimeError("vitmi Adam: gradients are not bound to the arena (run a forward first)")
+            # the launch reads the flat gradient buffer: every .grad must be its arena view (they
+            # are after a backward from an arena forward; a gradient set elsewhere is copied in)
+            arena.bind_grads()
             lp = arena.flat_lp
             check(lib().vitmi_adam_step(arena.numel, ops._p(arena.flat), ops._p(arena.grad), ops._p(self._m),
                                         ops._p(self._v), ops._p(lp), alpha, self.beta_1, self.beta_2, self.epsilon,
