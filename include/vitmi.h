@@ -355,6 +355,20 @@ int vitmi_sls_preprocess(int n, int H, int W, const void* src, int64_t img_bytes
 int vitmi_gather_rows(int64_t n, int64_t row_bytes, const void* src, int64_t n_src, const int64_t* idx, void* dst,
                       vitmi_stream_t stream);
 
+/* Split-bf16 operands of the precision knob (ViTConfig dtype "bf16x3"; csrc/split.hip).  The reference
+ * computes in fp32 (models/CvT(Par).py, Keras floatx); an operand carried as x = hi + lo, hi = bf16(x),
+ * lo = bf16(x - hi), makes a bf16 MFMA product good to ~2^-16: hi.hi + hi.lo + lo.hi, computed by the
+ * GEMMs above unchanged as ONE product over K' = 3K with the A rows laid out [hi | hi | lo] (pattern 0)
+ * and the weight rows [hi | lo | hi] (pattern 1).
+ *   vitmi_split_bf16x3: src fp32 [rows][ld_src] (K % 4 == 0) -> dst bf16 [rows][ld_dst >= 3K];
+ *     hi_copy (optional, bf16 [rows][ld_copy]) receives hi alone (the bf16 operand of the backward).
+ *   vitmi_gelu_split_bf16x3: act3 = split(gelu(u)) pattern 0, dgelu = gelu'(u) in bf16 (row-major, the
+ *     aux of a DGELU dgrad); u fp32 [rows][N] (the fc1 pre-activation, models/CvT(Par).py:254). */
+int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
+                       int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
+int vitmi_gelu_split_bf16x3(int64_t rows, int64_t N, const float* u, void* act3, int64_t ld_act3, void* dgelu,
+                            int64_t ld_dgelu, vitmi_stream_t stream);
+
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);
 /* bf16 -> fp32 cast of n elements (the bf16 gradient all-reduce writes back into the fp32 arena) */

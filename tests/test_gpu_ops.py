@@ -460,3 +460,48 @@ def test_cast():
 
 
 
+
+
+@pytest.mark.parametrize("rows,K", [(197 * 3, 768), (37, 3072), (5, 4)])
+def test_split_bf16x3_layout_and_residual(rows, K):
+    """vitmi_split_bf16x3: hi = bf16(x), lo = bf16(x - hi) in the [hi | hi | lo] / [hi | lo | hi]
+    layouts (row-strided source), hi + lo within 2^-16 of x, and the optional hi copy."""
+    x = (rnd(rows, K + 8, seed=91) * 3).to(DEV)[:, 4:4 + K]
+    x = x.contiguous() if (x.data_ptr() % 16) else x
+    a3, hi = ops.split_bf16x3(x, 0, hi_copy=True)
+    w3, none = ops.split_bf16x3(x, 1)
+    assert none is None
+    h = x.to(BF)
+    lo = (x - h.float()).to(BF)
+    assert torch.equal(a3[:, :K], h) and torch.equal(a3[:, K:2 * K], h) and torch.equal(a3[:, 2 * K:], lo)
+    assert torch.equal(w3[:, :K], h) and torch.equal(w3[:, K:2 * K], lo) and torch.equal(w3[:, 2 * K:], h)
+    assert torch.equal(hi, h)
+    assert ((h.float() + lo.float() - x).abs() <= x.abs() * 2.0 ** -16 + 1e-30).all()
+
+
+def test_bf16x3_gemm_is_fp32_accurate():
+    """One GEMM over K' = 3K of the split operands (hi.hi + hi.lo + lo.hi) against an fp64
+    product: ~2^-16 relative, where the plain bf16 GEMM is ~2^-9."""
+    M, N, K = 197 * 4, 768, 768
+    x = rnd(M, K, seed=92).to(DEV)
+    w = (rnd(N, K, seed=93) * 0.05).to(DEV)
+    exact = x.double() @ w.double().t()
+    x3, _ = ops.split_bf16x3(x, 0)
+    w3, _ = ops.split_bf16x3(w, 1)
+    y3 = ops.linear_fwd(x3, w3, None, torch.float32)
+    y1 = ops.linear_fwd(x.to(BF), w.to(BF), None, torch.float32)
+    e3 = ((y3.double() - exact).norm() / exact.norm()).item()
+    e1 = ((y1.double() - exact).norm() / exact.norm()).item()
+    assert e3 < 3e-5 and e1 > 20 * e3, (e3, e1)
+
+
+def test_gelu_split_bf16x3():
+    u = (rnd(197 * 2, 3072, seed=94) * 3).to(DEV)
+    act3, dg = ops.gelu_split_bf16x3(u)
+    ref = torch.nn.functional.gelu(u.double())
+    got = act3[:, :3072].double() + act3[:, 6144:].double()
+    assert torch.equal(act3[:, :3072], act3[:, 3072:6144])
+    assert ((got - ref).abs() <= ref.abs() * 2e-5 + 1e-6).all()
+    t = u.double()
+    dref = 0.5 * (1 + torch.erf(t / 2 ** 0.5)) + t * torch.exp(-0.5 * t * t) / (2 * torch.pi) ** 0.5
+    assert ((dg.double() - dref).abs() <= dref.abs() * 8e-3 + 1e-3).all()

@@ -47,7 +47,10 @@ class ViTConfig:
     # Keras default 0.1, training mode only).  0 = the parity / benchmark configuration.
     drop_rate: float = 0.0
     # compute dtype of the device path: 'bf16' (MFMA bf16, fp32 accumulate and
-    # fp32 residual stream) or 'fp32' (f32-input MFMA, exact fp32 products)
+    # fp32 residual stream), 'bf16x3' (the precision knob: as bf16, with the forward GEMMs'
+    # weights, LayerNorm outputs, attention output and GELU output carried as split hi + lo
+    # bf16 pairs and the attention forward in fp32; logits within 1e-3 of the fp32 reference)
+    # or 'fp32' (f32-input MFMA, exact fp32 products)
     dtype: str = "bf16"
 
     @property

@@ -343,6 +343,13 @@ class _BlockFn(torch.autograd.Function):
         a_ = blk.attn
         wq, wo = _lp(blk, a_.qkv.weight, T), _lp(blk, a_.proj.weight, T)
         w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
+        ctx.blk, ctx.shape = blk, (B, N, D)
+        ctx.prev_bias, ctx.bias_done, ctx.drop = prev_fc2_bias, fc2_bias_done, drop
+        ctx.handover = handover
+        ctx.aux_tiled = T != F32
+        if blk.dtype == "bf16x3":
+            out = _BlockFn._forward_x3(ctx, x2, blk, B, N, D, H, drop, (wq, wo, w1, w2))
+            return out.view(B, N, D)
         h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
         qkv = ops.linear_fwd(h1, wq, a_.qkv.bias, T)
         o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
@@ -356,10 +363,51 @@ class _BlockFn(torch.autograd.Function):
         act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1], aux_tiled=T != F32)
         out = ops.linear_fwd(act, w2, blk.mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, dropout=dr[2])
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2)
-        ctx.blk, ctx.shape = blk, (B, N, D)
-        ctx.prev_bias, ctx.bias_done, ctx.drop = prev_fc2_bias, fc2_bias_done, drop
-        ctx.handover = handover
         return out.view(B, N, D)
+
+    @staticmethod
+    def _forward_x3(ctx, x2, blk, B, N, D, H, drop, wlp):
+        """The precision knob's forward (ViTConfig dtype 'bf16x3'; tools/precision_emulate.py):
+        the qkv, out-projection, fc1 and fc2 GEMMs take split-bf16 operands (weights and the
+        LayerNorm / attention / GELU outputs as hi + lo, one GEMM over K' = 3K, vitmi_split_bf16x3)
+        and the attention forward runs in fp32 (f32 MFMA).  The backward is the bf16 one, on the
+        hi parts (row-strided views of the split operands), a bf16 copy of qkv and the bf16
+        attention forward's O and lse."""
+        if drop is not None:
+            raise ValueError("vitmi: dtype 'bf16x3' is the parity / evaluation knob; dropout is not supported")
+        n1, n2 = blk.norm1, blk._norm2
+        a_, mlp = blk.attn, blk.mlp
+
+        def w3(p):
+            return ops.split_bf16x3(p.detach(), 1)[0]
+        h1f, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, F32)
+        h1_3, _ = ops.split_bf16x3(h1f, 0)
+        del h1f
+        qkvf = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, F32)
+        of, _ = ops.attention_fwd(qkvf, B, N, H, a_.scale)
+        qkv = ops.cast_bf16(qkvf)
+        del qkvf
+        o3, _ = ops.split_bf16x3(of, 0)
+        del of
+        # the bf16 backward recomputes P from the bf16 q, k: its lse (and the O of delta =
+        # rowsum(dO o O)) must come from the bf16 forward of the same q, k, v, or P's rows would not
+        # sum to 1 and dS would carry a bias (C1 grads 1.7e-2 with the fp32 forward's lse)
+        o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
+        x1 = ops.linear_fwd(o3, w3(a_.proj.weight), a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2)
+        del o3
+        h2f, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, F32)
+        h2_3, _ = ops.split_bf16x3(h2f, 0)
+        del h2f
+        u = ops.linear_fwd(h2_3, w3(mlp.fc1.weight), mlp.fc1.bias, F32)
+        act3, dg = ops.gelu_split_bf16x3(u)
+        del u
+        out = ops.linear_fwd(act3, w3(mlp.fc2.weight), mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
+        # the bf16 backward's operands: hi parts of the split activations (row-strided views),
+        # gelu' row-major (not the tile-native layout of the fused GELU epilogue)
+        h1, h2, act = h1_3[:, :D], h2_3[:, :D], act3[:, :mlp.fc1.weight.shape[0]]
+        ctx.aux_tiled = False
+        ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dg, act, *wlp)
+        return out
 
     @staticmethod
     def backward(ctx, dout):
@@ -384,7 +432,7 @@ class _BlockFn(torch.autograd.Function):
             g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
         # MLP branch
         # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
-        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=gs(mlp.fc1.bias), aux_tiled=T != F32)
+        du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=gs(mlp.fc1.bias), aux_tiled=ctx.aux_tiled)
         if gs.wants(mlp.fc2.weight):
             ops.linear_wgrad(g2_lp, act, gs(mlp.fc2.weight))
         if not ctx.bias_done and gs.wants(mlp.fc2.bias):
@@ -457,7 +505,17 @@ class _EmbedFn(torch.autograd.Function):
         w = _lp(emb, emb.proj.weight, T).reshape(D, -1)
         cls_ = cls.detach().reshape(-1) if cls is not None else None
         pos_ = pos.detach().reshape(-1) if pos is not None else None
-        if emb.norm is None:
+        if emb.norm is None and emb.dtype == "bf16x3":
+            # the precision knob: patches and weight as split-bf16 pairs (tools/precision_emulate.py:
+            # the bf16 patch weight alone costs 1.1e-3 of ViT-B logits error); the backward reads hi
+            pf = ops.patch_im2col(img.contiguous().float(), P, F32)
+            p3, patches = ops.split_bf16x3(pf, 0, hi_copy=True)
+            del pf
+            w3, _ = ops.split_bf16x3(emb.proj.weight.detach().reshape(D, -1), 1)
+            tok = ops.linear_fwd(p3, w3, emb.proj.bias, F32)
+            x = ops.tokens_assemble(tok, B, np_, cls_, pos_)
+            saved = [patches]
+        elif emb.norm is None:
             # the §8(b) entry point: im2col -> patch GEMM (+bias) -> cls concat + pos-embed
             x, patches = ops.patch_embed_fwd(img.contiguous().float(), w, emb.proj.bias, cls_, pos_, P, T)
             saved = [patches]
@@ -737,7 +795,7 @@ class VisionTransformer(nn.Module):
     def arena(self) -> ParamArena:
         ps = self.backward_order()
         if self._arena is None or not self._arena.owns(ps) or self._arena.flat.device != ps[0].device:
-            self._arena = ParamArena(ps, ps[0].device, self.cfg.dtype == "bf16")
+            self._arena = ParamArena(ps, ps[0].device, self.cfg.dtype != "fp32")
             for m in self.modules():
                 if m is not self:
                     object.__setattr__(m, "_arena", self._arena)

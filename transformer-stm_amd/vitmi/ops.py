@@ -31,7 +31,8 @@ def dt(t: torch.dtype) -> int:
 
 
 def torch_dtype(name: str) -> torch.dtype:
-    return {"bf16": torch.bfloat16, "fp32": torch.float32}[name]
+    """The compute dtype of a ViTConfig.dtype ("bf16x3": bf16 MFMA with split forward operands)."""
+    return {"bf16": torch.bfloat16, "bf16x3": torch.bfloat16, "fp32": torch.float32}[name]
 
 
 def _s() -> int:
@@ -165,9 +166,14 @@ def bias_grad_(dy: Tensor, db: Tensor) -> None:
 
 
 def linear_wgrad(dy: Tensor, x: Tensor, dw: Tensor) -> None:
-    """dw[N,K] (fp32) += dy[M,N]^T x[M,K]."""
-    assert dy.is_contiguous() and x.is_contiguous() and dy.dtype == x.dtype
+    """dw[N,K] (fp32) += dy[M,N]^T x[M,K].  x may be row-strided (the hi part of a split
+    operand); then the generic GEMM entry point takes its row stride."""
+    assert dy.is_contiguous() and dy.dtype == x.dtype
     assert dw.dtype == torch.float32 and dw.is_contiguous()
+    if not x.is_contiguous():
+        M, N, K = dy.numel() // dy.shape[-1], dy.shape[-1], x.shape[-1]
+        gemm(dy.view(M, N), x, False, False, N, K, M, dw, EPI_ACCUM)
+        return
     M, N, K = dy.numel() // dy.shape[-1], dy.shape[-1], x.shape[-1]
     ws_n = lib().vitmi_linear_wgrad_workspace_size(dt(dy.dtype), M, N, K)
     ws = _ws(ws_n, dy)
@@ -422,6 +428,32 @@ def cast_bf16(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
         dst = torch.empty(src.shape, dtype=torch.bfloat16, device=src.device)
     check(lib().vitmi_cast_f32_bf16(src.numel(), _p(src), _p(dst), _s()), "cast")
     return dst
+
+
+def split_bf16x3(x: Tensor, pattern: int, hi_copy: bool = False):
+    """x fp32 [rows, K] (rows may be strided) -> (x3 bf16 [rows, 3K] laid out [hi | hi | lo]
+    (pattern 0, a GEMM's A operand) or [hi | lo | hi] (pattern 1, its weight), hi bf16 [rows, K]
+    or None): the split-bf16 operand of the precision knob (vitmi_split_bf16x3)."""
+    assert x.dtype == torch.float32
+    rows, ld = _rows(x)
+    K = x.shape[-1]
+    x3 = torch.empty(rows, 3 * K, dtype=torch.bfloat16, device=x.device)
+    hi = torch.empty(rows, K, dtype=torch.bfloat16, device=x.device) if hi_copy else None
+    check(lib().vitmi_split_bf16x3(rows, K, _p(x), ld, _p(x3), 3 * K, int(pattern), _p(hi), K, _s()),
+          "split_bf16x3")
+    return x3, hi
+
+
+def gelu_split_bf16x3(u: Tensor):
+    """u fp32 [rows, N] (the fc1 pre-activation) -> (split(gelu(u)) [rows, 3N] as [hi | hi | lo],
+    gelu'(u) bf16 [rows, N] row-major)."""
+    assert u.dtype == torch.float32 and u.is_contiguous()
+    N = u.shape[-1]
+    rows = u.numel() // N
+    act3 = torch.empty(rows, 3 * N, dtype=torch.bfloat16, device=u.device)
+    dg = torch.empty(rows, N, dtype=torch.bfloat16, device=u.device)
+    check(lib().vitmi_gelu_split_bf16x3(rows, N, _p(u), _p(act3), 3 * N, _p(dg), N, _s()), "gelu_split_bf16x3")
+    return act3, dg
 
 
 def cast_f32(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
