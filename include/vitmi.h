@@ -402,6 +402,18 @@ int vitmi_comm_check(void);
 /* abort != 0: ncclCommAbort (tear down after a peer failure without waiting) */
 int vitmi_comm_destroy(int abort);
 
+/* Deferred partial-sum folds.  The parameter-gradient outputs of vitmi_layernorm_bwd (dgamma, dbeta,
+ * dxsum), of the fused column sums of vitmi_linear_dgrad_bias / vitmi_attention_bwd_bias and of
+ * vitmi_bias_grad are formed in two steps: per-block partial rows in the caller's workspace, then a
+ * small fold launch (out += the column sums of the partial rows, fixed order).  Between
+ * vitmi_fold_begin() and vitmi_fold_end() on one host thread, those folds are queued instead of
+ * launched, and vitmi_fold_end launches them together (one launch per 16 folds, on the stream of the
+ * calls that queued them).  The caller keeps the workspaces of the queued calls alive until then; the
+ * outputs are final once vitmi_fold_end's launch has run (stream order).  vitmi/modules.py brackets
+ * each block's backward with them: one fold launch per block instead of four. */
+int vitmi_fold_begin(void);
+int vitmi_fold_end(vitmi_stream_t stream);
+
 /* Compute units the persistent GEMM leaves free (default 0): with data-parallel gradient
  * all-reduces in flight, RCCL's kernels need CUs while a one-block-per-CU GEMM would hold all
  * of them for its whole duration.  Returns the previous value. */

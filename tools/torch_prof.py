@@ -8,6 +8,7 @@ sys.path.insert(0, os.path.join(ROOT, "transformer-stm_amd"))
 import torch  # noqa: E402
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
+from vitmi import optim  # noqa: E402
 from vitmi.config import config_c3  # noqa: E402
 from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
@@ -17,13 +18,12 @@ def main():
     cfg = config_c3()
     model = VisionTransformer(cfg).cuda()
     model.reset_parameters(seed=0)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
-    arena = model.arena()
+    opt = optim.Adam(model, learning_rate=1e-3)
     img = torch.rand(B, 3, 224, 224, device="cuda")
     tgt = torch.randint(0, cfg.num_classes, (B,), device="cuda")
 
     def step():
-        arena.grad.zero_()
+        opt.zero_grad()
         loss = cross_entropy(model(img), tgt)
         loss.backward()
         opt.step()

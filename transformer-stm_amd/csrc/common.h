@@ -109,5 +109,8 @@ void stat_record(const void* kernel, double flops, double bytes);
 
 // db[n] += sum_z part[z][n] in a fixed order (elementwise.hip)
 int launch_colsum_finish(int64_t N, int Z, const float* part, float* db, hipStream_t s);
+// out[c] += sum_r part[r * ld + c] (fixed order), launched now or, between vitmi_fold_begin and
+// vitmi_fold_end on this thread, queued and launched with the other queued folds (elementwise.hip)
+int fold_rows(const float* part, int64_t rows, int64_t cols, int64_t ld, float* out, hipStream_t s);
 
 }  // namespace vitmi

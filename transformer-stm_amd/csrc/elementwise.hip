@@ -146,35 +146,92 @@ __global__ void colsum_kernel(int64_t M, int64_t N, const T* __restrict__ dy, in
   part[(int64_t)blockIdx.y * N + n] = s;
 }
 
-// db[n] += sum_z part[z][n]; 16 waves x 64 columns per block, fixed summation order
-// loads in flight per thread of the column-sum fold (A/B builds; the fold is latency-bound)
-#ifndef VITMI_CSF_UNROLL
-#define VITMI_CSF_UNROLL 8
+// ------------------------------------------------------------ partial-sum folds
+// out[c] += sum_r part[r * ld + c] for the per-block partial rows that the LayerNorm backward
+// (dgamma, dbeta and the fused bias-gradient column sums) and the fused column sums of the
+// DGELU dgrad / attention backward leave behind.  One launch folds up to FOLD_MAX such jobs
+// (blockIdx.y = job): each fold is a few MB and runs at the ~5 us floor of a dependent launch,
+// so a backward that queues its folds (vitmi_fold_begin / _end) pays that floor once per block
+// instead of four times.  Fixed summation order (row groups, then the 64 group sums in order):
+// deterministic, no atomics.
+struct FoldJob {
+  const float* part;
+  int64_t rows, cols, ld;
+  float* out;
+};
+constexpr int FOLD_MAX = 16;
+struct FoldBatch {
+  FoldJob j[FOLD_MAX];
+};
+
+#ifndef VITMI_FOLD_UNROLL
+#define VITMI_FOLD_UNROLL 8
 #endif
-__global__ __launch_bounds__(1024) void colsum_finish_kernel(int64_t N, int Z, const float* __restrict__ part,
-                                                             float* __restrict__ db) {
-  __shared__ float red[16][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t n = (int64_t)blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (n < N) {
-#pragma unroll VITMI_CSF_UNROLL
-    for (int z = w; z < Z; z += 16) s += part[(int64_t)z * N + n];
+__global__ __launch_bounds__(1024) void fold_kernel(FoldBatch b) {
+  __shared__ float red[64][17];
+  const FoldJob J = b.j[blockIdx.y];
+  if ((int64_t)blockIdx.x * 16 >= J.cols) return;              // block-uniform
+  const int c = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  const int64_t col = (int64_t)blockIdx.x * 16 + c;
+  float a = 0.f;
+  if (col < J.cols) {
+#pragma unroll VITMI_FOLD_UNROLL
+    for (int64_t r = gi; r < J.rows; r += 64) a += J.part[r * J.ld + col];
   }
-  red[w][lane] = s;
+  red[gi][c] = a;
   __syncthreads();
-  if (w == 0 && n < N) {
+  if (threadIdx.x < 16 && col < J.cols) {
     float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][lane];
-    db[n] += t;
+    for (int k = 0; k < 64; ++k) t += red[k][c];
+    J.out[col] += t;
   }
 }
 
-int launch_colsum_finish(int64_t N, int Z, const float* part, float* db, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, N, Z, part, db);
-  VITMI_LAUNCH_CHECK("colsum_finish");
+namespace {
+thread_local FoldBatch t_batch;
+thread_local int t_njobs = 0;
+thread_local bool t_defer = false;
+thread_local hipStream_t t_stream = nullptr;
+
+int launch_folds(const FoldBatch& b, int n, hipStream_t s) {
+  if (n == 0) return VITMI_OK;
+  int64_t bx = 1;
+  double by = 0;
+  for (int i = 0; i < n; ++i) {
+    const int64_t x = (b.j[i].cols + 15) / 16;
+    bx = x > bx ? x : bx;
+    by += 4.0 * (b.j[i].rows + 2) * b.j[i].cols;
+  }
+  hipLaunchKernelGGL(fold_kernel, dim3((unsigned)bx, (unsigned)n), dim3(1024), 0, s, b);
+  VITMI_LAUNCH_CHECK("fold");
+  VITMI_STAT(fold_kernel, 0, by);
   return VITMI_OK;
+}
+
+int flush_folds() {
+  const int n = t_njobs;
+  t_njobs = 0;
+  return launch_folds(t_batch, n, t_stream);
+}
+}  // namespace
+
+int fold_rows(const float* part, int64_t rows, int64_t cols, int64_t ld, float* out, hipStream_t s) {
+  if (out == nullptr || rows <= 0 || cols <= 0) return VITMI_OK;
+  const FoldJob job{part, rows, cols, ld, out};
+  if (!t_defer) {
+    FoldBatch b;
+    b.j[0] = job;
+    return launch_folds(b, 1, s);
+  }
+  if (t_njobs > 0 && (t_stream != s || t_njobs == FOLD_MAX))
+    if (int rc = flush_folds()) return rc;
+  t_stream = s;
+  t_batch.j[t_njobs++] = job;
+  return VITMI_OK;
+}
+
+int launch_colsum_finish(int64_t N, int Z, const float* part, float* db, hipStream_t s) {
+  return fold_rows(part, Z, N, N, db, s);
 }
 
 // number of row chunks: enough blocks to fill the chip (~1024) for the vector kernel
@@ -433,10 +490,8 @@ extern "C" int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, 
       hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)dy, ldy,
                          (float*)workspace, rows_per);
   }
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, s, N, Z,
-                     (const float*)workspace, db);
   VITMI_LAUNCH_CHECK("bias_grad");
-  return VITMI_OK;
+  return fold_rows((const float*)workspace, Z, N, N, db, s);
 }
 
 extern "C" int vitmi_head_fwd(int B, int D, int C, const float* y, int64_t ldy, const float* w,
@@ -517,4 +572,15 @@ extern "C" int vitmi_dropout_apply(int64_t M, int64_t N, const float* x, int64_t
 
 extern "C" uint32_t vitmi_dropout_hash(uint32_t seed, uint32_t site, uint32_t row, uint32_t col) {
   return drop_hash(drop_row_key(seed, site, row), col);
+}
+
+extern "C" int vitmi_fold_begin(void) {
+  t_defer = true;
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_fold_end(vitmi_stream_t stream) {
+  (void)stream;   // the queued folds run on the stream their producers ran on
+  t_defer = false;
+  return flush_folds();
 }

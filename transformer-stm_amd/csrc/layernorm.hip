@@ -165,46 +165,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 }
 
 
-// out[d] += sum_b part[b][d] for dgamma (rows 0..G-1), dbeta (G..2G-1), colsum(dx) (2G..3G-1),
-// in a fixed order (deterministic).
-// loads in flight per thread of the partial folds (A/B builds; the fold is latency-bound)
-#ifndef VITMI_LNR_UNROLL
-#define VITMI_LNR_UNROLL 8
-#endif
-__global__ __launch_bounds__(1024) void ln_param_reduce(const float* __restrict__ part, int G, int D,
-                                                        float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta,
-                                                        float* __restrict__ dxsum) {
-  // block = 16 columns x 64 row groups (48 blocks at D = 768, not 12: the fold is latency-
-  // bound, 13.4 us with 64-column blocks); row group gi sums partials gi, gi+64, ..., then
-  // thread (array, column) adds the 64 group sums in order
-  __shared__ float red[3][64][17];
-  const int c = threadIdx.x & 15, gi = threadIdx.x >> 4;
-  const int d = blockIdx.x * 16 + c;
-  float a = 0.f, b = 0.f, e = 0.f;
-  if (d < D) {
-#pragma unroll VITMI_LNR_UNROLL
-    for (int i = gi; i < G; i += 64) {
-      a += part[(int64_t)i * D + d];
-      b += part[(int64_t)(G + i) * D + d];
-      if (dxsum) e += part[(int64_t)(2 * G + i) * D + d];
-    }
-  }
-  red[0][gi][c] = a;
-  red[1][gi][c] = b;
-  red[2][gi][c] = e;
-  __syncthreads();
-  if (threadIdx.x < 48) {
-    const int w = threadIdx.x >> 4, c2 = threadIdx.x & 15, d2 = blockIdx.x * 16 + c2;
-    float* out = w == 0 ? dgamma : (w == 1 ? dbeta : dxsum);
-    if (d2 < D && out) {
-      float sum = 0.f;
-      for (int k = 0; k < 64; ++k) sum += red[w][k][c2];
-      out[d2] += sum;
-    }
-  }
-}
-
 #ifndef VITMI_LN_BWD_BLOCKS
 #define VITMI_LN_BWD_BLOCKS 512
 #endif
@@ -308,8 +268,9 @@ extern "C" int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtyp
     default: LNB(8) break;
   }
 #undef LNB
-  hipLaunchKernelGGL(ln_param_reduce, dim3((D + 15) / 16), dim3(1024), 0, s, (const float*)part, G,
-                     D, dgamma, dbeta, dxsum);
   VITMI_LAUNCH_CHECK("layernorm_bwd");
-  return VITMI_OK;
+  // the per-block partials of dgamma (rows 0..G-1), dbeta (G..2G-1), colsum(dx) (2G..3G-1)
+  if (int rc = fold_rows(part, G, D, D, dgamma, s)) return rc;
+  if (int rc = fold_rows(part + (int64_t)G * D, G, D, D, dbeta, s)) return rc;
+  return fold_rows(part + 2LL * G * D, G, D, D, dxsum, s);
 }

@@ -109,6 +109,17 @@ def _is_vitmi_node(x: Tensor) -> bool:
     return fn is not None and getattr(type(fn), "_forward_cls", None) in _HANDOVER_FNS
 
 
+def _folds(backward):
+    """Run a Function's backward with its partial-sum folds queued and launched together at
+    its end (ops.deferred_folds): one fold launch per backward, and every parameter gradient it
+    returns is final in stream order when it returns."""
+    def run(ctx, *grads):
+        with ops.deferred_folds():
+            return backward(ctx, *grads)
+    run.__doc__ = backward.__doc__
+    return run
+
+
 def _check_cuda(x: Tensor):
     if not x.is_cuda:
         raise RuntimeError("vitmi modules run only on the GPU (HIP); there is no CPU path")
@@ -139,6 +150,7 @@ class _LayerNormFn(torch.autograd.Function):
         return y.view(x.shape)
 
     @staticmethod
+    @_folds
     def backward(ctx, dy):
         xs, mean, rstd = ctx.saved_tensors
         mod = ctx.mod
@@ -223,6 +235,7 @@ class _AttentionFn(torch.autograd.Function):
         return y.view(B, N, D)
 
     @staticmethod
+    @_folds
     def backward(ctx, dy):
         xo, qkv, o, lse, wq, wo = ctx.saved_tensors
         mod, (B, N, D) = ctx.mod, ctx.shape
@@ -272,6 +285,7 @@ class _MlpFn(torch.autograd.Function):
         return y.view(shp)
 
     @staticmethod
+    @_folds
     def backward(ctx, dy):
         xo, a, u, w1, w2 = ctx.saved_tensors
         mod = ctx.mod
@@ -410,6 +424,7 @@ class _BlockFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_folds
     def backward(ctx, dout):
         (x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, u, act, wq, wo, w1, w2) = ctx.saved_tensors
         blk, (B, N, D) = ctx.blk, ctx.shape
@@ -531,6 +546,7 @@ class _EmbedFn(torch.autograd.Function):
         return x
 
     @staticmethod
+    @_folds
     def backward(ctx, dx):
         emb, cls, pos, (B, np_, D) = ctx.emb, ctx.cls, ctx.pos, ctx.dims
         ps = list(emb.parameters())
@@ -579,6 +595,7 @@ class _HeadFn(torch.autograd.Function):
         return logits
 
     @staticmethod
+    @_folds
     def backward(ctx, dlogits):
         x, y, mean, rstd = ctx.saved_tensors
         model, last = ctx.model, ctx.last_bias

@@ -7,6 +7,7 @@ fallback — a missing library or a bad shape raises.
 """
 from __future__ import annotations
 
+import threading
 from typing import Optional, Tuple
 
 import torch
@@ -59,8 +60,40 @@ def _p(t: Optional[Tensor]) -> Optional[int]:
     return t.data_ptr()
 
 
+# per host thread (the library's fold queue is thread-local too): the workspaces of calls whose
+# partial-sum folds are queued
+_TLS = threading.local()
+
+
 def _ws(nbytes: int, like: Tensor) -> Tensor:
-    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
+    ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
+    hold = getattr(_TLS, "hold", None)
+    if hold is not None:
+        hold.append(ws)
+    return ws
+
+
+class deferred_folds:
+    """``with ops.deferred_folds(): ...`` -- the partial-sum folds of the parameter-gradient
+    outputs inside (LayerNorm dgamma/dbeta/column sums, fused bias-gradient column sums) are
+    queued and launched together at exit (vitmi_fold_begin / vitmi_fold_end); the workspaces
+    they read are held until then.  The gradients are final in stream order after the exit."""
+
+    def __enter__(self):
+        self._nested = getattr(_TLS, "hold", None) is not None
+        if not self._nested:
+            _TLS.hold = []
+            check(lib().vitmi_fold_begin(), "fold_begin")
+        return self
+
+    def __exit__(self, *exc):
+        if self._nested:
+            return False
+        try:
+            check(lib().vitmi_fold_end(_s()), "fold_end")
+        finally:
+            _TLS.hold = None
+        return False
 
 
 def _rows(t: Tensor) -> Tuple[int, int]:
