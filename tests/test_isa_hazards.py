@@ -108,3 +108,96 @@ def test_no_valu_sgpr_write_feeds_vmem_within_5_wait_states(tmp_path):
         bad += scan(asm.splitlines())
     assert not bad, "VALU-written SGPR read by VMEM too early:\n" + "\n".join(
         f"{k[:60]}: {t} ({w} wait states, {r})" for k, t, w, r in bad[:20])
+
+
+# ------------------------------------------------------------------ inline-asm loads
+# The persistent dK/dV kernels (csrc/attention.hip attn_bwd_dkv_seq_bf16) load K, V, lse and delta
+# with inline-asm buffer loads the compiler does not track (asm_load16 / asm_load4) and stage Q | dO
+# with inline-asm LDS-DMA (dma_piece, which writes M0).  Correctness rests on the compiled code never
+# touching such a load's destination VGPRs before the kernel's own `s_waitcnt vmcnt` (a spill, copy
+# or back-edge move would read stale data or be overwritten when the load lands), and on every LDS-DMA
+# reading the M0 its own statement just wrote.
+_VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+
+
+def _vregs(text):
+    out = set()
+    for m in _VREG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def scan_asm_loads(lines, kernel_filter=lambda k: True):
+    """-> list of (kernel, problem): VGPR destinations of a (non-LDS) buffer load referenced before
+    the next s_waitcnt vmcnt; an LDS-DMA load not directly preceded (s_nop aside) by its own
+    s_mov_b32 m0."""
+    bad = []
+    kernel, pending, prev = "?", {}, []
+    for ln in lines:
+        m = re.match(r"^[0-9a-f]+ <(.+)>:", ln)
+        if m:
+            kernel, pending, prev = m.group(1), {}, []
+            continue
+        if not kernel_filter(kernel):
+            continue
+        t = ln.strip().split("//")[0].strip()
+        if not t or t.endswith(":"):
+            continue
+        op, _, rest = t.partition(" ")
+        if op == "s_waitcnt" and "vmcnt" in rest:
+            pending = {}
+        elif op.startswith("buffer_load") and rest.rstrip().endswith(" lds"):
+            real = [p for p in prev if not p.startswith("s_nop")]
+            if not real or not real[-1].startswith("s_mov_b32 m0,"):
+                bad.append((kernel, f"LDS-DMA without its own M0 write: {t}"))
+        elif op.startswith(("buffer_load", "global_load")):
+            ops = _operands(rest)
+            used = _vregs(" ".join(ops[1:]))
+            hit = used & set(pending)
+            if hit:
+                bad.append((kernel, f"{t} uses v{min(hit)} loaded by `{pending[min(hit)]}` before a vmcnt wait"))
+            for r in _vregs(ops[0]):
+                pending[r] = t
+        else:
+            hit = _vregs(rest) & set(pending)
+            if hit:
+                bad.append((kernel, f"{t} touches v{min(hit)} loaded by `{pending[min(hit)]}` before a vmcnt wait"))
+        prev = (prev + [t])[-4:]
+    return bad
+
+
+def test_asm_load_scanner_catches_both_hazards():
+    lines = ["0000000000000000 <k>:",
+             "\tbuffer_load_dwordx4 v[10:13], v2, s[4:7], 0 offen",
+             "\tv_mov_b32 v40, v11",
+             "\ts_waitcnt vmcnt(0)",
+             "\tv_mov_b32 v41, v12",
+             "\ts_mov_b32 m0, s3",
+             "\ts_nop 0",
+             "\tbuffer_load_dwordx4 v5, s[8:11], 0 offen lds",
+             "\tv_add_u32 v6, v6, v7",
+             "\tbuffer_load_dwordx4 v5, s[8:11], 0 offen lds"]
+    bad = scan_asm_loads(lines)
+    assert len(bad) == 2 and "v11" in bad[0][1] and "M0" in bad[1][1]
+
+
+def test_dkv_kernels_asm_loads_and_m0(tmp_path):
+    if not (os.path.exists(OBJDUMP) and os.path.exists(LIB)):
+        pytest.skip("needs llvm-objdump and the built library")
+    lib = tmp_path / "libvitmi.so"
+    shutil.copy(LIB, lib)
+    subprocess.run([OBJDUMP, "--offloading", str(lib)], check=True, capture_output=True, timeout=120)
+    objs = [f for f in glob.glob(str(tmp_path / "libvitmi.so.*")) if "amdgcn" in f]
+    seen, bad = 0, []
+    for f in objs:
+        asm = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", f], check=True, capture_output=True,
+                             text=True, timeout=300).stdout
+        if "attn_bwd_dkv_seq_bf16" not in asm:
+            continue
+        seen += 1
+        bad += scan_asm_loads(asm.splitlines(), lambda k: "attn_bwd_dkv_seq_bf16" in k)
+    assert seen, "no code object holds the dK/dV kernels"
+    assert not bad, "\n".join(f"{k[:50]}: {p}" for k, p in bad[:20])
