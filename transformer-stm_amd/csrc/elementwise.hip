@@ -223,7 +223,12 @@ int fold_rows(const float* part, int64_t rows, int64_t cols, int64_t ld, float* 
     b.j[0] = job;
     return launch_folds(b, 1, s);
   }
-  if (t_njobs > 0 && (t_stream != s || t_njobs == FOLD_MAX))
+  // two queued folds into overlapping outputs would race in one launch (+= from two blocks; a tied
+  // LayerNorm's dgamma receives both LN backwards' partials): launch the queue first
+  bool overlap = false;
+  for (int i = 0; i < t_njobs; ++i)
+    overlap |= t_batch.j[i].out < out + cols && out < t_batch.j[i].out + t_batch.j[i].cols;
+  if (t_njobs > 0 && (t_stream != s || t_njobs == FOLD_MAX || overlap))
     if (int rc = flush_folds()) return rc;
   t_stream = s;
   t_batch.j[t_njobs++] = job;
