@@ -31,7 +31,13 @@ extern "C" {
 typedef void* vitmi_stream_t; /* hipStream_t */
 
 enum { VITMI_OK = 0, VITMI_ERR_INVALID = 1, VITMI_ERR_HIP = 2, VITMI_ERR_UNSUPPORTED = 3, VITMI_ERR_COMM = 4 };
-enum { VITMI_F32 = 0, VITMI_BF16 = 1, VITMI_F64 = 2 /* comm only */ };
+enum {
+  VITMI_F32 = 0,
+  VITMI_BF16 = 1,
+  VITMI_F64 = 2,    /* comm only */
+  VITMI_BF16X3 = 3  /* vitmi_layernorm_fwd's y only: bf16 rows [hi | hi | lo] of 3D columns, the
+                       split-bf16 A operand of the precision knob (vitmi_split_bf16x3) */
+};
 
 /* GEMM epilogues (all apply `bias` (fp32, may be NULL) first where it applies) */
 enum {
@@ -48,6 +54,11 @@ enum {
  * transpose): the fc1 forward / fc2 dgrad pair of the ViT MLP (models/CvT(Par).py:253-258). */
 #define VITMI_EPI_AUX_TILED 0x100
 size_t vitmi_aux_tiled_bytes(int64_t rows, int64_t cols);
+/* OR'ed into BIAS_GELU of vitmi_linear_fwd (bf16 operands and output; the precision knob,
+ * ViTConfig dtype "bf16x3"): y is bf16 [M][3N], each row [hi | hi | lo] of the fp32 gelu(u)
+ * (hi = bf16(a), lo = bf16(a - hi): the split A operand of the next GEMM, vitmi_split_bf16x3
+ * pattern 0); aux = gelu'(u) as for BIAS_GELU. */
+#define VITMI_EPI_SPLIT_X3 0x200
 
 enum { VITMI_LOSS_CE = 0, VITMI_LOSS_MSE = 1 };
 
@@ -137,6 +148,7 @@ size_t vitmi_bias_grad_workspace_size(int64_t M, int64_t N);
 /* ---------------------------------------------------------------------------
  * LayerNorm over the last dim D (layers.LayerNormalization, models/CvT(Par).py:248,328;
  * old_codes/MS_CvT.py:39-45).  x is fp32 [M][ldx]; y [M][ldy] of y_dtype; mean/rstd fp32 [M].
+ * y_dtype VITMI_BF16X3: y is bf16 [M][ldy >= 3D], each row [hi | hi | lo] of the fp32 result.
  */
 int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const float* gamma,
                         const float* beta, float eps, void* y, int y_dtype, int64_t ldy,
@@ -159,6 +171,12 @@ size_t vitmi_layernorm_bwd_workspace_size(int64_t M, int D);
  */
 int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float scale, const void* qkv,
                         void* o, float* lse, vitmi_stream_t stream);
+/* The precision knob's attention forward (bf16 q, k, v; ViTConfig dtype "bf16x3"): as
+ * vitmi_attention_fwd(VITMI_BF16, ...) -- o (bf16 [B*N][H*dh]) and lse bit for bit -- plus o3,
+ * bf16 [B*N][3*H*dh], each row [hi | hi | lo] of the fp32 output (the out-projection GEMM's
+ * split A operand, vitmi_split_bf16x3 pattern 0).  N <= 256 (the whole-sequence kernel). */
+int vitmi_attention_fwd_x3(int B, int N, int H, int dh, float scale, const void* qkv, void* o, void* o3,
+                           float* lse, vitmi_stream_t stream);
 int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, const void* qkv,
                         const void* o, const void* dout, const float* lse, void* dqkv,
                         void* workspace, size_t ws_bytes, vitmi_stream_t stream);

@@ -333,11 +333,11 @@ def test_vit_b_precision_knob_fp32_meets_1e3():
 
 def test_vit_b_precision_knob_bf16x3_meets_1e3():
     """The split-bf16 precision knob (dtype='bf16x3': the forward GEMMs' weights, LayerNorm
-    outputs, attention output and GELU output as hi + lo bf16 pairs, the attention forward in
-    fp32; tools/precision_emulate.py ranks those operands) meets the north star's logits within
-    1e-3 against the fp32 CPU oracle at ViT-B/16 full depth 12, on the randomised-parameter
-    stress case where the bf16 default measures 3.6e-3.  The backward is the bf16 one (grads
-    at the bf16 bound)."""
+    outputs, attention output and GELU output as hi + lo bf16 pairs; q, k, v and the softmax P
+    bf16; tools/precision_emulate.py ranks those operands and puts this set at 1.5e-4) meets the
+    north star's logits within 1e-3 against the fp32 CPU oracle at ViT-B/16 full depth 12, on the
+    randomised-parameter stress case where the bf16 default measures 3.6e-3 (measured 1.7e-4).
+    The backward is the bf16 one (grads at the bf16 bound)."""
     cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype="bf16x3")
     params = vit_ref.init_params(cfg, seed=0)
     img, tgt = vit_ref.synthetic_batch(cfg, 2)
@@ -348,11 +348,13 @@ def test_vit_b_precision_knob_bf16x3_meets_1e3():
 
 def test_bf16x3_knob_small_model_matches_oracle():
     """bf16x3 on the C1 shape (ViT-Ti/16 64^2, N = 17) and on a ragged token count (48^2, N = 10):
-    logits at the fp32-class bound, gradients (the bf16 backward) at SURVEY §8d's bf16 bound 2e-2
-    (the worst, block 0's norm1.bias at 5 images, measures 1.7e-2: a column sum over 50 rows)."""
+    logits within the north star's 1e-3 (C1 measures 3.3e-4: the bf16 q, k, v and P), gradients
+    (the bf16 backward) at SURVEY §8d's bf16 bound 2e-2 (the worst, block 0's norm1.bias at 5
+    images, measures 1.7e-2: a column sum over 50 rows)."""
     for cfg in (config_c1(dtype="bf16x3"), config_c1(dtype="bf16x3", img_size=48)):
         params = vit_ref.init_params(cfg, seed=3)
         img, tgt = vit_ref.synthetic_batch(cfg, 5)
-        _, w3 = compare(cfg, params, img, tgt, logit_tol=2e-4, grad_tol=2e-2, loss_tol=1e-4)
-        _, wb = compare(cfg.replace(dtype="bf16"), params, img, tgt, logit_tol=5e-3, grad_tol=2e-2, loss_tol=2e-2)
-        print(f"{cfg.img_size}px: worst grad bf16x3 {w3[1]} {w3[0]:.3e}, bf16 {wb[1]} {wb[0]:.3e}")
+        e3, w3 = compare(cfg, params, img, tgt, logit_tol=1e-3, grad_tol=2e-2, loss_tol=1e-3)
+        eb, wb = compare(cfg.replace(dtype="bf16"), params, img, tgt, logit_tol=5e-3, grad_tol=2e-2, loss_tol=2e-2)
+        print(f"{cfg.img_size}px: logits bf16x3 {e3:.3e}, bf16 {eb:.3e}; "
+              f"worst grad bf16x3 {w3[1]} {w3[0]:.3e}, bf16 {wb[1]} {wb[0]:.3e}")

@@ -505,3 +505,59 @@ def test_gelu_split_bf16x3():
     t = u.double()
     dref = 0.5 * (1 + torch.erf(t / 2 ** 0.5)) + t * torch.exp(-0.5 * t * t) / (2 * torch.pi) ** 0.5
     assert ((dg.double() - dref).abs() <= dref.abs() * 8e-3 + 1e-3).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(197 * 8, 3072, 3 * 768), (50, 256, 3 * 192), (197 * 2, 520, 3 * 64)])
+def test_linear_fwd_gelu_split_x3(M, N, K):
+    """VITMI_EPI_SPLIT_X3: the fc1 epilogue writes the GELU output as [hi | hi | lo] rows.  hi and
+    gelu' are bit for bit the plain BIAS_GELU epilogue's (same accumulation, same GELU), and
+    hi + lo carries gelu(u) to ~2^-16 (u = the fp32 GEMM output).  Shapes: gemm256 with the
+    tail split (K' = 2304), the 128-tile kernel, ragged N."""
+    x = rnd(M, K, seed=101).to(DEV).to(BF)
+    w = (rnd(N, K, seed=102) * 0.05).to(DEV).to(BF)
+    b = (rnd(N, seed=103) * 0.5).to(DEV)
+    y3, g3 = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, aux_tiled=True, split_x3=True)
+    y1, g1 = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, aux_tiled=True)
+    assert y3.shape == (M, 3 * N)
+    assert torch.equal(y3[:, :N], y1) and torch.equal(y3[:, N:2 * N], y1) and torch.equal(g3, g1)
+    u = ops.linear_fwd(x, w, b, torch.float32).double()
+    ref = torch.nn.functional.gelu(u)
+    got = y3[:, :N].double() + y3[:, 2 * N:].double()
+    assert ((got - ref).abs() <= ref.abs() * 2.0 ** -15 + 2e-6).all(), (got - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("M,D", [(197 * 3, 768), (37, 192), (5, 1024)])
+def test_layernorm_fwd_writes_split_rows(M, D):
+    """layernorm_fwd with out_dtype BF16X3 (VITMI_BF16X3): the [hi | hi | lo] rows of the fp32
+    LayerNorm output, bit for bit what split_bf16x3 makes of the fp32 kernel's y; mean/rstd equal."""
+    x = (rnd(M, D + 4, seed=95) * 2 + 0.5).to(DEV)[:, :D]
+    w = (1 + 0.3 * rnd(D, seed=96)).to(DEV)
+    b = (0.2 * rnd(D, seed=97)).to(DEV)
+    y3, m3, r3 = ops.layernorm_fwd(x, w, b, 1e-6, ops.BF16X3)
+    yf, mf, rf = ops.layernorm_fwd(x, w, b, 1e-6, torch.float32)
+    ref, _ = ops.split_bf16x3(yf, 0)
+    assert y3.shape == (M, 3 * D) and torch.equal(y3, ref)
+    assert torch.equal(m3, mf) and torch.equal(r3, rf)
+
+
+@pytest.mark.parametrize("B,N,H", [(3, 197, 12), (2, 17, 3), (1, 256, 2)])
+def test_attention_fwd_x3_split_output(B, N, H):
+    """vitmi_attention_fwd_x3: o and lse are the bf16 whole-sequence kernel's, bit for bit; o3 rows
+    are [hi | hi | lo] with hi = o, and hi + lo tracks the softmax-attention of the same bf16 q, k, v
+    (fp64) ~2^-9 relative (the kernel's bf16 P), where hi alone is 2^-9 rounding on top."""
+    D = 64 * H
+    qkv = (rnd(B * N, 3 * D, seed=98) * 0.7).to(DEV).to(BF)
+    o, o3, lse = ops.attention_fwd_x3(qkv, B, N, H, 0.125)
+    o_ref, lse_ref = ops.attention_fwd(qkv, B, N, H, 0.125)
+    assert torch.equal(o, o_ref) and torch.equal(lse, lse_ref)
+    assert torch.equal(o3[:, :D], o) and torch.equal(o3[:, D:2 * D], o)
+    q, k, v = (t.double().view(B, N, H, 64).transpose(1, 2) for t in qkv.split(D, dim=1))
+    ref = torch.softmax(q @ k.transpose(-1, -2) * 0.125, -1) @ v
+    ref = ref.transpose(1, 2).reshape(B * N, D)
+    full = o3[:, :D].double() + o3[:, 2 * D:].double()
+    scale = ref.abs().max().item()
+    e_full = (full - ref).abs().max().item() / scale
+    e_hi = (o.double() - ref).abs().max().item() / scale
+    assert e_full < 4e-3, (e_full, e_hi)
+    # lo is the residual of the fp32 O below hi's rounding step
+    assert (o3[:, 2 * D:].double().abs() <= o.double().abs() * 2.0 ** -8 + 1e-30).all()

@@ -8,7 +8,7 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/transformer-stm_amd/variants
 mkdir -p $out /tmp/vb_$name
 objs=""
-for f in abi.cpp boundary.cpp comm.cpp gemm.hip attention.hip layernorm.hip elementwise.hip cvt.hip dense.hip optim.hip sls.hip; do
+for f in abi.cpp boundary.cpp comm.cpp gemm.hip attention.hip layernorm.hip elementwise.hip cvt.hip dense.hip optim.hip sls.hip split.hip; do
   extra=""; [ "$f" = optim.hip ] && extra=-ffp-contract=off
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $extra $VARIANT_FLAGS -c $src/$f -o /tmp/vb_$name/$f.o &
   objs="$objs /tmp/vb_$name/$f.o"

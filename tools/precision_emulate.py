@@ -85,12 +85,12 @@ SETTINGS = [
     ("q, k, v only", {"QKV"}),
     ("softmax P only", {"PR"}),
     ("patches only", {"P"}),
-    ("bf16x3 GEMM operands (W, P, LN, O, ACT split); q/k/v and P bf16", {"QKV", "PR"}),
+    ("the knob as built: GEMM operands split; q/k/v and P bf16", {"QKV", "PR"}),
     ("bf16x3 on W, P, LN, ACT; O, q/k/v and P bf16", {"QKV", "PR", "O"}),
     ("bf16x3 on W, LN, O, ACT; patches, q/k/v and P bf16", {"QKV", "PR", "P"}),
     ("bf16x3 on the block GEMMs; the patch GEMM (patches, weight) bf16", {"QKV", "PR", "P", "WP"}),
     ("the patch weight only", {"WP"}),
-    ("none (the knob as built: every GEMM operand split, attention fp32)", set()),
+    ("none (GEMM operands split and attention in fp32)", set()),
 ]
 
 

@@ -661,10 +661,12 @@ __device__ __forceinline__ void stage_seq_dma(char* lds, __amdgpu_buffer_rsrc_t 
 
 // grid B*H, block 64*NW.  Online softmax over key tiles of 64 (a final tile of 32 when NP is
 // an odd multiple of 32); keys >= N exist only in the last tile and are masked there.
-template <int NPMAX>
+// X3 (the precision knob, vitmi_attention_fwd_x3): also o3 = [hi | hi | lo] rows of the fp32 O.
+template <int NPMAX, bool X3 = false>
 __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __restrict__ qkv,
                                                                bf16* __restrict__ o, float* __restrict__ lse,
-                                                               int N, int H, float scale) {
+                                                               int N, int H, float scale,
+                                                               bf16* __restrict__ o3 = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -764,7 +766,26 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   __syncthreads();
   const int64_t ldo = (int64_t)D * 2;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
-  store_tile32(smem + wave * ST_BYTES, oacc, 1.f / lt, ro, ldo, wave * 32, lane_here());
+  const float inv = 1.f / lt;
+  store_tile32(smem + wave * ST_BYTES, oacc, inv, ro, ldo, wave * 32, lane_here());
+  if constexpr (X3) {
+    // hi = bf16(O) twice, then lo = bf16(O - hi), O = oacc * inv exactly as store_tile32 forms it
+    const int64_t ld3 = 3 * ldo;
+    const uint32_t by3 = (uint32_t)((int64_t)N * ld3);
+    bf16* base3 = o3 + (int64_t)b * N * 3 * D + hd * DH;
+    store_tile32(smem + wave * ST_BYTES, oacc, inv, make_rsrc(base3 + D, by3 - (D + hd * DH) * 2), ld3, wave * 32,
+                 lane_here());
+    store_tile32(smem + wave * ST_BYTES, oacc, inv, make_rsrc(base3, by3 - hd * DH * 2), ld3, wave * 32, lane_here());
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = oacc[dt][r] * inv;
+        oacc[dt][r] = v - (float)(bf16)v;
+      }
+    store_tile32(smem + wave * ST_BYTES, oacc, 1.f, make_rsrc(base3 + 2 * D, by3 - (2 * D + hd * DH) * 2), ld3,
+                 wave * 32, lane_here());
+  }
 }
 
 // dQ (+ delta = rowsum(dO * O)): grid B*H, block 64*NW, wave w owns queries 32w..+31, K and V
@@ -1568,6 +1589,20 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
     else if (seq_path(N)) VITMI_STAT(attn_fwd_seq_f32<SEQ_MAX>, fl, by);
     else VITMI_STAT(attn_fwd_f32, fl, by);
   }
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_attention_fwd_x3(int B, int N, int H, int dh, float scale, const void* qkv, void* o, void* o3,
+                                      float* lse, vitmi_stream_t stream) {
+  if (int rc = attn_check(VITMI_BF16, B, N, H, dh)) return rc;
+  VITMI_CHECK_ARG(N <= SEQ_MAX, "attention_fwd_x3: N must be <= %d (the whole-sequence kernel)", SEQ_MAX);
+  VITMI_CHECK_ARG(qkv && o && o3 && lse, "attention_fwd_x3: null pointer");
+  VITMI_CHECK_ARG((int64_t)N * 3 * H * DH * 2 < 0x7fffffffLL, "attention_fwd_x3: one batch row block exceeds 2 GiB");
+  hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, true>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
+                     (hipStream_t)stream, (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o3);
+  VITMI_LAUNCH_CHECK("attention_fwd_x3");
+  const double bh = (double)B * H;
+  VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, true>), 4.0 * bh * N * N * DH, bh * N * DH * 2 * (3 + 1 + 3) + bh * N * 4);
   return VITMI_OK;
 }
 

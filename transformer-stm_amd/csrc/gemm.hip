@@ -121,15 +121,17 @@ __device__ __forceinline__ void tile_rc(const GemmArgs& g, int tl, int& tm, int&
 }
 
 // internal epilogues: split-K partial slab, and GELU / residual with a fused dropout
-enum { EPI_PARTIAL = 100, EPI_GELU_DROP = 101, EPI_RESIDUAL_DROP = 102 };
+// EPI_GELU_X3: BIAS_GELU with the activation written split, [hi | hi | lo] (VITMI_EPI_SPLIT_X3)
+enum { EPI_PARTIAL = 100, EPI_GELU_DROP = 101, EPI_RESIDUAL_DROP = 102, EPI_GELU_X3 = 103 };
 // the public epilogue an internal one extends, and whether it drops
 template <int EPI> struct EpiOf {
-  static constexpr int base = EPI == EPI_GELU_DROP ? VITMI_EPI_BIAS_GELU
+  static constexpr int base = EPI == EPI_GELU_DROP || EPI == EPI_GELU_X3 ? VITMI_EPI_BIAS_GELU
                               : EPI == EPI_RESIDUAL_DROP ? VITMI_EPI_RESIDUAL : EPI;
   static constexpr bool drop = EPI == EPI_GELU_DROP || EPI == EPI_RESIDUAL_DROP;
 };
 static inline int epi_base(int epi) {
-  return epi == EPI_GELU_DROP ? VITMI_EPI_BIAS_GELU : epi == EPI_RESIDUAL_DROP ? VITMI_EPI_RESIDUAL : epi;
+  return epi == EPI_GELU_DROP || epi == EPI_GELU_X3 ? VITMI_EPI_BIAS_GELU
+         : epi == EPI_RESIDUAL_DROP ? VITMI_EPI_RESIDUAL : epi;
 }
 // dropout factor (0 or 1/(1-p)) of output element (row, col)
 __device__ __forceinline__ float drop_factor(const GemmArgs& g, int64_t row, int64_t col) {
@@ -281,6 +283,14 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, int64_t row, int64_
     const float u = acc + biasv;
     ((T*)g.aux)[aux_at(g, row, col)] = from_f32<T>(gelu_grad_f(u));
     ((TC*)g.C)[row * g.ldc + col] = from_f32<TC>(gelu_f(u));
+  } else if constexpr (EPI == EPI_GELU_X3) {
+    const float u = acc + biasv, a = gelu_f(u);
+    const bf16 hi = (bf16)a;
+    bf16* c = (bf16*)g.C + row * g.ldc + col;
+    ((T*)g.aux)[aux_at(g, row, col)] = from_f32<T>(gelu_grad_f(u));
+    c[0] = hi;
+    c[g.N] = hi;
+    c[2 * g.N] = (bf16)(a - (float)hi);
   } else if constexpr (EPI == VITMI_EPI_RESIDUAL) {
     ((float*)g.C)[row * g.ldc + col] = g.residual[row * g.ldr + col] + acc + biasv;
   } else if constexpr (EPI == VITMI_EPI_DGELU) {
@@ -811,6 +821,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       if constexpr (EPI == EPI_PARTIAL) zoff = (int64_t)(blockIdx.z + zs) * g.split_stride;
       char* cbase = (char*)g.C + (zoff + m0 * g.ldc + n0) * CES;
       const __amdgpu_buffer_rsrc_t rc = make_rsrc(cbase, clamp_bytes(((g.M - m0) * g.ldc - n0) * CES));
+      // EPI_GELU_X3: the second hi copy at column N + c, lo at 2N + c
+      [[maybe_unused]] __amdgpu_buffer_rsrc_t rc2 = rc, rc3 = rc;
+      if constexpr (EPI == EPI_GELU_X3) {
+        rc2 = make_rsrc(cbase + g.N * 2, clamp_bytes(((g.M - m0) * g.ldc - n0 - g.N) * 2));
+        rc3 = make_rsrc(cbase + g.N * 4, clamp_bytes(((g.M - m0) * g.ldc - n0 - 2 * g.N) * 2));
+      }
       const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
       const uint32_t vbase = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldc + wn * 64 + lc4) * CES);
       // Branch-free ragged N (straight-line epilogue code schedules far better): lanes past
@@ -876,6 +892,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         }
         lane_xchg();   // and the next writes of the image stay after these reads
       };
+      [[maybe_unused]] bf16x4 lo3[4];   // EPI_GELU_X3: lo = bf16(a - hi) of the row group's fragments
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand.
       // Returns the fragment of the second output (gelu') for BIAS_GELU.
       auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) -> bf16x4 {
@@ -918,6 +935,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
           lds_put(ni, o);
+          if constexpr (EPI == EPI_GELU_X3) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lo3[ni][e] = (bf16)(v[e] - (float)o[e]);
+          }
         }
         return u;
       };
@@ -928,6 +949,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         for (int ni = 0; ni < 4; ++ni) us[ni] = emit(mi, ni, ldv[ni], ldb[ni]);
         if constexpr (CES == 2) {
           flush(rc, g.ldc, mi);
+          if constexpr (EPI == EPI_GELU_X3) {   // the same image again at +N, then lo at +2N
+            flush(rc2, g.ldc, mi);
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) lds_put(ni, lo3[ni]);
+            flush(rc3, g.ldc, mi);
+          }
           if constexpr (EB == VITMI_EPI_BIAS_GELU) {
             if (g.aux_tiled) {   // straight from the registers: 2 KiB-wide stores (aux_at)
               const u32x4 w0 = __builtin_bit_cast(u32x4, bf16x8{us[0][0], us[0][1], us[0][2], us[0][3],
@@ -1137,7 +1164,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       // stores only make the waits below stricter.)
       constexpr int CES2 = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EB != VITMI_EPI_ACCUM &&
                            EB != VITMI_EPI_RESIDUAL;
-      constexpr int EP = CES2 ? (EB == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU ? 32 : 16)
+      constexpr int EP = CES2 ? (EPI == EPI_GELU_X3 ? 64 : EB == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU ? 32 : 16)
                               : (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ? 64
                                  : EPI == VITMI_EPI_DGELU ? 48 : 32);
       ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : EP;
@@ -1357,7 +1384,7 @@ static void gemm_stat(const void* kernel, const GemmArgs& g) {
   const double M = (double)g.M, N = (double)g.N, K = (double)g.K, es = sizeof(T);
   double bytes = (M * K + N * K) * es;
   if (EPI == EPI_PARTIAL || EB == VITMI_EPI_ACCUM) bytes += 2.0 * M * N * 4;   // dW += (read + write, fp32)
-  else bytes += M * N * sizeof(TC);
+  else bytes += M * N * sizeof(TC) * (EPI == EPI_GELU_X3 ? 3 : 1);
   if (EB == VITMI_EPI_BIAS_GELU || EB == VITMI_EPI_DGELU) bytes += M * N * es;   // gelu' written / read
   if (EB == VITMI_EPI_RESIDUAL) bytes += M * N * 4;                               // residual read
   VITMI_STAT(kernel, 2.0 * M * N * K, bytes);
@@ -1465,6 +1492,10 @@ static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits
     case EPI_RESIDUAL_DROP:
       if (!(ak && bk)) break;
       return launch_t<T, true, true, EPI_RESIDUAL_DROP, float>(g, splits, big, s);
+    case EPI_GELU_X3:   // forward linear layers, bf16 operands and output only (gemm_impl checks)
+      if (!(ak && bk)) break;
+      if constexpr (std::is_same<T, bf16>::value) return launch_t<T, true, true, EPI_GELU_X3, bf16>(g, splits, big, s);
+      break;
   }
   return fail(VITMI_ERR_INVALID, "gemm: unknown epilogue %d", epi);
 }
@@ -1494,7 +1525,14 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
                      const GemmArgs* drop = nullptr, float* colsum = nullptr, bool* colsum_done = nullptr) {
   if (colsum_done) *colsum_done = false;
   const bool aux_tiled = (epi & VITMI_EPI_AUX_TILED) != 0;
-  epi &= ~VITMI_EPI_AUX_TILED;
+  const bool x3 = (epi & VITMI_EPI_SPLIT_X3) != 0;
+  epi &= ~(VITMI_EPI_AUX_TILED | VITMI_EPI_SPLIT_X3);
+  if (x3) {
+    VITMI_CHECK_ARG(epi == VITMI_EPI_BIAS_GELU && dtype == VITMI_BF16 && c_dtype == VITMI_BF16 && ak && bk,
+                    "gemm: SPLIT_X3 needs BIAS_GELU, bf16 operands and output, k-major A and B");
+    VITMI_CHECK_ARG(ldc >= 3 * N, "gemm: SPLIT_X3 needs ldc >= 3N");
+    epi = EPI_GELU_X3;
+  }
   VITMI_CHECK_ARG(dtype == VITMI_BF16 || dtype == VITMI_F32, "gemm: bad dtype %d", dtype);
   VITMI_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
   if (M == 0 || N == 0) return VITMI_OK;
@@ -1650,10 +1688,11 @@ extern "C" int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, cons
                                 const void* w, const float* bias, void* y, int y_dtype,
                                 int epilogue, void* aux, const float* residual, void* workspace,
                                 size_t ws_bytes, vitmi_stream_t stream) {
-  const int eb = epilogue & ~VITMI_EPI_AUX_TILED;
+  const int eb = epilogue & ~(VITMI_EPI_AUX_TILED | VITMI_EPI_SPLIT_X3);
   VITMI_CHECK_ARG(eb == VITMI_EPI_STORE || eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_RESIDUAL,
                   "linear_fwd: bad epilogue %d", epilogue);
-  return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, N, y_dtype, epilogue, bias, aux, N,
+  const int64_t ldy = (epilogue & VITMI_EPI_SPLIT_X3) ? 3 * N : N;
+  return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, ldy, y_dtype, epilogue, bias, aux, N,
                    residual, N, workspace, ws_bytes, (hipStream_t)stream, false);
 }
 

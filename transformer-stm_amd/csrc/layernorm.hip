@@ -8,6 +8,7 @@
 // second pass folds into the fp32 parameter gradients (+=).
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace vitmi {
 
@@ -42,6 +43,10 @@ __device__ __forceinline__ f32x4 load4<bf16>(const bf16* p) {
 }
 
 // ---------------------------------------------------------------- forward
+// y dtype tag of the precision knob's A operand (VITMI_BF16X3): bf16 rows [hi | hi | lo] of 3D
+// columns, hi = bf16(y), lo = bf16(y - hi) (csrc/split.hip), written straight from the fp32 row
+struct SplitX3 {};
+
 template <int NV, typename TY>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const float* __restrict__ x,
                                                      int64_t ldx, const float* __restrict__ gamma,
@@ -71,14 +76,27 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
     }
   }
   const float rs = rsqrtf(wave_sum(q) / D + eps);
-  TY* yr = y + row * ldy;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (lane + 64 * i) * 4;
     if (c < D) {
       const f32x4 g = *(const f32x4*)(gamma + c);
       const f32x4 b = *(const f32x4*)(beta + c);
-      store4<TY>(yr + c, (v[i] - mu) * rs * g + b);
+      const f32x4 o = (v[i] - mu) * rs * g + b;
+      if constexpr (std::is_same_v<TY, SplitX3>) {
+        bf16* yr = (bf16*)y + row * ldy + c;
+        bf16x4 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          hi[e] = (bf16)o[e];
+          lo[e] = (bf16)(o[e] - (float)hi[e]);
+        }
+        put((bf16x4*)yr, hi);
+        put((bf16x4*)(yr + D), hi);
+        put((bf16x4*)(yr + 2 * D), lo);
+      } else {
+        store4<TY>(y + row * ldy + c, o);
+      }
     }
   }
   if (lane == 0) {
@@ -178,6 +196,12 @@ static void ln_fwd_launch(hipStream_t s, int64_t M, int D, const float* x, int64
                           const float* gamma, const float* beta, float eps, void* y, int ydt,
                           int64_t ldy, float* mean, float* rstd) {
   dim3 grid((unsigned)((M + 3) / 4));
+  if (ydt == VITMI_BF16X3) {
+    hipLaunchKernelGGL((ln_fwd_kernel<NV, SplitX3>), grid, dim3(256), 0, s, M, D, x, ldx, gamma, beta, eps,
+                       (SplitX3*)y, ldy, mean, rstd);
+    VITMI_STAT((ln_fwd_kernel<NV, SplitX3>), 0, (double)M * D * (4 + 6) + 8.0 * M);
+    return;
+  }
   if (ydt == VITMI_BF16)
     hipLaunchKernelGGL((ln_fwd_kernel<NV, bf16>), grid, dim3(256), 0, s, M, D, x, ldx, gamma, beta,
                        eps, (bf16*)y, ldy, mean, rstd);
@@ -219,6 +243,10 @@ extern "C" int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx
                                    vitmi_stream_t stream) {
   VITMI_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "layernorm: D must be a multiple of 4 in [4, 2048]");
   VITMI_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "layernorm: strides must be multiples of 4");
+  VITMI_CHECK_ARG(y_dtype == VITMI_F32 || y_dtype == VITMI_BF16 || y_dtype == VITMI_BF16X3,
+                  "layernorm_fwd: y dtype must be VITMI_F32, VITMI_BF16 or VITMI_BF16X3");
+  VITMI_CHECK_ARG(ldx >= D && ldy >= (y_dtype == VITMI_BF16X3 ? 3LL * D : (int64_t)D),
+                  "layernorm_fwd: ldx >= D and ldy >= D (3D for VITMI_BF16X3) required");
   if (M == 0) return VITMI_OK;
   VITMI_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;

@@ -48,6 +48,7 @@ SIGNATURES = {
     "vitmi_layernorm_bwd": (I, [L, I, P, I, L, P, L, P, P, P, P, L, P, L, P, L, P, P, P, P, S, P]),
     "vitmi_layernorm_bwd_workspace_size": (S, [L, I]),
     "vitmi_attention_fwd": (I, [I, I, I, I, I, F, P, P, P, P]),
+    "vitmi_attention_fwd_x3": (I, [I, I, I, I, F, P, P, P, P, P]),
     "vitmi_attention_bwd": (I, [I, I, I, I, I, F, P, P, P, P, P, P, S, P]),
     "vitmi_attention_bwd_workspace_size": (S, [I, I, I]),
     "vitmi_patch_im2col": (I, [I, I, I, I, I, P, P, P]),

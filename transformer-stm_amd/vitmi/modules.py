@@ -383,10 +383,11 @@ class _BlockFn(torch.autograd.Function):
     def _forward_x3(ctx, x2, blk, B, N, D, H, drop, wlp):
         """The precision knob's forward (ViTConfig dtype 'bf16x3'; tools/precision_emulate.py):
         the qkv, out-projection, fc1 and fc2 GEMMs take split-bf16 operands (weights and the
-        LayerNorm / attention / GELU outputs as hi + lo, one GEMM over K' = 3K, vitmi_split_bf16x3)
-        and the attention forward runs in fp32 (f32 MFMA).  The backward is the bf16 one, on the
-        hi parts (row-strided views of the split operands), a bf16 copy of qkv and the bf16
-        attention forward's O and lse."""
+        LayerNorm / attention / GELU outputs as hi + lo, one GEMM over K' = 3K).  The LayerNorm
+        and attention kernels write their outputs split (VITMI_BF16X3, vitmi_attention_fwd_x3);
+        q, k, v and the softmax P are bf16 (emulated cost 1.5-1.8e-4 of logits at depth 12).  The
+        backward is the bf16 one, on the hi parts (row-strided views of the split operands) and
+        the attention forward's own bf16 O and lse (so P's rows in the backward sum to 1)."""
         if drop is not None:
             raise ValueError("vitmi: dtype 'bf16x3' is the parity / evaluation knob; dropout is not supported")
         n1, n2 = blk.norm1, blk._norm2
@@ -394,32 +395,29 @@ class _BlockFn(torch.autograd.Function):
 
         def w3(p):
             return ops.split_bf16x3(p.detach(), 1)[0]
-        h1f, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, F32)
-        h1_3, _ = ops.split_bf16x3(h1f, 0)
-        del h1f
-        qkvf = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, F32)
-        of, _ = ops.attention_fwd(qkvf, B, N, H, a_.scale)
-        qkv = ops.cast_bf16(qkvf)
-        del qkvf
-        o3, _ = ops.split_bf16x3(of, 0)
-        del of
-        # the bf16 backward recomputes P from the bf16 q, k: its lse (and the O of delta =
-        # rowsum(dO o O)) must come from the bf16 forward of the same q, k, v, or P's rows would not
-        # sum to 1 and dS would carry a bias (C1 grads 1.7e-2 with the fp32 forward's lse)
-        o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
+        h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, ops.BF16X3)
+        if N <= ops.ATTN_SEQ_MAX:   # q, k, v leave the GEMM epilogue in bf16
+            qkv = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, torch.bfloat16)
+            o, o3, lse = ops.attention_fwd_x3(qkv, B, N, H, a_.scale)
+        else:   # streamed kernels (N > 256): O from the fp32 kernel, o / lse from the bf16 one
+            qkvf = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, F32)
+            qkv = ops.cast_bf16(qkvf)
+            of, _ = ops.attention_fwd(qkvf, B, N, H, a_.scale)
+            del qkvf
+            o3, _ = ops.split_bf16x3(of, 0)
+            del of
+            o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
         x1 = ops.linear_fwd(o3, w3(a_.proj.weight), a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2)
         del o3
-        h2f, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, F32)
-        h2_3, _ = ops.split_bf16x3(h2f, 0)
-        del h2f
-        u = ops.linear_fwd(h2_3, w3(mlp.fc1.weight), mlp.fc1.bias, F32)
-        act3, dg = ops.gelu_split_bf16x3(u)
-        del u
+        h2_3, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, ops.BF16X3)
+        # GELU in the fc1 epilogue, its output split there (VITMI_EPI_SPLIT_X3); gelu' saved in
+        # the tile-native layout of the bf16 path
+        act3, dg = ops.linear_fwd(h2_3, w3(mlp.fc1.weight), mlp.fc1.bias, torch.bfloat16, ops.EPI_BIAS_GELU,
+                                  aux_tiled=True, split_x3=True)
         out = ops.linear_fwd(act3, w3(mlp.fc2.weight), mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
-        # the bf16 backward's operands: hi parts of the split activations (row-strided views),
-        # gelu' row-major (not the tile-native layout of the fused GELU epilogue)
+        # the bf16 backward's operands: hi parts of the split activations (row-strided views)
         h1, h2, act = h1_3[:, :D], h2_3[:, :D], act3[:, :mlp.fc1.weight.shape[0]]
-        ctx.aux_tiled = False
+        ctx.aux_tiled = True
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dg, act, *wlp)
         return out
 

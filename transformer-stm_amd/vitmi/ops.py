@@ -19,6 +19,7 @@ Tensor = torch.Tensor
 F32, BF16 = 0, 1
 EPI_STORE, EPI_BIAS_GELU, EPI_RESIDUAL, EPI_DGELU, EPI_ACCUM = 0, 1, 2, 3, 4
 EPI_AUX_TILED = 0x100   # gelu' in the library's tile-native layout (include/vitmi.h)
+EPI_SPLIT_X3 = 0x200    # BIAS_GELU output as [hi | hi | lo] rows (the precision knob)
 LOSS_CE, LOSS_MSE = 0, 1
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
@@ -111,18 +112,21 @@ def dropout_params(p: float):
 
 def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dtype,
                epilogue: int = EPI_STORE, residual: Optional[Tensor] = None, dropout=None,
-               aux_tiled: bool = False):
+               aux_tiled: bool = False, split_x3: bool = False):
     """y = x W^T + b (+GELU, +residual).  x [M,K], w [N,K] (same dtype).  Returns y
     (and gelu'(pre-activation), the saved GELU derivative, for EPI_BIAS_GELU).
     ``dropout`` = (seed, site, rate) fuses the dropout of the GELU output / of the branch
     before the residual add into the epilogue (vitmi_linear_fwd_dropout).
     ``aux_tiled`` (bf16): gelu' comes back as an opaque buffer in the tile-native layout, for a
-    linear_dgrad(..., EPI_DGELU, aux_tiled=True) of the same [M, N]."""
+    linear_dgrad(..., EPI_DGELU, aux_tiled=True) of the same [M, N].
+    ``split_x3`` (EPI_BIAS_GELU, bf16): y is [M, 3N], each row [hi | hi | lo] of the fp32 GELU
+    output (VITMI_EPI_SPLIT_X3, the precision knob's fc2 A operand)."""
     assert x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N = w.shape[0]
     assert w.shape[1] == K
-    y = torch.empty(*x.shape[:-1], N, dtype=out_dtype, device=x.device)
+    assert not split_x3 or (epilogue == EPI_BIAS_GELU and dropout is None)
+    y = torch.empty(*x.shape[:-1], 3 * N if split_x3 else N, dtype=out_dtype, device=x.device)
     aux = None
     aux_tiled = aux_tiled and epilogue == EPI_BIAS_GELU
     if aux_tiled:
@@ -130,6 +134,8 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
         epilogue |= EPI_AUX_TILED
     elif epilogue == EPI_BIAS_GELU:
         aux = torch.empty(*x.shape[:-1], N, dtype=x.dtype, device=x.device)
+    if split_x3:
+        epilogue |= EPI_SPLIT_X3
     if residual is not None:
         assert residual.is_contiguous() and residual.dtype == torch.float32
     probe = _PROBE is not None and _PROBE["key"] == (M, N, K)
@@ -150,7 +156,7 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
     if probe:
         e1.record()
         _PROBE["events"].append((e0, e1))
-    return (y, aux) if epilogue & ~EPI_AUX_TILED == EPI_BIAS_GELU else y
+    return (y, aux) if epilogue & ~(EPI_AUX_TILED | EPI_SPLIT_X3) == EPI_BIAS_GELU else y
 
 
 def dropout_apply(x: Tensor, seed: int, site: int, rate: float, out_dtype: torch.dtype) -> Tensor:
@@ -239,16 +245,22 @@ def gemm(a: Tensor, b: Tensor, a_kmajor: bool, b_kmajor: bool, M: int, N: int, K
 
 
 # ---------------------------------------------------------------- LayerNorm
-def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype: torch.dtype):
-    """x fp32 [..., D] (rows may be strided) -> (y [rows, D] contiguous, mean, rstd)."""
+BF16X3 = "bf16x3"   # layernorm_fwd out_dtype of the precision knob (VITMI_BF16X3)
+ATTN_SEQ_MAX = 256  # largest N of the whole-sequence attention kernels (csrc/attention.hip SEQ_MAX)
+
+
+def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype):
+    """x fp32 [..., D] (rows may be strided) -> (y [rows, D] contiguous, mean, rstd).
+    out_dtype BF16X3: y is bf16 [rows, 3D], each row [hi | hi | lo] of the fp32 result."""
     assert x.dtype == torch.float32
     M, ldx = _rows(x)
     D = x.shape[-1]
-    y = torch.empty(M, D, dtype=out_dtype, device=x.device)
+    x3 = out_dtype == BF16X3
+    y = torch.empty(M, 3 * D if x3 else D, dtype=torch.bfloat16 if x3 else out_dtype, device=x.device)
     mean = torch.empty(M, dtype=torch.float32, device=x.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x.device)
-    check(lib().vitmi_layernorm_fwd(M, D, _p(x), ldx, _p(w), _p(b), float(eps), _p(y), dt(out_dtype), D,
-                                    _p(mean), _p(rstd), _s()), "layernorm_fwd")
+    check(lib().vitmi_layernorm_fwd(M, D, _p(x), ldx, _p(w), _p(b), float(eps), _p(y), 3 if x3 else dt(out_dtype),
+                                    y.shape[1], _p(mean), _p(rstd), _s()), "layernorm_fwd")
     return y, mean, rstd
 
 
@@ -297,6 +309,19 @@ def attention_fwd(qkv: Tensor, B: int, N: int, H: int, scale: float):
     check(lib().vitmi_attention_fwd(dt(qkv.dtype), B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(lse),
                                     _s()), "attention_fwd")
     return o, lse
+
+
+def attention_fwd_x3(qkv: Tensor, B: int, N: int, H: int, scale: float):
+    """bf16 qkv [B*N, 3*H*64] -> (o bf16 [B*N, H*64], o3 bf16 [B*N, 3*H*64] = [hi | hi | lo] rows of
+    the fp32 output, lse fp32 [B*H, N]); N <= 256.  o and lse are attention_fwd's, bit for bit."""
+    D = qkv.shape[-1] // 3
+    assert qkv.is_contiguous() and qkv.dtype == torch.bfloat16 and qkv.numel() == B * N * 3 * D
+    o = torch.empty(B * N, D, dtype=torch.bfloat16, device=qkv.device)
+    o3 = torch.empty(B * N, 3 * D, dtype=torch.bfloat16, device=qkv.device)
+    lse = torch.empty(B * H, N, dtype=torch.float32, device=qkv.device)
+    check(lib().vitmi_attention_fwd_x3(B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(o3), _p(lse), _s()),
+          "attention_fwd_x3")
+    return o, o3, lse
 
 
 def attention_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, B: int, N: int, H: int,
