@@ -380,12 +380,10 @@ int vitmi_gather_rows(int64_t n, int64_t row_bytes, const void* src, int64_t n_s
  * and the weight rows [hi | lo | hi] (pattern 1).
  *   vitmi_split_bf16x3: src fp32 [rows][ld_src] (K % 4 == 0) -> dst bf16 [rows][ld_dst >= 3K];
  *     hi_copy (optional, bf16 [rows][ld_copy]) receives hi alone (the bf16 operand of the backward).
- *   vitmi_gelu_split_bf16x3: act3 = split(gelu(u)) pattern 0, dgelu = gelu'(u) in bf16 (row-major, the
- *     aux of a DGELU dgrad); u fp32 [rows][N] (the fc1 pre-activation, models/CvT(Par).py:254). */
+ * The activation operands come split straight from their producers: vitmi_layernorm_fwd (y dtype
+ * VITMI_BF16X3), vitmi_attention_fwd_x3 and the fc1 epilogue (VITMI_EPI_SPLIT_X3). */
 int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
                        int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
-int vitmi_gelu_split_bf16x3(int64_t rows, int64_t N, const float* u, void* act3, int64_t ld_act3, void* dgelu,
-                            int64_t ld_dgelu, vitmi_stream_t stream);
 
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);

@@ -22,7 +22,8 @@ stage    ConvEmbed (Conv2D 'same', ``:194-217``)      ConvTransformerBlock (``:2
 * ``ConvAttention.call`` (``:144-191``): q/k/v Dense(D) then MultiHeadAttention(q, v, k) whose
   own query/key/value EinsumDense projections compose with them into one linear each (the
   build holds the composition ``proj_{q,k,v}``), softmax(QK^T / sqrt(D/H)) V, output Dense
-  composed with ``self.proj`` into ``proj``.
+  composed with ``self.proj`` into ``proj``.  ``keras_dense``: both factors of every pair as
+  parameters (``proj_c`` then ``mha_c``; ``mha_o`` then ``proj``), applied one after the other.
 * block: ``x += Attn(LN1(x)); x += MLP(LN1(x))`` with the SAME norm1 used twice (``:248,272,278``).
 * ``Projection('avg')``: AveragePooling2D(3, 1, 'same') for k and v, q stays linear
   (``:95-96,107-108,130-132``); ``'linear'``: identity (``qkv_method`` per stage).
@@ -82,6 +83,7 @@ class CvTConfig:
     proc_hidden: int = 256            # Proc_Dense_1/2 width (:343-344)
     drop_rate: float = 0.0            # Dropout after proj (:141,189) and both MLP Dense (:255,257)
     dtype: str = "bf16"
+    keras_dense: bool = False         # the Dense pairs as separate factors (mha_{q,k,v,o}; see block)
 
     def replace(self, **kw) -> "CvTConfig":
         return dataclasses.replace(self, **kw)
@@ -122,6 +124,10 @@ def param_shapes(cfg: CvTConfig) -> Dict[str, tuple]:
                 s[b + f"attn.proj_{c}.weight"] = (D, D)
                 if cfg.qkv_bias:
                     s[b + f"attn.proj_{c}.bias"] = (D,)
+            if cfg.keras_dense:   # MultiHeadAttention's query/key/value/output EinsumDense (use_bias)
+                for c in "qkvo":
+                    s[b + f"attn.mha_{c}.weight"] = (D, D)
+                    s[b + f"attn.mha_{c}.bias"] = (D,)
             s[b + "attn.proj.weight"] = (D, D)
             s[b + "attn.proj.bias"] = (D,)
             if not cfg.tie_norms:
@@ -220,11 +226,16 @@ def block(x: Tensor, hw: Tuple[int, int], p: Dict[str, Tensor], pre: str, cfg: C
         t = t.flatten(2).transpose(1, 2)
         if cls is not None:
             t = torch.cat([cls, t], dim=1)
-        proj.append(F.linear(t, p[pre + f"attn.proj_{c}.weight"], p.get(pre + f"attn.proj_{c}.bias")))
+        t = F.linear(t, p[pre + f"attn.proj_{c}.weight"], p.get(pre + f"attn.proj_{c}.bias"))
+        if cfg.keras_dense:   # then MHA's own query/key/value projection (:185; Keras MHA internals)
+            t = F.linear(t, p[pre + f"attn.mha_{c}.weight"], p[pre + f"attn.mha_{c}.bias"])
+        proj.append(t)
     q, k, v = (t.reshape(B, N, Hh, dh).transpose(1, 2) for t in proj)
     scale = dh ** -0.5 if cfg.attn_scale == "head" else D ** -0.5
     a = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * scale, dim=-1)
     o = torch.matmul(a, v).transpose(1, 2).reshape(B, N, D)
+    if cfg.keras_dense:       # MHA's output projection, then self.proj (:188)
+        o = F.linear(o, p[pre + "attn.mha_o.weight"], p[pre + "attn.mha_o.bias"])
     x = x + dp(F.linear(o, p[pre + "attn.proj.weight"], p[pre + "attn.proj.bias"]), 0)
     y = F.layer_norm(x, (D,), n2w, n2b, cfg.ln_eps)
     y = dp(F.gelu(F.linear(y, p[pre + "mlp.fc1.weight"], p[pre + "mlp.fc1.bias"])), 1)

@@ -112,3 +112,26 @@ def test_proc_head_is_concat_then_dense():
     W = p["head.weight"]
     ref = f @ W[:, :f.shape[1]].t() + h @ W[:, f.shape[1]:].t() + p["head.bias"]
     assert torch.allclose(cvt_ref.forward(img, p, cfg, proc), ref, atol=1e-5)
+
+
+def test_keras_dense_factors_compose_to_the_held_map():
+    """keras_dense: the oracle applies each Dense pair as two layers (models/CvT(Par).py:
+    132-137,180-188); with the pair composed into one map (W2 W1, W2 b1 + b2) the default oracle
+    gives the same logits -- the forward equivalence the composed build relies on."""
+    cfg = cvt_ref.CvTConfig(img_size=32, num_classes=2, keras_dense=True,
+                            stages=[cvt_ref.CvTStage(16, 7, 4, 1), cvt_ref.CvTStage(32, 3, 2, 2, with_cls_token=True)])
+    p = cvt_ref.init_params(cfg, seed=2)
+    comp = {k: v for k, v in p.items() if ".mha_" not in k}
+    for i in range(len(cfg.stages)):
+        a = f"stage{i}.blocks.0.attn."
+        for c in "qkv":
+            comp[a + f"proj_{c}.weight"] = p[a + f"mha_{c}.weight"] @ p[a + f"proj_{c}.weight"]
+            comp[a + f"proj_{c}.bias"] = p[a + f"mha_{c}.weight"] @ p[a + f"proj_{c}.bias"] + p[a + f"mha_{c}.bias"]
+        comp[a + "proj.weight"] = p[a + "proj.weight"] @ p[a + "mha_o.weight"]
+        comp[a + "proj.bias"] = p[a + "proj.weight"] @ p[a + "mha_o.bias"] + p[a + "proj.bias"]
+    img, _ = cvt_ref.synthetic_batch(cfg, 3, seed=3)
+    with torch.no_grad():
+        y_fact = cvt_ref.forward(img, p, cfg)
+        y_comp = cvt_ref.forward(img, comp, cfg.replace(keras_dense=False))
+    assert set(p) - set(comp) == {k for k in p if ".mha_" in k}
+    assert torch.allclose(y_fact, y_comp, rtol=1e-4, atol=1e-5)

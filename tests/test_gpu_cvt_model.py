@@ -64,7 +64,8 @@ def run_product(pcfg, params, img, tgt, proc=None):
 def test_param_names_match_oracle():
     # pure host check (no kernels): the module tree names every oracle parameter
     for ocfg in (mscvt_cfg(), cvt_ref.CvTConfig(img_size=64), mscvt_avg_cfg(),
-                 with_method(cvt_ref.CvTConfig(img_size=64, proc_dim=5), "linear")):
+                 with_method(cvt_ref.CvTConfig(img_size=64, proc_dim=5), "linear"),
+                 cvt_ref.CvTConfig(img_size=64, keras_dense=True)):
         model = cvt.CvT(product_cfg(ocfg))
         shapes = {k: tuple(p.shape) for k, p in model.named_parameters()}
         assert shapes == {k: tuple(s) for k, s in cvt_ref.param_shapes(ocfg).items()}
@@ -211,3 +212,89 @@ def test_cvt_dropout_matches_oracle(dtype):
     model.eval()                                       # inference: no dropout
     with torch.no_grad():
         assert torch.equal(model(img.to(DEV), proc.to(DEV)), model(img.to(DEV), proc.to(DEV)))
+
+
+def _factored_cfg():
+    # dh = 64 per head (the attention kernels' head dim); 8x8 tokens, then 4x4 + cls
+    return cvt_ref.CvTConfig(img_size=32, num_classes=1, dtype="fp32", keras_dense=True,
+                             stages=[cvt_ref.CvTStage(64, 7, 4, 1), cvt_ref.CvTStage(128, 3, 2, 2, with_cls_token=True)])
+
+
+def test_keras_dense_param_names_match_oracle():
+    # host check: the factored module tree names every factored oracle parameter (mha_{q,k,v,o})
+    ocfg = _factored_cfg()
+    model = cvt.CvT(product_cfg(ocfg))
+    shapes = {k: tuple(p.shape) for k, p in model.named_parameters()}
+    assert shapes == {k: tuple(s) for k, s in cvt_ref.param_shapes(ocfg).items()}
+    assert any(".mha_o." in k for k in shapes)
+
+
+@pytest.mark.gpu
+def test_keras_dense_factored_adam_trajectory_matches_oracle():
+    """CvTConfig.keras_dense (models/CvT(Par).py:132-137,180-188: Dense then MHA's own q/k/v
+    projection; MHA's output projection then Dense): 8 Keras-Adam steps of vitmi.optim.Adam on the
+    factored model against the factored oracle stepped by oracle/optim_ref.adam_step on the same
+    batches (fp32): every parameter's total update within 2e-2 relative (the key biases and the
+    k projection's BN beta in a stage without cls, whose exact gradient is 0 -- softmax ignores a
+    per-row shift of the keys -- excluded, as in test_cvt_keras_spec_vs_oracle).  The composed model (keras_dense=False) started from the same
+    map takes a different trajectory: its out-projection update differs by > 10 %."""
+    from oracle.optim_ref import adam_step
+    from vitmi.optim import Adam
+    ocfg = _factored_cfg()
+    params = cvt_ref.init_params(ocfg, seed=11)
+    model = cvt.CvT(product_cfg(ocfg)).to(DEV)
+    model.load_param_dict(params)
+    model.train()
+    opt = Adam(model.parameters(), learning_rate=1e-3)
+    p = {k: v.numpy().copy() for k, v in params.items()}
+    m = {k: np.zeros_like(v) for k, v in p.items()}
+    v_ = {k: np.zeros_like(v) for k, v in p.items()}
+    # the composed model from the same initial map
+    comp_params = {}
+    for k, t in params.items():
+        if ".mha_" in k:
+            continue
+        comp_params[k] = t
+    for i in range(len(ocfg.stages)):
+        pre = f"stage{i}.blocks.0.attn."
+        for c in "qkv":
+            W1, b1 = params[pre + f"proj_{c}.weight"], params[pre + f"proj_{c}.bias"]
+            W2, b2 = params[pre + f"mha_{c}.weight"], params[pre + f"mha_{c}.bias"]
+            comp_params[pre + f"proj_{c}.weight"] = W2 @ W1
+            comp_params[pre + f"proj_{c}.bias"] = W2 @ b1 + b2
+        W1, b1 = params[pre + "mha_o.weight"], params[pre + "mha_o.bias"]
+        W2, b2 = params[pre + "proj.weight"], params[pre + "proj.bias"]
+        comp_params[pre + "proj.weight"] = W2 @ W1
+        comp_params[pre + "proj.bias"] = W2 @ b1 + b2
+    comp = cvt.CvT(product_cfg(ocfg.replace(keras_dense=False))).to(DEV)
+    comp.load_param_dict(comp_params)
+    comp.train()
+    copt = Adam(comp.parameters(), learning_rate=1e-3)
+    for step in range(1, 9):
+        img, tgt = cvt_ref.synthetic_batch(ocfg, 4, seed=100 + step)
+        for mod, o in ((model, opt), (comp, copt)):
+            o.zero_grad()
+            mse_loss(mod(img.to(DEV)), tgt.to(DEV)).backward()
+            o.step()
+        _, _, g = cvt_ref.forward_backward(img, tgt, {k: torch.from_numpy(t) for k, t in p.items()}, ocfg)
+        for k in p:
+            p[k], m[k], v_[k] = adam_step(p[k], g[k].numpy(), m[k], v_[k], 1e-3, step)
+    torch.cuda.synchronize()
+    got = {k: t.detach().cpu() for k, t in model.named_parameters()}
+    zero = [k for k in p if k.endswith("attn.proj_k.bias") or k.endswith("attn.mha_k.bias") or (
+        k.endswith("attn.conv_proj_k.bn.bias") and not ocfg.stages[int(k[5])].with_cls_token)]
+    bad = {}
+    for k in p:
+        if k in zero:
+            continue
+        d_ref = torch.from_numpy(p[k]) - params[k]
+        r = rel(got[k] - params[k], d_ref, 1e-6)
+        if r >= 2e-2:
+            bad[k] = r
+    assert not bad, bad
+    # the composed trajectory: compare the out-projection maps after 8 steps
+    pre = "stage1.blocks.0.attn."
+    Wf = got[pre + "proj.weight"] @ got[pre + "mha_o.weight"]
+    Wc = dict(comp.named_parameters())[pre + "proj.weight"].detach().cpu()
+    W0 = comp_params[pre + "proj.weight"]
+    assert rel(Wc - W0, Wf - W0) > 0.1

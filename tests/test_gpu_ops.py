@@ -495,18 +495,6 @@ def test_bf16x3_gemm_is_fp32_accurate():
     assert e3 < 3e-5 and e1 > 20 * e3, (e3, e1)
 
 
-def test_gelu_split_bf16x3():
-    u = (rnd(197 * 2, 3072, seed=94) * 3).to(DEV)
-    act3, dg = ops.gelu_split_bf16x3(u)
-    ref = torch.nn.functional.gelu(u.double())
-    got = act3[:, :3072].double() + act3[:, 6144:].double()
-    assert torch.equal(act3[:, :3072], act3[:, 3072:6144])
-    assert ((got - ref).abs() <= ref.abs() * 2e-5 + 1e-6).all()
-    t = u.double()
-    dref = 0.5 * (1 + torch.erf(t / 2 ** 0.5)) + t * torch.exp(-0.5 * t * t) / (2 * torch.pi) ** 0.5
-    assert ((dg.double() - dref).abs() <= dref.abs() * 8e-3 + 1e-3).all()
-
-
 @pytest.mark.parametrize("M,N,K", [(197 * 8, 3072, 3 * 768), (50, 256, 3 * 192), (197 * 2, 520, 3 * 64)])
 def test_linear_fwd_gelu_split_x3(M, N, K):
     """VITMI_EPI_SPLIT_X3: the fc1 epilogue writes the GELU output as [hi | hi | lo] rows.  hi and
@@ -516,10 +504,14 @@ def test_linear_fwd_gelu_split_x3(M, N, K):
     x = rnd(M, K, seed=101).to(DEV).to(BF)
     w = (rnd(N, K, seed=102) * 0.05).to(DEV).to(BF)
     b = (rnd(N, seed=103) * 0.5).to(DEV)
-    y3, g3 = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, aux_tiled=True, split_x3=True)
-    y1, g1 = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, aux_tiled=True)
+    y3, g3 = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, split_x3=True)
+    y1, g1 = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU)
     assert y3.shape == (M, 3 * N)
     assert torch.equal(y3[:, :N], y1) and torch.equal(y3[:, N:2 * N], y1) and torch.equal(g3, g1)
+    # with the tile-native gelu' (the model's form; the opaque buffer's padding rows are not
+    # compared): the same split output
+    y3t, _ = ops.linear_fwd(x, w, b, BF, ops.EPI_BIAS_GELU, aux_tiled=True, split_x3=True)
+    assert torch.equal(y3t, y3)
     u = ops.linear_fwd(x, w, b, torch.float32).double()
     ref = torch.nn.functional.gelu(u)
     got = y3[:, :N].double() + y3[:, 2 * N:].double()

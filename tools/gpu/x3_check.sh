@@ -11,3 +11,5 @@ timeout -k 10 400 python3 -u -m pytest tests/test_gpu_model.py -k "bf16x3" -x -q
 grep -E "logits|worst|passed|failed" gpurun_out/$tag/model.log
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-evidence --no-secondary --dtype bf16x3 --steps 10 --warmup 3 > gpurun_out/$tag/bench.json 2> gpurun_out/$tag/bench.err || exit 1
 cut -c1-300 gpurun_out/$tag/bench.json
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_cvt_model.py -x -q --timeout 200 --timeout-method thread > gpurun_out/$tag/cvt.log 2>&1 || { tail -30 gpurun_out/$tag/cvt.log; exit 1; }
+tail -2 gpurun_out/$tag/cvt.log

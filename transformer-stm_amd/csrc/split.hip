@@ -9,7 +9,9 @@
 // (lo.lo is below fp32 rounding), and the GEMM kernels do them unchanged as ONE GEMM over
 // K' = 3K: the A operand's rows are laid out [hi | hi | lo] and the weight's [hi | lo | hi].
 //
-// Both kernels are HBM-bound streams: 16-B loads, 8-B stores, 4 columns per thread.
+// The weights (and the patch-embedding im2col rows) are split here; the activation operands come
+// split from their producers (LayerNorm, attention, the fc1 epilogue).  An HBM-bound stream:
+// 16-B loads, 8-B stores, 4 columns per thread.
 #include "common.h"
 
 namespace vitmi {
@@ -39,32 +41,6 @@ __global__ __launch_bounds__(256) void split3_kernel(int64_t rows, int64_t K, co
   }
 }
 
-// act = gelu(u) (exact erf, fp32) split [hi | hi | lo]; dgelu = gelu'(u) in bf16 (the saved
-// operand of the DGELU backward epilogue, row-major)
-__global__ __launch_bounds__(256) void gelu_split3_kernel(int64_t rows, int64_t N, const float* __restrict__ u,
-                                                          bf16* __restrict__ act, int64_t ld_act,
-                                                          bf16* __restrict__ dg, int64_t ld_dg) {
-  const int64_t N4 = N / 4, total = rows * N4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / N4, c = (i - r * N4) * 4;
-    const f32x4 x = *(const f32x4*)(u + r * N + c);
-    f32x4 a;
-    bf16x4 g;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      a[e] = gelu_f(x[e]);
-      g[e] = (bf16)gelu_grad_f(x[e]);
-    }
-    bf16x4 hi, lo;
-    split4(a, hi, lo);
-    bf16* d = act + r * ld_act + c;
-    *(bf16x4*)d = hi;
-    *(bf16x4*)(d + N) = hi;
-    *(bf16x4*)(d + 2 * N) = lo;
-    *(bf16x4*)(dg + r * ld_dg + c) = g;
-  }
-}
-
 static unsigned grid_of(int64_t items) {
   int64_t b = (items + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -89,21 +65,5 @@ extern "C" int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int
                      ld_src, (bf16*)dst, ld_dst, pattern, (bf16*)hi_copy, ld_copy);
   VITMI_LAUNCH_CHECK("split_bf16x3");
   VITMI_STAT(split3_kernel, 0, (double)rows * K * (4 + 6 + (hi_copy ? 2 : 0)));
-  return VITMI_OK;
-}
-
-extern "C" int vitmi_gelu_split_bf16x3(int64_t rows, int64_t N, const float* u, void* act3, int64_t ld_act3,
-                                       void* dgelu, int64_t ld_dgelu, vitmi_stream_t stream) {
-  VITMI_CHECK_ARG(rows >= 0 && N > 0 && N % 4 == 0, "gelu_split_bf16x3: N must be a positive multiple of 4");
-  VITMI_CHECK_ARG(ld_act3 >= 3 * N && ld_act3 % 4 == 0 && ld_dgelu >= N && ld_dgelu % 4 == 0,
-                  "gelu_split_bf16x3: bad strides");
-  if (rows == 0) return VITMI_OK;
-  VITMI_CHECK_ARG(u && act3 && dgelu, "gelu_split_bf16x3: null pointer");
-  VITMI_CHECK_ARG(((uintptr_t)u % 16) == 0 && ((uintptr_t)act3 % 8) == 0 && ((uintptr_t)dgelu % 8) == 0,
-                  "gelu_split_bf16x3: alignment");
-  hipLaunchKernelGGL(gelu_split3_kernel, dim3(grid_of(rows * N / 4)), dim3(256), 0, (hipStream_t)stream, rows, N, u,
-                     (bf16*)act3, ld_act3, (bf16*)dgelu, ld_dgelu);
-  VITMI_LAUNCH_CHECK("gelu_split_bf16x3");
-  VITMI_STAT(gelu_split3_kernel, 0, (double)rows * N * (4 + 6 + 2));
   return VITMI_OK;
 }

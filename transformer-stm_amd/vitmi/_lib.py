@@ -61,7 +61,6 @@ SIGNATURES = {
     "vitmi_split_bf16x3": (I, [L, L, P, L, P, L, I, P, L, P]),
     "vitmi_fold_begin": (I, []),
     "vitmi_fold_end": (I, [P]),
-    "vitmi_gelu_split_bf16x3": (I, [L, L, P, P, L, P, L, P]),
     "vitmi_dropout_hash": (U, [U, U, U, U]),
     "vitmi_linear_fwd_dropout": (I, [I, L, L, L, P, P, P, P, I, I, P, P, P, S, U, U, U, F, P]),
     "vitmi_dropout_apply": (I, [L, L, P, L, P, I, L, U, U, U, F, P]),

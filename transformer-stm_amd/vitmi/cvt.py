@@ -80,6 +80,14 @@ class CvTConfig:
     # Keras default 0.1 in training.  0 = the parity / benchmark configuration.
     drop_rate: float = 0.0
     dtype: str = "bf16"
+    # Keras' stacked Dense pairs as separate parameters (models/CvT(Par).py:132-137,180-188): the
+    # q/k/v Dense then MultiHeadAttention's query/key/value projection, and MHA's output
+    # projection then self.proj.  False: each pair is ONE linear map (their composition; the same
+    # forward, fewer parameters, a different Adam trajectory).  True: both factors are parameters
+    # (attn.proj_{q,k,v} / attn.mha_{q,k,v}, attn.mha_o / attn.proj); every forward composes them
+    # (fp32 GEMMs, D^3 each) and the backward hands each factor its chain-rule gradient, so Adam
+    # steps the same parameters Keras does.
+    keras_dense: bool = False
 
     def replace(self, **kw) -> "CvTConfig":
         return dataclasses.replace(self, **kw)
@@ -186,15 +194,65 @@ class DwBnProjection(nn.Module):
 
 
 class CvTAttention(nn.Module):
-    def __init__(self, dim: int, num_heads: int, qkv_bias: bool, methods=("dw_bn",) * 3):
+    def __init__(self, dim: int, num_heads: int, qkv_bias: bool, methods=("dw_bn",) * 3, keras_dense: bool = False):
         super().__init__()
         self.num_heads = num_heads
         self.methods = tuple(methods)
+        self.keras_dense = keras_dense
         for c, m in zip("qkv", self.methods):
             if m == "dw_bn":
                 setattr(self, f"conv_proj_{c}", DwBnProjection(dim))
         self.proj_q, self.proj_k, self.proj_v = (Linear(dim, dim, bias=qkv_bias) for _ in range(3))
+        if keras_dense:   # MultiHeadAttention's own EinsumDense projections (use_bias=True)
+            self.mha_q, self.mha_k, self.mha_v, self.mha_o = (Linear(dim, dim) for _ in range(4))
         self.proj = Linear(dim, dim)
+
+    def linear_pair(self, c: str):
+        """(outer, inner) Linear modules of projection c ('q', 'k', 'v' or 'o'): the map applied
+        is outer(inner(x)).  None for inner when the pair is held composed."""
+        if c == "o":
+            return self.proj, (self.mha_o if self.keras_dense else None)
+        lin = getattr(self, f"proj_{c}")
+        return (getattr(self, f"mha_{c}"), lin) if self.keras_dense else (lin, None)
+
+
+def _compose(outer: Linear, inner: Linear):
+    """W = W_outer W_inner, b = W_outer b_inner + b_outer (fp32, the library's fp32 GEMM)."""
+    A, B = outer.weight.detach(), inner.weight.detach()
+    D_out, D_mid = A.shape
+    D_in = B.shape[1]
+    W = torch.empty(D_out, D_in, dtype=F32, device=A.device)
+    ops.gemm(A, B, True, False, D_out, D_in, D_mid, W)                      # W[o, i] = sum_j A[o, j] B[j, i]
+    b = torch.empty(1, D_out, dtype=F32, device=A.device)
+    bi = inner.bias.detach() if inner.bias is not None else torch.zeros(D_mid, device=A.device)
+    ops.gemm(bi.view(1, D_mid), A, True, True, 1, D_out, D_mid, b, bias=outer.bias)   # b[o] = sum_j A[o, j] bi[j] + bo[o]
+    return W, b.view(D_out)
+
+
+def _chain(outer: Linear, inner: Linear, G: Tensor, gb: Tensor, gs) -> None:
+    """The factors' gradients from the composed map's (G = dL/dW, gb = dL/db):
+    dW_outer += G W_inner^T + gb b_inner^T, dW_inner += W_outer^T G, db_outer += gb,
+    db_inner += W_outer^T gb (all fp32 GEMMs of the library; the outer product rides in the
+    first GEMM as one extra, zero-padded K column)."""
+    A, B = outer.weight.detach(), inner.weight.detach()
+    D_out, D_mid = A.shape
+    D_in = B.shape[1]
+    if gs.wants(outer.weight):
+        Kp = D_in + 32
+        Gp = torch.zeros(D_out, Kp, dtype=F32, device=G.device)
+        Bp = torch.zeros(D_mid, Kp, dtype=F32, device=G.device)
+        Gp[:, :D_in] = G
+        Bp[:, :D_in] = B
+        if inner.bias is not None:
+            Gp[:, D_in] = gb
+            Bp[:, D_in] = inner.bias.detach()
+        ops.gemm(Gp, Bp, True, True, D_out, D_mid, Kp, gs(outer.weight), ops.EPI_ACCUM)
+    if gs.wants(inner.weight):
+        ops.gemm(A, G, False, False, D_mid, D_in, D_out, gs(inner.weight), ops.EPI_ACCUM)
+    if gs.wants(outer.bias):
+        gs(outer.bias).add_(gb)
+    if inner.bias is not None and gs.wants(inner.bias):
+        ops.gemm(gb.view(1, D_out), A, True, False, 1, D_mid, D_out, gs(inner.bias).view(1, D_mid), ops.EPI_ACCUM)
 
 
 class _Mlp(nn.Module):
@@ -210,7 +268,7 @@ class CvTBlock(nn.Module):
     def __init__(self, dim: int, num_heads: int, cfg: CvTConfig, methods=("dw_bn",) * 3):
         super().__init__()
         self.norm1 = LayerNorm(dim, cfg.ln_eps)
-        self.attn = CvTAttention(dim, num_heads, cfg.qkv_bias, methods)
+        self.attn = CvTAttention(dim, num_heads, cfg.qkv_bias, methods, cfg.keras_dense)
         self.tie_norms = cfg.tie_norms
         if not cfg.tie_norms:
             self.norm2 = LayerNorm(dim, cfg.ln_eps)
@@ -249,8 +307,14 @@ class _CvTBlockFn(torch.autograd.Function):
         qkv = torch.empty(M, 3 * D, dtype=T, device=x.device)
         saved_proj = []
         h_lp = None
+        def weight_of(c):
+            """(operand weight in T, bias) of projection c: the Linear's, or the composed pair's"""
+            outer, inner = a_.linear_pair(c)
+            if inner is None:
+                return _lp(blk, outer.weight, T), outer.bias
+            W, b = _compose(outer, inner)
+            return (W if T == F32 else ops.cast_bf16(W)), b
         for c_i, (c, meth) in enumerate(zip("qkv", a_.methods)):
-            lin = getattr(a_, f"proj_{c}")
             z = mean = rstd = None
             if meth == "linear":                       # identity projection: the LN output itself
                 if h_lp is None:
@@ -268,15 +332,15 @@ class _CvTBlockFn(torch.autograd.Function):
                 else:                                  # 'avg'
                     ops.avgpool3_fwd(h, B, H, W, inp, x_img=N, x_off=off, y_img=N, y_off=off,
                                      count_pad=cfg.avg_count_pad)
-            wl = _lp(blk, lin.weight, T)
-            ops.gemm(inp, wl, True, True, M, D, D, qkv[:, c_i * D:(c_i + 1) * D], ops.EPI_STORE, bias=lin.bias)
+            wl, bl = weight_of(c)
+            ops.gemm(inp, wl, True, True, M, D, D, qkv[:, c_i * D:(c_i + 1) * D], ops.EPI_STORE, bias=bl)
             saved_proj += [inp, z, mean, rstd, wl]
         o, lse = ops.attention_fwd(qkv, B, N, Hh, scale)
         dr = [None, None, None]
         if drop is not None:   # (seed, rate, site0): sites site0 (proj), +1 (GELU), +2 (fc2)
             dr = [(drop[0], drop[2] + j, drop[1]) for j in range(3)]
-        wo = _lp(blk, a_.proj.weight, T)
-        x1 = ops.linear_fwd(o, wo, a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
+        wo, bo = weight_of("o")
+        x1 = ops.linear_fwd(o, wo, bo, F32, ops.EPI_RESIDUAL, residual=x2, dropout=dr[0])
         h2, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, cfg.ln_eps, T)
         w1, w2 = _lp(blk, blk.mlp.fc1.weight, T), _lp(blk, blk.mlp.fc2.weight, T)
         act, u = ops.linear_fwd(h2, w1, blk.mlp.fc1.bias, T, ops.EPI_BIAS_GELU, dropout=dr[1],
@@ -322,24 +386,43 @@ class _CvTBlockFn(torch.autograd.Function):
             dx1_lp = ops.dropout_apply(dx1, drop[0], drop[2], drop[1], T)
         elif dx1_lp is None:
             dx1_lp = dx1
+        def grads_of(c):
+            """(wants W, wants b, dW dst, db dst) of projection c's applied map: the Linear's own
+            gradients, or zeroed buffers of the composed map that chain_of passes to the factors"""
+            outer, inner = a_.linear_pair(c)
+            if inner is None:
+                return gs.wants(outer.weight), gs.wants(outer.bias), gs(outer.weight), gs(outer.bias)
+            if not any(gs.wants(p) for p in (outer.weight, outer.bias, inner.weight, inner.bias)):
+                return False, False, None, None
+            Dn = outer.weight.shape[0]
+            return (True, True, torch.zeros(Dn, inner.weight.shape[1], dtype=F32, device=g2.device),
+                    torch.zeros(Dn, dtype=F32, device=g2.device))
+
+        def chain_of(c, G, gb):
+            outer, inner = a_.linear_pair(c)
+            if inner is not None and G is not None:
+                _chain(outer, inner, G, gb, gs)
         # attention + out-projection
         do = ops.linear_dgrad(dx1_lp, wo, T)
-        if gs.wants(a_.proj.weight):
-            ops.linear_wgrad(dx1_lp, o, gs(a_.proj.weight))
-        if gs.wants(a_.proj.bias):
-            ops.bias_grad(dx1_lp, gs(a_.proj.bias))
+        ww, wb, dWo, dbo = grads_of("o")
+        if ww:
+            ops.linear_wgrad(dx1_lp, o, dWo)
+        if wb:
+            ops.bias_grad(dx1_lp, dbo)
+        chain_of("o", dWo, dbo)
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, scale)
         # q/k/v GEMMs, the cls rows, dw_bn: all into the LN1-output gradient dh
         dh = torch.zeros(M, D, dtype=torch.float32, device=g2.device)
         for c_i, (c, meth) in enumerate(zip("qkv", a_.methods)):
             inp, z, mean, rstd, wl = sp[5 * c_i:5 * c_i + 5]
-            lin = getattr(a_, f"proj_{c}")
             dq = dqkv[:, c_i * D:(c_i + 1) * D].contiguous()
             dinp = ops.linear_dgrad(dq, wl, F32)
-            if gs.wants(lin.weight):
-                ops.linear_wgrad(dq, inp, gs(lin.weight))
-            if gs.wants(lin.bias):
-                ops.bias_grad(dq, gs(lin.bias))
+            ww, wb, dW, db_ = grads_of(c)
+            if ww:
+                ops.linear_wgrad(dq, inp, dW)
+            if wb and db_ is not None:
+                ops.bias_grad(dq, db_)
+            chain_of(c, dW, db_)
             if meth == "linear":
                 dh.add_(dinp)
                 continue
@@ -507,7 +590,8 @@ class CvT(nn.Module):
         return _CvTHeadFn.apply(f, self.head, self.head.weight, self.head.bias)
 
     def reset_parameters(self, seed: int = 0) -> None:
-        """Keras initialisers: glorot_uniform kernels (Dense, Conv2D, DepthwiseConv2D), zero
+        """Keras initialisers: glorot_uniform kernels (Dense, Conv2D, DepthwiseConv2D; the
+        MultiHeadAttention EinsumDense kernels with Keras' fans of their 3-d shapes), zero
         biases / betas / cls token, unit gammas."""
         g = torch.Generator().manual_seed(seed)
         with torch.no_grad():
@@ -524,6 +608,9 @@ class CvT(nn.Module):
                     fan_in, fan_out = p.shape[1] * rf, p.shape[0] * rf
                     if "conv_proj" in name:               # depthwise: one input channel per filter
                         fan_in, fan_out = rf, rf
+                    if ".mha_" in name:   # EinsumDense kernels [D, H, dh] (q/k/v) and [H, dh, D] (output)
+                        D, Hh = p.shape[0], self.cfg.stages[int(name[5:name.index(".")])].num_heads
+                        fan_in, fan_out = (D, D * Hh) if ".mha_o." in name else (Hh * D, (D // Hh) * D)
                     lim = (6.0 / (fan_in + fan_out)) ** 0.5
                     t = (torch.rand(p.shape, generator=g) * 2 - 1) * lim
                 p.copy_(t.to(p.device))

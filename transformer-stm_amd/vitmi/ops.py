@@ -502,18 +502,6 @@ def split_bf16x3(x: Tensor, pattern: int, hi_copy: bool = False):
     return x3, hi
 
 
-def gelu_split_bf16x3(u: Tensor):
-    """u fp32 [rows, N] (the fc1 pre-activation) -> (split(gelu(u)) [rows, 3N] as [hi | hi | lo],
-    gelu'(u) bf16 [rows, N] row-major)."""
-    assert u.dtype == torch.float32 and u.is_contiguous()
-    N = u.shape[-1]
-    rows = u.numel() // N
-    act3 = torch.empty(rows, 3 * N, dtype=torch.bfloat16, device=u.device)
-    dg = torch.empty(rows, N, dtype=torch.bfloat16, device=u.device)
-    check(lib().vitmi_gelu_split_bf16x3(rows, N, _p(u), _p(act3), 3 * N, _p(dg), N, _s()), "gelu_split_bf16x3")
-    return act3, dg
-
-
 def cast_f32(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
     """bf16 -> fp32 (vitmi_cast_bf16_f32)."""
     assert src.dtype == torch.bfloat16 and src.is_contiguous()
