@@ -6,6 +6,7 @@ cd $GRAFT_REPO_ROOT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 tag=${1:-r04}
 mkdir -p gpurun_out/$tag
+timeout -k 10 120 python3 tools/host_overhead.py > gpurun_out/$tag/host.log 2>&1 || exit 1
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -rs --timeout 240 --timeout-method thread > gpurun_out/$tag/test.log 2>&1 || { tail -30 gpurun_out/$tag/test.log; exit 1; }
 tail -3 gpurun_out/$tag/test.log
 bash tools/gpu/bench.sh $tag
