@@ -32,30 +32,62 @@ __device__ __forceinline__ void adam1(const AdamArgs& a, float& p, float g, floa
   p = __fsub_rn(p, __fdiv_rn(__fmul_rn(m, a.alpha), den));
 }
 
+// VITMI_ADAM_NT: streaming (non-temporal) loads and stores, two 16-B groups per thread in flight:
+// 573-595 -> 504-526 us per ViT-B step (tools/ln_bench.py, same box; gpurun_out r04_ln A/B)
+#ifndef VITMI_ADAM_NT
+#define VITMI_ADAM_NT 1
+#endif
+template <typename V>
+__device__ __forceinline__ V ld_s(const V* q) {
+  if constexpr (VITMI_ADAM_NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <typename V>
+__device__ __forceinline__ void st_s(V* q, V x) {
+  if constexpr (VITMI_ADAM_NT) __builtin_nontemporal_store(x, q);
+  else *q = x;
+}
+
 template <bool LP>
 __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16* __restrict__ lp, AdamArgs a) {
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 pv = ((const f32x4*)p)[i], gv = ((const f32x4*)g)[i], mv = ((const f32x4*)m)[i], vv = ((const f32x4*)v)[i];
+  constexpr int U = VITMI_ADAM_NT ? 2 : 1;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += U * stride) {
+    f32x4 pv[U], gv[U], mv[U], vv[U];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pv[e], me = mv[e], ve = vv[e];
-      adam1(a, pe, gv[e], me, ve);
-      pv[e] = pe;
-      mv[e] = me;
-      vv[e] = ve;
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (u == 0 || i < n4) {
+        pv[u] = ld_s((const f32x4*)p + i);
+        gv[u] = ld_s((const f32x4*)g + i);
+        mv[u] = ld_s((const f32x4*)m + i);
+        vv[u] = ld_s((const f32x4*)v + i);
+      }
     }
-    ((f32x4*)p)[i] = pv;
-    ((f32x4*)m)[i] = mv;
-    ((f32x4*)v)[i] = vv;
-    if constexpr (LP) {
-      bf16x4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = from_f32<bf16>(pv[e]);
-      ((bf16x4*)lp)[i] = o;
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (u > 0 && i >= n4) break;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pe = pv[u][e], me = mv[u][e], ve = vv[u][e];
+        adam1(a, pe, gv[u][e], me, ve);
+        pv[u][e] = pe;
+        mv[u][e] = me;
+        vv[u][e] = ve;
+      }
+      st_s((f32x4*)p + i, pv[u]);
+      st_s((f32x4*)m + i, mv[u]);
+      st_s((f32x4*)v + i, vv[u]);
+      if constexpr (LP) {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = from_f32<bf16>(pv[u][e]);
+        ((bf16x4*)lp)[i] = o;
+      }
     }
   }
   // tail (n % 4) by the first threads
