@@ -298,3 +298,29 @@ def test_keras_dense_factored_adam_trajectory_matches_oracle():
     Wc = dict(comp.named_parameters())[pre + "proj.weight"].detach().cpu()
     W0 = comp_params[pre + "proj.weight"]
     assert rel(Wc - W0, Wf - W0) > 0.1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_keras_dense_one_step_grads_match_oracle(dtype):
+    """keras_dense forward + backward against the factored oracle: logits and every factor's
+    gradient (the chain-rule GEMMs of vitmi.cvt._chain) at the fp32 / bf16 bounds of
+    test_cvt_keras_spec_vs_oracle; the key biases (exact gradient 0) bounded against the query's."""
+    ocfg = _factored_cfg().replace(num_classes=3)
+    params = cvt_ref.init_params(ocfg, seed=13)
+    img, tgt = cvt_ref.synthetic_batch(ocfg, 4, seed=14)
+    logits_ref, loss_ref, gref = cvt_ref.forward_backward(img, tgt, params, ocfg)
+    _, logits, loss, grads = run_product(product_cfg(ocfg, dtype), params, img, tgt)
+    tl, tg = (1e-4, 1e-3) if dtype == "fp32" else (3e-2, 8e-2)
+    assert rel(logits, logits_ref) < tl
+    bad = {}
+    for k, g in gref.items():
+        if k.endswith("attn.proj_k.bias") or k.endswith("attn.mha_k.bias") or (
+                k.endswith("attn.conv_proj_k.bn.bias") and not ocfg.stages[int(k[5])].with_cls_token):
+            kq = k.replace("_k.", "_q.")
+            r = grads[k].norm().item() / max(grads[kq].norm().item(), 1e-30)
+        else:
+            r = rel(grads[k], g, 1e-4)
+        if r >= tg:
+            bad[k] = r
+    assert not bad, bad
