@@ -305,7 +305,11 @@ def test_keras_dense_factored_adam_trajectory_matches_oracle():
 def test_keras_dense_one_step_grads_match_oracle(dtype):
     """keras_dense forward + backward against the factored oracle: logits and every factor's
     gradient (the chain-rule GEMMs of vitmi.cvt._chain) at the fp32 / bf16 bounds of
-    test_cvt_keras_spec_vs_oracle; the key biases (exact gradient 0) bounded against the query's."""
+    test_cvt_keras_spec_vs_oracle.  The key biases have an exact gradient of 0 (softmax ignores a
+    per-row shift of the keys): their error is bounded against the matching query bias gradient.
+    The k projection's BN beta is such a shift too except for the cls key, which bypasses the BN
+    (17 tokens here): its gradient nearly cancels, so its error is bounded against the norm of
+    the same BN's gamma gradient."""
     ocfg = _factored_cfg().replace(num_classes=3)
     params = cvt_ref.init_params(ocfg, seed=13)
     img, tgt = cvt_ref.synthetic_batch(ocfg, 4, seed=14)
@@ -315,10 +319,11 @@ def test_keras_dense_one_step_grads_match_oracle(dtype):
     assert rel(logits, logits_ref) < tl
     bad = {}
     for k, g in gref.items():
-        if k.endswith("attn.proj_k.bias") or k.endswith("attn.mha_k.bias") or (
-                k.endswith("attn.conv_proj_k.bn.bias") and not ocfg.stages[int(k[5])].with_cls_token):
+        if k.endswith("attn.proj_k.bias") or k.endswith("attn.mha_k.bias"):
             kq = k.replace("_k.", "_q.")
-            r = grads[k].norm().item() / max(grads[kq].norm().item(), 1e-30)
+            r = (grads[k].detach().cpu() - g).norm().item() / gref[kq].norm().item()
+        elif k.endswith("attn.conv_proj_k.bn.bias"):
+            r = (grads[k].detach().cpu() - g).norm().item() / gref[k.replace("bn.bias", "bn.weight")].norm().item()
         else:
             r = rel(grads[k], g, 1e-4)
         if r >= tg:

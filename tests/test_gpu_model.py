@@ -346,6 +346,28 @@ def test_vit_b_precision_knob_bf16x3_meets_1e3():
     print(f"ViT-B/16 bf16x3 depth 12 bs 2: logits max-abs {err:.3e}, worst grad {worst[1]} rel {worst[0]:.3e}")
 
 
+def test_bf16x3_knob_streamed_attention_n290():
+    """bf16x3 at N > 256 (ViT-Ti/16 at 272 px, N = 290): the whole-sequence x3 attention does not
+    apply, the knob takes O from the fp32 streamed attention forward and o / lse from the bf16
+    one (vitmi/modules.py _forward_x3); logits within 1e-3 of the fp32 oracle at depth 4.  The
+    backward is the bf16 one: at this shape the bias gradients nearly cancel (|d norm1.bias| ~
+    2e-3, measured relative error 0.23 for plain bf16 and for the knob alike, fp32 5e-5), so the
+    gradients are held to the bf16 path's own error on the same inputs."""
+    cfg = config_c1(dtype="bf16x3", img_size=272, depth=4)
+    params = vit_ref.init_params(cfg, seed=8)
+    img, tgt = vit_ref.synthetic_batch(cfg, 2)
+    l_ref, _, g_ref = vit_ref.forward_backward(img, tgt, params, cfg)
+    worst = {}
+    for c in (cfg.replace(dtype="bf16"), cfg):
+        l, _, g = gpu_step(c, params, img, tgt)
+        worst[c.dtype] = max(vit_ref.rel_err(g[k], g_ref[k]) for k in g_ref)
+        if c.dtype == "bf16x3":
+            err = (l - l_ref).abs().max().item()
+    print(f"N=290 bf16x3: logits {err:.3e}; worst grad rel bf16x3 {worst['bf16x3']:.3e}, bf16 {worst['bf16']:.3e}")
+    assert err <= 1e-3
+    assert worst["bf16x3"] <= 1.25 * worst["bf16"] + 1e-2
+
+
 def test_bf16x3_knob_small_model_matches_oracle():
     """bf16x3 on the C1 shape (ViT-Ti/16 64^2, N = 17) and on a ragged token count (48^2, N = 10):
     logits within the north star's 1e-3 (C1 measures 3.3e-4: the bf16 q, k, v and P), gradients
