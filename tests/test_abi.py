@@ -44,6 +44,30 @@ def test_host_validation_rejects_bad_shapes():
     assert rc == 1
 
 
+def test_precision_knob_entry_points_validate_on_the_host():
+    """The split-operand paths of the bf16x3 knob reject bad arguments before any launch."""
+    lib = _lib.lib()
+    # VITMI_BF16X3 LayerNorm output needs ldy >= 3D
+    rc = lib.vitmi_layernorm_fwd(4, 64, 16, 64, 16, 16, 1e-6, 16, 3, 64, 16, 16, None)
+    assert rc == 1 and b"3D" in lib.vitmi_last_error()
+    # an unknown LayerNorm output dtype
+    rc = lib.vitmi_layernorm_fwd(4, 64, 16, 64, 16, 16, 1e-6, 16, 7, 64, 16, 16, None)
+    assert rc == 1 and b"dtype" in lib.vitmi_last_error()
+    # the x3 attention forward serves the whole-sequence kernels only (N <= 256)
+    rc = lib.vitmi_attention_fwd_x3(1, 300, 2, 64, 0.125, 16, 16, 16, 16, None)
+    assert rc == 1 and b"256" in lib.vitmi_last_error()
+    # VITMI_EPI_SPLIT_X3 only with the bias+GELU epilogue, and the 3N-wide output row of linear_fwd
+    rc = lib.vitmi_gemm(1, 1, 1, 128, 128, 128, 16, 128, 16, 128, 16, 128, 1, 0x200, None, None, 0, None, 0,
+                        None, 0, None)
+    assert rc == 1 and b"SPLIT_X3" in lib.vitmi_last_error()
+    rc = lib.vitmi_gemm(1, 1, 1, 128, 128, 128, 16, 128, 16, 128, 16, 128, 1, 0x201, None, 16, 128, None, 0,
+                        None, 0, None)
+    assert rc == 1 and b"3N" in lib.vitmi_last_error()
+    # split_bf16x3: K % 4 and the pattern
+    assert lib.vitmi_split_bf16x3(4, 6, 16, 6, 16, 18, 0, None, 0, None) == 1
+    assert lib.vitmi_split_bf16x3(4, 8, 16, 8, 16, 24, 2, None, 0, None) == 1
+
+
 def test_workspace_queries_are_pure_host():
     lib = _lib.lib()
     assert lib.vitmi_attention_bwd_workspace_size(2, 197, 12) == 2 * 197 * 12 * 4
