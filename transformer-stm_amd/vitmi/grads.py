@@ -14,8 +14,10 @@ out one fp32 destination per parameter, which the kernels accumulate into (+=):
     of the arena's flat gradient buffer, zeroed once at the forward (``ParamArena.begin_step``).
     AccumulateGrad keeps ("steals") that exact tensor as ``.grad``, so ``.grad`` IS the arena
     view and the DP buckets and the fused Adam read the flat buffer directly;
-  * otherwise a fresh zero tensor, which AccumulateGrad adds into an existing ``.grad``
-    (gradient accumulation across backwards) or keeps as the new ``.grad``.
+  * otherwise a zeroed buffer, which AccumulateGrad adds into an existing ``.grad`` (gradient
+    accumulation across backwards) or keeps as the new ``.grad``.  The buffers of one backward
+    are views of ONE flat allocation, zeroed by one fill (a model without an arena, e.g. the CvT,
+    otherwise paid a fill launch per parameter per step: CvT step 7.32-7.33 -> 7.23-7.27 ms).
 """
 from __future__ import annotations
 
@@ -37,11 +39,31 @@ class GradSink:
     def __init__(self, ctx, slots: Iterable[Tuple[int, Tensor]], arena=None):
         need = ctx.needs_input_grad
         self._need: Dict[int, bool] = {}
+        self._params: Dict[int, Tensor] = {}
         for i, p in slots:
             if p is not None:
                 self._need[id(p)] = self._need.get(id(p), False) or bool(need[i])
+                self._params[id(p)] = p
         self._arena = arena
         self._dst: Dict[int, Optional[Tensor]] = {}
+        self._flat: Optional[Tensor] = None
+        self._off: Dict[int, int] = {}
+
+    def _fresh(self, p: Tensor) -> Tensor:
+        """p's zeroed destination: a view of the flat buffer laid out, on the first call, for every
+        parameter of this backward that takes a gradient (the call only comes when the arena,
+        if any, has no fresh view to offer, i.e. for all of them but in a mixed case)."""
+        if self._flat is None:
+            n = 0
+            for k, q in self._params.items():
+                if self._need[k]:
+                    self._off[k] = n
+                    n += (q.numel() + 3) // 4 * 4     # 16-B aligned views
+            self._flat = torch.zeros(max(n, 4), dtype=torch.float32, device=p.device)
+        o = self._off.get(id(p))
+        if o is None or p.dtype != torch.float32 or p.device != self._flat.device:
+            return torch.zeros_like(p, memory_format=torch.contiguous_format)
+        return self._flat[o:o + p.numel()].view(p.shape)
 
     def __call__(self, p: Optional[Tensor]) -> Optional[Tensor]:
         """The fp32 buffer the kernels add p's gradient into, or None (no gradient wanted)."""
@@ -55,7 +77,7 @@ class GradSink:
             if self._arena is not None:
                 d = self._arena.take(p)
             if d is None:
-                d = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                d = self._fresh(p)
         self._dst[id(p)] = d
         return d
 
