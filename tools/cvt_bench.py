@@ -104,7 +104,7 @@ def main():
     opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True)
 
     def step_vitmi():
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad()
         loss = mse_loss(model(img), tgt)
         loss.backward()
         opt.step()
@@ -118,7 +118,7 @@ def main():
         topt = torch.optim.Adam(list(p.values()), lr=1e-4, fused=True)
 
         def step_torch():
-            topt.zero_grad(set_to_none=False)
+            topt.zero_grad()
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 y = torch_forward(p, bufs, img, cfg)
             loss = F.mse_loss(y.float().squeeze(-1), tgt)
