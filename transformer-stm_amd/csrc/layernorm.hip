@@ -106,6 +106,24 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
 }
 
 // ---------------------------------------------------------------- backward
+// VITMI_LN_BWD_NTLD: the backward's once-read inputs (x, dy, dres) with the non-temporal hint
+#ifndef VITMI_LN_BWD_NTLD
+#define VITMI_LN_BWD_NTLD 1
+#endif
+template <typename V>
+__device__ __forceinline__ V ldg_s(const V* p) {
+  if constexpr (VITMI_LN_BWD_NTLD) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T>
+__device__ __forceinline__ f32x4 load4s(const T* p);
+template <>
+__device__ __forceinline__ f32x4 load4s<float>(const float* p) { return ldg_s((const f32x4*)p); }
+template <>
+__device__ __forceinline__ f32x4 load4s<bf16>(const bf16* p) {
+  const bf16x4 b = ldg_s((const bf16x4*)p);
+  return f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+}
 // grid = G blocks x 256 threads; wave w of block b handles rows b*4+w, +4G, ...
 template <int NV, typename TDY, bool LP>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
@@ -133,14 +151,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 4;
-      rv[i] = (dres && c < D) ? *(const f32x4*)(dres + row * ldres + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      rv[i] = (dres && c < D) ? ldg_s((const f32x4*)(dres + row * ldres + c)) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (lane + 64 * i) * 4;
       if (c < D) {
-        const f32x4 xv = *(const f32x4*)(x + row * ldx + c);
-        const f32x4 dyv = load4<TDY>(dy + row * lddy + c);
+        const f32x4 xv = ldg_s((const f32x4*)(x + row * ldx + c));
+        const f32x4 dyv = load4s<TDY>(dy + row * lddy + c);
         xh[i] = (xv - mu) * rs;
         gy[i] = dyv * g[i];
         dg[i] += dyv * xh[i];
