@@ -388,7 +388,9 @@ def main():
     if world > 1:
         dist.barrier()
     M, F_, D = B * cfg.seq_len, cfg.mlp_dim, cfg.embed_dim
-    events = ops.set_probe((M, F_, D))        # fc1 forward GEMM launches
+    # the bf16x3 knob's fc1 GEMM runs over K' = 3D ([hi|hi|lo] x [hi|lo|hi] operand rows)
+    KD = 3 * D if cfg.dtype == "bf16x3" else D
+    events = ops.set_probe((M, F_, KD))       # fc1 forward GEMM launches
     if args.stats_out:
         _lib.lib().vitmi_stats_enable(1)
         torch.cuda._sleep(1000)               # marker kernel: the timed region starts
@@ -419,8 +421,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     imgs = B * world * args.steps / elapsed
     kern_ms = sum(a.elapsed_time(b) for a, b in events) / max(1, len(events))
-    kflop = 2.0 * M * F_ * D
-    # (no probe events: the bf16x3 knob's fc1 GEMM runs over K' = 3D, not the probed shape)
+    kflop = 2.0 * M * F_ * KD                 # MFMA work of the launch (3x the product's for bf16x3)
     achieved = kflop / (kern_ms * 1e-3) / 1e12 if events else 0.0
     step_flops = cfg.flops_per_image_fwd_bwd() * B * world
     out = {
@@ -444,11 +445,12 @@ def main():
                    "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
                    "model": model_name, "global_batch": B * world, "seq_len": cfg.seq_len,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd {'fp32' if fp32 else 'bf16'} [{M}x{F_}x{D}] +bias+GELU",
+        "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd {'fp32' if fp32 else 'bf16'} [{M}x{F_}x{KD}] +bias+GELU"
+                               + (" (bf16x3 split operands)" if KD != D else ""),
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,
                      "launches_timed": len(events), "avg_launch_ms": round(kern_ms, 4),
-                     "algorithmic_bytes": (4 if fp32 else 2) * (M * D + F_ * D + 2 * M * F_)},
+                     "algorithmic_bytes": (4 if fp32 else 2) * (M * KD + F_ * KD + (4 if KD != D else 2) * M * F_)},
         "optimizer_ms": phases_ms.get("optimizer"),
         "phases_ms": phases_ms,
         "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (peak * world), 4),
