@@ -96,20 +96,23 @@ __global__ void tokens_pos_bwd_kernel(int B, int N, int D, const float* __restri
 
 // ------------------------------------------------------------ bias gradient
 // partial[z][n] = sum over the rows of chunk z of dy[m][n].  256 threads = 4 row groups x
-// 64 lanes x 8 columns (one 16-byte load of bf16 / two of fp32 per row per lane).
+// 64 lanes, 8 columns per lane (one 16-byte load of bf16 / two of fp32 per row).  A wave covers
+// 2^lshift lanes x 8 columns of a row and 64 >> lshift rows at a time (lshift = 6 unless N < 512:
+// at N = 64 a one-row wave left 56 lanes idle).  Fixed summation order.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum8_kernel(int64_t M, int64_t N, const T* __restrict__ dy,
                                                       int64_t ldy, float* __restrict__ part,
-                                                      int64_t rows_per) {
+                                                      int64_t rows_per, int lshift) {
   __shared__ f32x4 red[4][64][2];
   const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 8;
+  const int R = 64 >> lshift, j = lane & ((1 << lshift) - 1), r = lane >> lshift;
+  const int64_t c = ((int64_t)blockIdx.x * 64 + j) * 8;
   const int64_t m0 = (int64_t)blockIdx.y * rows_per;
   const int64_t m1 = m0 + rows_per < M ? m0 + rows_per : M;
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
   if (c < N) {
 #pragma unroll 4
-    for (int64_t m = m0 + rg; m < m1; m += 4) {
+    for (int64_t m = m0 + rg * R + r; m < m1; m += 4 * R) {
       const T* p = dy + m * ldy + c;
       if constexpr (sizeof(T) == 2) {
         const bf16x8 v = *(const bf16x8*)p;
@@ -124,9 +127,14 @@ __global__ __launch_bounds__(256) void colsum8_kernel(int64_t M, int64_t N, cons
   red[rg][lane][0] = a0;
   red[rg][lane][1] = a1;
   __syncthreads();
-  if (rg == 0 && c < N) {
+  if (rg == 0 && r == 0 && c < N) {
     f32x4 s0 = red[0][lane][0] + red[1][lane][0] + red[2][lane][0] + red[3][lane][0];
     f32x4 s1 = red[0][lane][1] + red[1][lane][1] + red[2][lane][1] + red[3][lane][1];
+    for (int q = 1; q < R; ++q) {
+      const int l2 = (q << lshift) + j;
+      s0 += red[0][l2][0] + red[1][l2][0] + red[2][l2][0] + red[3][l2][0];
+      s1 += red[0][l2][1] + red[1][l2][1] + red[2][l2][1] + red[3][l2][1];
+    }
     float* o = part + (int64_t)blockIdx.y * N + c;
     *(f32x4*)o = s0;
     *(f32x4*)(o + 4) = s1;
@@ -477,13 +485,15 @@ extern "C" int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, 
   const bool vec = (N % 8 == 0) && (ldy % 8 == 0) && ((uintptr_t)dy % 16 == 0);
   if (vec) {
     dim3 grid((unsigned)((N + 511) / 512), Z);
+    int lshift = 6;   // lanes per row: the smallest power of two >= N / 8, at most 64
+    while (lshift > 0 && (int64_t)8 << (lshift - 1) >= N) --lshift;
     if (dtype == VITMI_BF16) {
       hipLaunchKernelGGL(colsum8_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)dy, ldy,
-                         (float*)workspace, rows_per);
+                         (float*)workspace, rows_per, lshift);
       VITMI_STAT(colsum8_kernel<bf16>, 0, (double)M * N * 2);
     } else {
       hipLaunchKernelGGL(colsum8_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)dy, ldy,
-                         (float*)workspace, rows_per);
+                         (float*)workspace, rows_per, lshift);
       VITMI_STAT(colsum8_kernel<float>, 0, (double)M * N * 4);
     }
   } else {

@@ -1199,6 +1199,37 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
   }
 }
 
+// The same for small outputs with many slabs (n / 4 <= SMALL_RED_MAX): 16 waves per block split
+// the slabs (wave w sums z = w, w + 16, ...), then the 16 wave sums are added in wave order and
+// onto dst.  Fixed order, deterministic; one lane per 4 elements would walk up to 512 slabs alone.
+constexpr int64_t SMALL_RED_MAX = 16384;
+__global__ __launch_bounds__(1024) void splitk_reduce_small_kernel(const float* __restrict__ ws, float* __restrict__ dst,
+                                                                   int64_t n, int splits, int64_t stride) {
+  __shared__ f32x4 red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (i + 4 <= n) {
+#pragma unroll 8
+    for (int z = w; z < splits; z += 16) s += *(const f32x4*)(ws + z * stride + i);
+  } else if (i < n) {
+    for (int z = w; z < splits; z += 16)
+      for (int64_t e = i; e < n; ++e) s[e - i] += ws[z * stride + e];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i < n) {
+    f32x4 t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][lane];
+    if (i + 4 <= n) {
+      *(f32x4*)(dst + i) = *(const f32x4*)(dst + i) + t;
+    } else {
+      for (int64_t e = i; e < n; ++e) dst[e] += t[e - i];
+    }
+  }
+}
+
 // Finish the tail tiles of a split gemm256 launch: sum the nsplit fp32 partials of each
 // element and apply the epilogue (the elementwise epi_store of the 128x128 kernel).
 template <typename T, typename TC, int EPI>
@@ -1317,11 +1348,11 @@ static void init_cus() {
   done = true;
 }
 
-static int64_t splits_for(int64_t tiles, int64_t ktiles, int64_t target) {
+static int64_t splits_for(int64_t tiles, int64_t ktiles, int64_t target, int64_t cap = 64) {
   int64_t want = target / tiles;
   const int64_t maxs = ktiles / 4;
   if (want > maxs) want = maxs;
-  if (want > 64) want = 64;
+  if (want > cap) want = cap;
   return want < 1 ? 1 : want;
 }
 
@@ -1515,7 +1546,13 @@ static int choose_splits(int dtype, int64_t M, int64_t N, int64_t K, int reserve
   // fixed 256 left a few units for a second full round (fc1 wgrad 262 -> 440 us at 8 reserved)
   init_cus();
   const int avail = g_cus - reserved > 8 ? g_cus - reserved : 8;
-  return (int)splits_for(tiles, ktiles, big ? avail : 2 * avail);
+  // small outputs (the CvT's 64x64 .. 256x256 weight gradients over 16-262 k tokens) may take up
+  // to 512 slabs while all of them stay under 32 MiB: with the usual cap of 64 a one-tile output
+  // ran 64 workgroups on 256 CUs
+  int64_t cap = 64;
+  const int64_t slab = M * N * (int64_t)sizeof(float);
+  if (slab > 0 && (32LL << 20) / slab > cap) cap = (32LL << 20) / slab < 512 ? (32LL << 20) / slab : 512;
+  return (int)splits_for(tiles, ktiles, big ? avail : 2 * avail, cap);
 }
 
 static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K, const void* A,
@@ -1626,6 +1663,13 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   if (rc) return rc;
   VITMI_CHECK_ARG(ldc == N, "gemm: split-K accumulate needs a dense C");
   const int64_t n = M * N;
+  if ((n + 3) / 4 <= SMALL_RED_MAX && splits >= 16) {
+    hipLaunchKernelGGL(splitk_reduce_small_kernel, dim3((unsigned)(((n + 3) / 4 + 63) / 64)), dim3(1024), 0, s,
+                       (const float*)ws, (float*)C, n, splits, M * N);
+    VITMI_LAUNCH_CHECK("splitk_reduce_small_kernel");
+    VITMI_STAT(splitk_reduce_small_kernel, 0, (double)n * 4 * (splits + 2));
+    return VITMI_OK;
+  }
   int blocks = (int)((n / 4 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
