@@ -101,6 +101,11 @@ __global__ void conv_col2im_kernel(ConvGeo g, const T* __restrict__ dp, int Kp, 
 }
 
 // ---------------------------------------------------------------- depthwise 3x3 + BatchNorm
+// VITMI_DW_ROWS (1: opt-in, being measured): the stats / dz / dx passes walk image rows with the 3x3 window in
+// registers (the *_rows kernels); 0: one pixel per thread-iteration, 9 tap loads each
+#ifndef VITMI_DW_ROWS
+#define VITMI_DW_ROWS 0
+#endif
 // Thread (pixel lane pl, channel group cg) with cg = tid % C4 fixed for the whole grid-stride
 // loop: 256 / C4 pixels per block iteration (C4 divides 256).  Pixel indices are 32-bit
 // (n = B*H*W < 2^31, checked on the host): one (b, h, w) split per pixel, none per tap.
@@ -153,6 +158,73 @@ __global__ __launch_bounds__(256) void dw_fwd_stats_kernel(DwGeo g, const float*
     *(f32x4*)(z + (int64_t)p * g.ldz + c) = acc;
     s1 += acc;
     s2 += acc * acc;
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (pl == 0) {
+    for (int l = 1; l < lanes; ++l) {
+      s1 += red[0][l * C4 + cg];
+      s2 += red[1][l * C4 + cg];
+    }
+    *(f32x4*)(part + (int64_t)blockIdx.x * 2 * g.C + c) = s1;
+    *(f32x4*)(part + (int64_t)blockIdx.x * 2 * g.C + g.C + c) = s2;
+  }
+}
+
+// The same pass walking image rows: thread (row b*H + h, channel group cg) runs along w with the
+// 3x3 window in registers (3 new taps per pixel instead of 9, no per-pixel index divisions).
+// Taps are summed in the same (i, j) order as dw_fwd_stats_kernel (out-of-image taps add 0), so z
+// is identical; the per-block statistics partials follow this kernel's own fixed order.
+__global__ __launch_bounds__(256) void dw_fwd_stats_rows_kernel(DwGeo g, const float* __restrict__ x,
+                                                                const float* __restrict__ wt,  // [3][3][C]
+                                                                float* __restrict__ z, float* __restrict__ part) {
+  __shared__ f32x4 red[2][256];
+  const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
+  const int c = cg * 4;
+  const uint32_t rows = (uint32_t)g.B * g.H;
+  f32x4 wv[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wv[k] = *(const f32x4*)(wt + k * g.C + c);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4 s1 = zero, s2 = zero;
+  for (uint32_t rw = blockIdx.x * lanes + pl; rw < rows; rw += gridDim.x * lanes) {
+    const uint32_t b = rw / (uint32_t)g.H;
+    const int h = (int)(rw - b * (uint32_t)g.H);
+    const float* xb = x + img_row0(b, g.x_img, g.x_off) * g.ldx + c;
+    const float* xr[3];
+    bool ok[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int hh = h + i - 1;
+      ok[i] = hh >= 0 && hh < g.H;
+      xr[i] = xb + (int64_t)(ok[i] ? hh : 0) * g.W * g.ldx;
+    }
+    auto tap = [&](int i, int ww) -> f32x4 {
+      return ok[i] && ww < g.W ? *(const f32x4*)(xr[i] + (int64_t)ww * g.ldx) : zero;
+    };
+    f32x4 L[3], M[3], R[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { L[i] = zero; M[i] = tap(i, 0); R[i] = tap(i, 1); }
+    float* zr = z + (int64_t)rw * g.W * g.ldz + c;
+    for (int w = 0; w < g.W; ++w) {
+      f32x4 nx[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) nx[i] = tap(i, w + 2);   // next column, in flight under the FMAs
+      f32x4 acc = zero;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (!ok[i]) continue;
+        if (w > 0) acc += wv[i * 3 + 0] * L[i];
+        acc += wv[i * 3 + 1] * M[i];
+        if (w + 1 < g.W) acc += wv[i * 3 + 2] * R[i];
+      }
+      *(f32x4*)(zr + (int64_t)w * g.ldz) = acc;
+      s1 += acc;
+      s2 += acc * acc;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { L[i] = M[i]; M[i] = R[i]; R[i] = nx[i]; }
+    }
   }
   red[0][threadIdx.x] = s1;
   red[1][threadIdx.x] = s2;
@@ -349,6 +421,138 @@ __global__ __launch_bounds__(256) void dw_bwd_dz_kernel(DwGeo g, const TD* __res
   }
 }
 
+// The same pass walking image rows (see dw_fwd_stats_rows_kernel): the x window slides along w,
+// so each pixel loads dy, z and 3 new x taps.  dz is identical; the weight-gradient partials
+// follow this kernel's fixed order.
+template <typename TD>
+__global__ __launch_bounds__(256) void dw_bwd_dz_rows_kernel(DwGeo g, const TD* __restrict__ dy, int64_t lddy,
+                                                             int64_t dy_img, int64_t dy_off,
+                                                             const float* __restrict__ z, const float* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ kk, float* __restrict__ dz,
+                                                             float* __restrict__ part) {
+  __shared__ f32x4 red[256];
+  const int C4 = g.C / 4, cg = threadIdx.x % C4, lanes = 256 / C4, pl = threadIdx.x / C4;
+  const int c = cg * 4;
+  const uint32_t rows = (uint32_t)g.B * g.H;
+  const f32x4 mu = *(const f32x4*)(mean + c), rs = *(const f32x4*)(rstd + c);
+  const f32x4 gr = *(const f32x4*)(gamma + c) * rs;
+  const f32x4 k1 = *(const f32x4*)(kk + c), k2 = *(const f32x4*)(kk + g.C + c);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4 dw[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) dw[k] = zero;
+  for (uint32_t rw = blockIdx.x * lanes + pl; rw < rows; rw += gridDim.x * lanes) {
+    const uint32_t b = rw / (uint32_t)g.H;
+    const int h = (int)(rw - b * (uint32_t)g.H);
+    const float* xb = x + img_row0(b, g.x_img, g.x_off) * g.ldx + c;
+    const float* xr[3];
+    bool ok[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int hh = h + i - 1;
+      ok[i] = hh >= 0 && hh < g.H;
+      xr[i] = xb + (int64_t)(ok[i] ? hh : 0) * g.W * g.ldx;
+    }
+    auto tap = [&](int i, int ww) -> f32x4 {
+      return ok[i] && ww < g.W ? *(const f32x4*)(xr[i] + (int64_t)ww * g.ldx) : zero;
+    };
+    f32x4 L[3], M[3], R[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { L[i] = zero; M[i] = tap(i, 0); R[i] = tap(i, 1); }
+    const TD* dyr = dy + (img_row0(b, dy_img, dy_off) + (int64_t)h * g.W) * lddy + c;
+    const float* zr = z + (int64_t)rw * g.W * g.ldz + c;
+    float* dzr = dz + (int64_t)rw * g.W * g.ldz + c;
+    for (int w = 0; w < g.W; ++w) {
+      f32x4 nx[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) nx[i] = tap(i, w + 2);
+      f32x4 d;
+      const TD* src = dyr + (int64_t)w * lddy;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = to_f32(src[e]);
+      const f32x4 zh = (*(const f32x4*)(zr + (int64_t)w * g.ldz) - mu) * rs;
+      const f32x4 dzv = gr * (d - k1 - zh * k2);
+      *(f32x4*)(dzr + (int64_t)w * g.ldz) = dzv;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (!ok[i]) continue;
+        if (w > 0) dw[i * 3 + 0] += dzv * L[i];
+        dw[i * 3 + 1] += dzv * M[i];
+        if (w + 1 < g.W) dw[i * 3 + 2] += dzv * R[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { L[i] = M[i]; M[i] = R[i]; R[i] = nx[i]; }
+    }
+  }
+  for (int k = 0; k < 9; ++k) {
+    __syncthreads();
+    red[threadIdx.x] = dw[k];
+    __syncthreads();
+    if (pl == 0) {
+      f32x4 s = dw[k];
+      for (int l = 1; l < lanes; ++l) s += red[l * C4 + cg];
+      *(f32x4*)(part + ((int64_t)blockIdx.x * 9 + k) * g.C + c) = s;
+    }
+  }
+}
+
+// dx[p] += sum_{i,j} w[i][j] * dz[p - (i-1, j-1)] walking image rows: thread (row, channel group)
+// slides a 3x3 dz window along w (3 new loads per pixel); same (i, j) order as dw_bwd_dx_kernel,
+// so dx is identical.
+__global__ __launch_bounds__(256) void dw_bwd_dx_rows_kernel(DwGeo g, const float* __restrict__ dz,
+                                                             const float* __restrict__ wt, float* __restrict__ dx) {
+  const uint32_t C4 = g.C / 4;
+  const uint32_t total = (uint32_t)g.B * g.H * C4;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int c = (int)(t % C4) * 4;
+    const uint32_t rw = t / C4;
+    const uint32_t b = rw / (uint32_t)g.H;
+    const int h = (int)(rw - b * (uint32_t)g.H);
+    f32x4 wv[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wv[k] = *(const f32x4*)(wt + k * g.C + c);
+    // dz rows h + 1 (i = 0), h (i = 1), h - 1 (i = 2) of image b
+    const float* zb = dz + (int64_t)b * g.H * g.W * g.ldz + c;
+    const float* zr[3];
+    bool ok[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int hh = h - i + 1;
+      ok[i] = hh >= 0 && hh < g.H;
+      zr[i] = zb + (int64_t)(ok[i] ? hh : 0) * g.W * g.ldz;
+    }
+    auto tap = [&](int i, int ww) -> f32x4 {
+      return ok[i] && ww < g.W ? *(const f32x4*)(zr[i] + (int64_t)ww * g.ldz) : zero;
+    };
+    // window: P = dz(w - 1), Q = dz(w), S = dz(w + 1); tap j reads column w - j + 1
+    f32x4 P[3], Q[3], S[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { P[i] = zero; Q[i] = tap(i, 0); S[i] = tap(i, 1); }
+    float* dr = dx + (img_row0(b, g.x_img, g.x_off) + (int64_t)h * g.W) * g.ldx + c;
+    for (int w = 0; w < g.W; ++w) {
+      f32x4 nx[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) nx[i] = tap(i, w + 2);
+      f32x4 acc = zero;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (!ok[i]) continue;
+        if (w + 1 < g.W) acc += wv[i * 3 + 0] * S[i];
+        acc += wv[i * 3 + 1] * Q[i];
+        if (w > 0) acc += wv[i * 3 + 2] * P[i];
+      }
+      float* d = dr + (int64_t)w * g.ldx;
+      *(f32x4*)d = *(const f32x4*)d + acc;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { P[i] = Q[i]; Q[i] = S[i]; S[i] = nx[i]; }
+    }
+  }
+}
+
 // dW[k][c] += sum over blocks of the partials (fixed order)
 __global__ __launch_bounds__(1024) void dw_wgrad_finalize_kernel(const float* __restrict__ part, int G, int C,
                                                                  float* __restrict__ dwt) {
@@ -510,9 +714,17 @@ extern "C" int vitmi_dwconv_bn_fwd(int B, int H, int W, int C, const float* x, i
   VITMI_CHECK_ARG(training || (run_mean && run_var), "dwconv_bn_fwd: inference needs the moving statistics");
   hipStream_t st = (hipStream_t)stream;
   const int64_t n = (int64_t)B * H * W;
-  const int G = dw_blocks(n, C);
   float* part = (float*)workspace;
+#if VITMI_DW_ROWS
+  // row-walking stats pass: one thread per (image row, channel group), at most dw_blocks blocks
+  // (the workspace's partial rows)
+  int G = (int)(((int64_t)B * H * (C / 4) + 255) / 256);
+  if (G > dw_blocks(n, C)) G = dw_blocks(n, C);
+  hipLaunchKernelGGL(dw_fwd_stats_rows_kernel, dim3(G), dim3(256), 0, st, g, x, wt, z, part);
+#else
+  const int G = dw_blocks(n, C);
   hipLaunchKernelGGL(dw_fwd_stats_kernel, dim3(G), dim3(256), 0, st, g, x, wt, z, part);
+#endif
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + RED_COLS - 1) / RED_COLS), dim3(1024), 0, st, (const float*)part, G, C, n, eps,
                      momentum, mean, rstd, run_mean, run_var, training);
   const int64_t work = n * (C / 4);
@@ -551,6 +763,20 @@ extern "C" int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, i
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + RED_COLS - 1) / RED_COLS), dim3(1024), 0, st, (const float*)part, G, C, n,
                      dgamma, dbeta, kk);
+#if VITMI_DW_ROWS
+  int Gw = (int)(((int64_t)B * H * (C / 4) + 255) / 256);
+  if (Gw > G) Gw = G;
+  if (dy_dtype == VITMI_BF16)
+    hipLaunchKernelGGL(dw_bwd_dz_rows_kernel<bf16>, dim3(Gw), dim3(256), 0, st, g, (const bf16*)dy, lddy, dy_img, dy_off,
+                       z, x, mean, rstd, gamma, (const float*)kk, dz, part);
+  else
+    hipLaunchKernelGGL(dw_bwd_dz_rows_kernel<float>, dim3(Gw), dim3(256), 0, st, g, (const float*)dy, lddy, dy_img,
+                       dy_off, z, x, mean, rstd, gamma, (const float*)kk, dz, part);
+  hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3((9 * C + RED_COLS - 1) / RED_COLS), dim3(1024), 0, st, (const float*)part, Gw, C,
+                     dwt);
+  hipLaunchKernelGGL(dw_bwd_dx_rows_kernel, dim3(grid_of((int64_t)B * H * (C / 4))), dim3(256), 0, st, g, (const float*)dz,
+                     wt, dx);
+#else
   if (dy_dtype == VITMI_BF16)
     hipLaunchKernelGGL(dw_bwd_dz_kernel<bf16>, dim3(G), dim3(256), 0, st, g, (const bf16*)dy, lddy, dy_img, dy_off, z,
                        x, mean, rstd, gamma, (const float*)kk, dz, part);
@@ -560,6 +786,7 @@ extern "C" int vitmi_dwconv_bn_bwd(int B, int H, int W, int C, const void* dy, i
   hipLaunchKernelGGL(dw_wgrad_finalize_kernel, dim3((9 * C + RED_COLS - 1) / RED_COLS), dim3(1024), 0, st, (const float*)part, G, C,
                      dwt);
   hipLaunchKernelGGL(dw_bwd_dx_kernel, dim3(grid_of(n * (C / 4))), dim3(256), 0, st, g, (const float*)dz, wt, dx);
+#endif
   VITMI_LAUNCH_CHECK("dwconv_bn_bwd");
   return VITMI_OK;
 }
