@@ -101,10 +101,10 @@ __global__ void conv_col2im_kernel(ConvGeo g, const T* __restrict__ dp, int Kp, 
 }
 
 // ---------------------------------------------------------------- depthwise 3x3 + BatchNorm
-// VITMI_DW_ROWS (1: opt-in, being measured): the stats / dz / dx passes walk image rows with the 3x3 window in
+// VITMI_DW_ROWS (default 1): the stats / dz / dx passes walk image rows with the 3x3 window in
 // registers (the *_rows kernels); 0: one pixel per thread-iteration, 9 tap loads each
 #ifndef VITMI_DW_ROWS
-#define VITMI_DW_ROWS 0
+#define VITMI_DW_ROWS 1
 #endif
 // Thread (pixel lane pl, channel group cg) with cg = tid % C4 fixed for the whole grid-stride
 // loop: 256 / C4 pixels per block iteration (C4 divides 256).  Pixel indices are 32-bit
