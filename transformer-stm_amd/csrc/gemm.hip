@@ -309,6 +309,11 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
   constexpr int A_BYTES = BM * BK * ES, B_BYTES = BN * BK * ES;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  // bf16 outputs of the store / GELU / DGELU epilogues: MFMA operands swapped (C^T in the
+  // accumulator, as in gemm256), so a lane owns 4 consecutive columns of one row and stores them
+  // as one 8-byte vector instead of four 2-byte scalars (the CvT's K = 64 stage-1 MLP GEMMs)
+  constexpr bool SWP = std::is_same<T, bf16>::value && std::is_same<TC, bf16>::value &&
+                       (EPI == VITMI_EPI_STORE || EPI == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU);
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int lane = threadIdx.x & 63;
@@ -376,10 +381,51 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mma(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = SWP ? mma(bfr[j], af[i], acc[i][j]) : mma(af[i], bfr[j], acc[i][j]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+
+  if constexpr (SWP) {
+    // C^T layout: row = lane & 15, columns 4 * (lane >> 4) + 0..3
+    const int rl = lane & 15, cq = 4 * (lane >> 4);
+    const bool vst = (g.ldc & 3) == 0 && ((uintptr_t)g.C & 7) == 0;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col0 = n0 + wn * (BN / WN) + j * 16 + cq;
+      if (col0 >= g.N) continue;
+      float bv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = (g.bias && EPI != VITMI_EPI_DGELU && col0 + e < g.N) ? g.bias[col0 + e] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int64_t row = m0 + wm * (BM / WM) + i * 16 + rl;
+        if (row >= g.M) continue;
+        if (vst && col0 + 4 <= g.N) {
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = acc[i][j][e];
+            if constexpr (EPI == VITMI_EPI_STORE) {
+              o[e] = (bf16)(v + bv[e]);
+            } else if constexpr (EPI == VITMI_EPI_BIAS_GELU) {
+              const float u = v + bv[e];
+              ((T*)g.aux)[aux_at(g, row, col0 + e)] = from_f32<T>(gelu_grad_f(u));
+              o[e] = (bf16)gelu_f(u);
+            } else {   // DGELU
+              o[e] = (bf16)(v * to_f32(((const T*)g.aux)[aux_at(g, row, col0 + e)]));
+            }
+          }
+          *(bf16x4*)((bf16*)g.C + row * g.ldc + col0) = o;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col0 + e < g.N) epi_store<T, TC, EPI>(g, row, col0 + e, acc[i][j][e], bv[e]);
+        }
+      }
+    }
+    return;
   }
 
   // epilogue: C layout of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + i
