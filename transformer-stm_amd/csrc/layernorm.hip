@@ -200,6 +200,66 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
+// D = 4L <= 128 (the CvT's stages 1 and 2: D = 64, 128): L lanes per row and 64 / L rows per wave
+// (the one-row-per-wave kernel above left 48 / 32 of the 64 lanes idle there).  Same math, the
+// row sums over the row's L lanes by xor shuffles, same partial layout (fixed order).
+template <int L, typename TDY, bool LP>
+__global__ __launch_bounds__(256) void ln_bwd_small_kernel(
+    int64_t M, const TDY* __restrict__ dy, int64_t lddy, const float* __restrict__ x, int64_t ldx,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
+    const float* __restrict__ dres, int64_t ldres, float* __restrict__ dx, int64_t lddx,
+    bf16* __restrict__ dx_lp, int64_t lddx_lp, float* __restrict__ part) {
+  constexpr int D = 4 * L, RW = 64 / L;
+  __shared__ f32x4 red[4][64 * 3];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / L, c = (lane % L) * 4;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 g = *(const f32x4*)(gamma + c);
+  f32x4 dg = zero, db = zero, ds = zero;
+  for (int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * RW; r0 < M; r0 += (int64_t)gridDim.x * 4 * RW) {
+    const int64_t row = r0 + sub;
+    const bool ok = row < M;
+    float mu = 0.f, rs = 0.f;
+    f32x4 xv = zero, dyv = zero, rv = zero;
+    if (ok) {
+      mu = mean[row];
+      rs = rstd[row];
+      if (dres) rv = ldg_s((const f32x4*)(dres + row * ldres + c));
+      xv = ldg_s((const f32x4*)(x + row * ldx + c));
+      dyv = load4s<TDY>(dy + row * lddy + c);
+    }
+    const f32x4 xh = (xv - mu) * rs;
+    const f32x4 gy = dyv * g;
+    dg += dyv * xh;
+    db += dyv;
+    float s1 = gy[0] + gy[1] + gy[2] + gy[3];
+    const f32x4 t = gy * xh;
+    float s2 = t[0] + t[1] + t[2] + t[3];
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    const float c1 = s1 / D, c2 = s2 / D;
+    if (ok) {
+      const f32x4 o = (gy - c1 - xh * c2) * rs + rv;
+      ds += o;
+      put((f32x4*)(dx + row * lddx + c), o);
+      if (LP) store4<bf16>(dx_lp + row * lddx_lp + c, o);
+    }
+  }
+  red[wave][lane] = dg;
+  red[wave][64 + lane] = db;
+  red[wave][128 + lane] = ds;
+  __syncthreads();
+  if (threadIdx.x < 3 * L) {
+    const int which = threadIdx.x / L, cc = threadIdx.x % L;
+    f32x4 acc = zero;
+    for (int w = 0; w < 4; ++w)
+      for (int q = 0; q < RW; ++q) acc += red[w][which * 64 + q * L + cc];
+    *(f32x4*)(part + ((int64_t)which * gridDim.x + blockIdx.x) * D + cc * 4) = acc;
+  }
+}
 
 #ifndef VITMI_LN_BWD_BLOCKS
 #define VITMI_LN_BWD_BLOCKS 512
@@ -299,6 +359,27 @@ extern "C" int vitmi_layernorm_bwd(int64_t M, int D, const void* dy, int dy_dtyp
   const int G = ln_blocks_bwd(M);
   float* part = (float*)workspace;
   const int nv = (D + 255) / 256;
+#ifndef VITMI_LN_BWD_SMALL
+#define VITMI_LN_BWD_SMALL 1
+#endif
+  if (VITMI_LN_BWD_SMALL && (D == 64 || D == 128)) {
+#define LNS(LL, TD, LPB)                                                                          \
+  hipLaunchKernelGGL((ln_bwd_small_kernel<LL, TD, LPB>), dim3(G), dim3(256), 0, s, M, (const TD*)dy, lddy, x, ldx, \
+                     mean, rstd, gamma, dres, ldres, dx, lddx, (bf16*)dx_lp, lddx_lp, part)
+    const bool bf = dy_dtype == VITMI_BF16, lp = dx_lp != nullptr;
+    if (D == 64) {
+      if (bf) { if (lp) LNS(16, bf16, true); else LNS(16, bf16, false); }
+      else { if (lp) LNS(16, float, true); else LNS(16, float, false); }
+    } else {
+      if (bf) { if (lp) LNS(32, bf16, true); else LNS(32, bf16, false); }
+      else { if (lp) LNS(32, float, true); else LNS(32, float, false); }
+    }
+#undef LNS
+    VITMI_LAUNCH_CHECK("layernorm_bwd");
+    if (int rc = fold_rows(part, G, D, D, dgamma, s)) return rc;
+    if (int rc = fold_rows(part + (int64_t)G * D, G, D, D, dbeta, s)) return rc;
+    return fold_rows(part + 2LL * G * D, G, D, D, dxsum, s);
+  }
 #define LNB(NV)                                                                                  \
   if (dy_dtype == VITMI_BF16)                                                                    \
     ln_bwd_launch<NV, bf16>(s, G, M, D, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx,    \
