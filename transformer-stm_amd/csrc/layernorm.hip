@@ -105,6 +105,40 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
   }
 }
 
+// D = 4L <= 128 (the CvT's stages 1 and 2): L lanes per row, 64 / L rows per wave, row sums by xor
+// shuffles inside the row's lanes (the one-row kernel keeps 16 / 32 of 64 lanes busy there)
+template <int L, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_small_kernel(int64_t M, const float* __restrict__ x, int64_t ldx,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps,
+                                                           TY* __restrict__ y, int64_t ldy,
+                                                           float* __restrict__ mean, float* __restrict__ rstd) {
+  constexpr int D = 4 * L, RW = 64 / L;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (lane % L) * 4;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * RW + lane / L;
+  const bool ok = row < M;
+  const f32x4 v = ok ? *(const f32x4*)(x + row * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  float s = v[0] + v[1] + v[2] + v[3];
+#pragma unroll
+  for (int o = 1; o < L; o <<= 1) s += __shfl_xor(s, o, 64);
+  const float mu = s / D;
+  const f32x4 d = v - mu;
+  float q = d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+#pragma unroll
+  for (int o = 1; o < L; o <<= 1) q += __shfl_xor(q, o, 64);
+  const float rs = rsqrtf(q / D + eps);
+  if (ok) {
+    const f32x4 g = *(const f32x4*)(gamma + c);
+    const f32x4 b = *(const f32x4*)(beta + c);
+    store4<TY>(y + row * ldy + c, (v - mu) * rs * g + b);
+    if (c == 0) {
+      mean[row] = mu;
+      rstd[row] = rs;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- backward
 // VITMI_LN_BWD_NTLD: the backward's once-read inputs (x, dy, dres) with the non-temporal hint
 #ifndef VITMI_LN_BWD_NTLD
@@ -328,6 +362,30 @@ extern "C" int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx
   if (M == 0) return VITMI_OK;
   VITMI_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
+#ifndef VITMI_LN_FWD_SMALL
+#define VITMI_LN_FWD_SMALL 1
+#endif
+  if (VITMI_LN_FWD_SMALL && (D == 64 || D == 128) && y_dtype != VITMI_BF16X3) {
+    const int rw = 64 / (D / 4);
+    const dim3 grid((unsigned)((M + 4 * rw - 1) / (4 * rw)));
+    if (D == 64) {
+      if (y_dtype == VITMI_BF16)
+        hipLaunchKernelGGL((ln_fwd_small_kernel<16, bf16>), grid, dim3(256), 0, s, M, x, ldx, gamma, beta, eps,
+                           (bf16*)y, ldy, mean, rstd);
+      else
+        hipLaunchKernelGGL((ln_fwd_small_kernel<16, float>), grid, dim3(256), 0, s, M, x, ldx, gamma, beta, eps,
+                           (float*)y, ldy, mean, rstd);
+    } else {
+      if (y_dtype == VITMI_BF16)
+        hipLaunchKernelGGL((ln_fwd_small_kernel<32, bf16>), grid, dim3(256), 0, s, M, x, ldx, gamma, beta, eps,
+                           (bf16*)y, ldy, mean, rstd);
+      else
+        hipLaunchKernelGGL((ln_fwd_small_kernel<32, float>), grid, dim3(256), 0, s, M, x, ldx, gamma, beta, eps,
+                           (float*)y, ldy, mean, rstd);
+    }
+    VITMI_LAUNCH_CHECK("layernorm_fwd");
+    return VITMI_OK;
+  }
   const int nv = (D + 255) / 256;
   switch (nv) {
     case 1: ln_fwd_launch<1>(s, M, D, x, ldx, gamma, beta, eps, y, y_dtype, ldy, mean, rstd); break;
