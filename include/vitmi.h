@@ -424,8 +424,9 @@ int vitmi_comm_destroy(int abort);
  * small fold launch (out += the column sums of the partial rows, fixed order).  Between
  * vitmi_fold_begin() and vitmi_fold_end() on one host thread, those folds are queued instead of
  * launched, and vitmi_fold_end launches them together (one launch per 16 folds, on the stream of the
- * calls that queued them).  The caller keeps the workspaces of the queued calls alive until then; the
- * outputs are final once vitmi_fold_end's launch has run (stream order).  vitmi/modules.py brackets
+ * calls that queued them) and orders `stream` after every other stream that ran folds since
+ * vitmi_fold_begin (an event wait).  The caller keeps the workspaces of the queued calls alive until
+ * then; the outputs are final in `stream` order after vitmi_fold_end.  vitmi/modules.py brackets
  * each block's backward with them: one fold launch per block instead of four. */
 int vitmi_fold_begin(void);
 int vitmi_fold_end(vitmi_stream_t stream);

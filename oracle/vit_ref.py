@@ -248,6 +248,20 @@ def forward_backward(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg, dro
     return logits.detach(), loss.detach(), grads
 
 
+def per_image_grad_scale(img: Tensor, target: Tensor, p: Dict[str, Tensor], cfg) -> Dict[str, float]:
+    """{name: sum_i ||g_i||}: the norms of each image's contribution g_i to the batch-mean gradient
+    g = sum_i g_i, summed.  kappa = sum_i ||g_i|| / ||g|| measures how much the contributions cancel;
+    a low-precision backward rounds each contribution, so its error scales with this sum, not with
+    ||g|| (tests/test_gpu_model.py uses it as the denominator of the conditioned error)."""
+    B = img.shape[0]
+    out: Dict[str, float] = {}
+    for i in range(B):
+        _, _, g = forward_backward(img[i:i + 1], target[i:i + 1], p, cfg)
+        for k, v in g.items():
+            out[k] = out.get(k, 0.0) + v.double().norm().item() / B
+    return out
+
+
 def synthetic_batch(cfg, batch: int, seed: int = 1234):
     """Images in [0,1) like the reference's /255 normalisation (models/CvT(Par).py:423)."""
     g = torch.Generator().manual_seed(seed)
@@ -268,7 +282,7 @@ def rel_err(a: Tensor, b: Tensor) -> float:
 
 __all__ = [
     "param_shapes", "init_params", "forward", "forward_features", "forward_backward",
-    "loss_fn", "synthetic_batch", "rel_err", "layer_norm", "attention", "mlp", "block", "embed",
+    "loss_fn", "synthetic_batch", "rel_err", "per_image_grad_scale", "layer_norm", "attention", "mlp", "block", "embed",
     "dropout", "dropout_hash", "dropout_params",
 ]
 

@@ -347,25 +347,43 @@ def test_vit_b_precision_knob_bf16x3_meets_1e3():
 
 
 def test_bf16x3_knob_streamed_attention_n290():
-    """bf16x3 at N > 256 (ViT-Ti/16 at 272 px, N = 290): the whole-sequence x3 attention does not
-    apply, the knob takes O from the fp32 streamed attention forward and o / lse from the bf16
-    one (vitmi/modules.py _forward_x3); logits within 1e-3 of the fp32 oracle at depth 4.  The
-    backward is the bf16 one: at this shape the bias gradients nearly cancel (|d norm1.bias| ~
-    2e-3, measured relative error 0.23 for plain bf16 and for the knob alike, fp32 5e-5), so the
-    gradients are held to the bf16 path's own error on the same inputs."""
+    """bf16 and bf16x3 at N > 256 (ViT-Ti/16 at 272 px, N = 290, depth 4: the streamed attention
+    kernels; the knob takes O from the fp32 streamed forward and o / lse from the bf16 one,
+    vitmi/modules.py _forward_x3).  Logits of the knob within 1e-3 of the fp32 oracle.
+
+    Gradients, against the ORACLE, two ways (SURVEY §8d bf16 bound 2e-2):
+      * a well-conditioned batch (both images labelled 0): ||d|| / ||g|| <= 2e-2 per tensor;
+      * the seed's own labels (0, 1): the two images' gradients nearly cancel here (the model
+        gives both noise images almost the same logits, so g = g_0 + g_1 with ||g_i|| up to 75 x
+        ||g||: kappa, oracle.vit_ref.per_image_grad_scale).  A backward that rounds each image's
+        contribution to bf16 (2^-9) cannot meet 2e-2 of ||g|| there: even the fp32 path's error grows
+        by the same factor (6e-7 at N = 197 -> 4.6e-5 here; tools/diag_grad_precision.py).  The bound
+        is applied to what the rounding acts on: ||d|| <= 2e-2 * sum_i ||g_i|| (the same bound at
+        kappa = 1), and kappa is asserted so the case stays the ill-conditioned one."""
     cfg = config_c1(dtype="bf16x3", img_size=272, depth=4)
     params = vit_ref.init_params(cfg, seed=8)
     img, tgt = vit_ref.synthetic_batch(cfg, 2)
-    l_ref, _, g_ref = vit_ref.forward_backward(img, tgt, params, cfg)
-    worst = {}
-    for c in (cfg.replace(dtype="bf16"), cfg):
-        l, _, g = gpu_step(c, params, img, tgt)
-        worst[c.dtype] = max(vit_ref.rel_err(g[k], g_ref[k]) for k in g_ref)
-        if c.dtype == "bf16x3":
-            err = (l - l_ref).abs().max().item()
-    print(f"N=290 bf16x3: logits {err:.3e}; worst grad rel bf16x3 {worst['bf16x3']:.3e}, bf16 {worst['bf16']:.3e}")
-    assert err <= 1e-3
-    assert worst["bf16x3"] <= 1.25 * worst["bf16"] + 1e-2
+    assert tgt.tolist() == [0, 1]
+    for labels in (torch.zeros_like(tgt), tgt):
+        l_ref, _, g_ref = vit_ref.forward_backward(img, labels, params, cfg)
+        scale = vit_ref.per_image_grad_scale(img, labels, params, cfg)
+        kappa = max(scale[k] / g_ref[k].double().norm().item() for k in g_ref)
+        for c in (cfg.replace(dtype="bf16"), cfg):
+            l, _, g = gpu_step(c, params, img, labels)
+            plain = max((vit_ref.rel_err(g[k], g_ref[k]), k) for k in g_ref)
+            cond = max(((g[k] - g_ref[k]).double().norm().item() / scale[k], k) for k in g_ref)
+            print(f"N=290 {c.dtype} labels {labels.tolist()}: kappa {kappa:.1f}; worst grad rel {plain[0]:.3e} "
+                  f"({plain[1]}), conditioned {cond[0]:.3e} ({cond[1]})")
+            if c.dtype == "bf16x3":
+                err = (l - l_ref).abs().max().item()
+                print(f"   bf16x3 logits max-abs {err:.3e}")
+                assert err <= 1e-3
+            if labels.sum() == 0:
+                assert kappa < 1.5
+                assert plain[0] <= 2e-2, plain
+            else:
+                assert kappa > 30
+                assert cond[0] <= 2e-2, cond
 
 
 def test_bf16x3_knob_small_model_matches_oracle():

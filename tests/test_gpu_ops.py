@@ -242,7 +242,7 @@ def test_bias_grad(T):
 
 
 # ------------------------------------------------------------------ LayerNorm
-@pytest.mark.parametrize("D", [64, 192, 384, 768, 1024])
+@pytest.mark.parametrize("D", [64, 128, 192, 384, 768, 1024])
 @pytest.mark.parametrize("T", [BF, torch.float32])
 def test_layernorm_fwd_bwd(D, T):
     M = 197 * 2 + 3
@@ -264,6 +264,44 @@ def test_layernorm_fwd_bwd(D, T):
     assert rel(dg, 0.5 + ww.grad) < 1e-5
     assert rel(dbb, -0.5 + bb.grad) < 1e-5
     assert rel(dsum, 2.0 + (xx.grad + dres).sum(0)) < 1e-5   # fused bias-grad column sums
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("dy_dtype", [BF, torch.float32])
+@pytest.mark.parametrize("with_dres", [False, True])
+def test_layernorm_small_d_backward_variants(D, dy_dtype, with_dres):
+    """the several-rows-per-wave LayerNorm kernels (D = 64 / 128: L = 16 / 32 lanes
+    per row) without the residual gradient, without the bf16 copy, with an fp32 dy, and the
+    forward and backward over strided rows (the head-LN pattern x[:, 0]), against F.layer_norm."""
+    B, N = 37, 9
+    x = rnd(B, N, D, seed=40) * 2 + 0.5
+    w, b = 1 + 0.1 * rnd(D, seed=41), 0.1 * rnd(D, seed=42)
+    xd = x.to(DEV)
+    # contiguous rows, no dres, no bf16 copy
+    y, mean, rstd = ops.layernorm_fwd(xd.view(B * N, D), w.to(DEV), b.to(DEV), 1e-6, torch.float32)
+    assert rel(y, F.layer_norm(x.view(B * N, D), (D,), w, b, 1e-6)) < 1e-6
+    dy = rnd(B * N, D, seed=43).to(dy_dtype)
+    dres = rnd(B * N, D, seed=44) if with_dres else None
+    dg, dbb = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    dx, dx_lp = ops.layernorm_bwd(dy.to(DEV), xd.view(B * N, D), mean, rstd, w.to(DEV), dg, dbb,
+                                  dres=dres.to(DEV) if with_dres else None, lp_dtype=None)
+    assert dx_lp is None
+    xx, ww, bb = x.view(B * N, D).clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    F.layer_norm(xx, (D,), ww, bb, 1e-6).backward(dy.float())
+    want = xx.grad + (dres if with_dres else 0)
+    assert rel(dx, want) < 1e-5
+    assert rel(dg, ww.grad) < 1e-5 and rel(dbb, bb.grad) < 1e-5
+    # strided rows (every image's cls row), fp32 and bf16 outputs, backward into strided dx
+    for T in (torch.float32, BF):
+        yc, mc, rc = ops.layernorm_fwd(xd[:, 0], w.to(DEV), b.to(DEV), 1e-6, T)
+        assert rel(yc.float(), F.layer_norm(x[:, 0], (D,), w, b, 1e-6)) < (5e-3 if T == BF else 1e-6)
+    dxs = torch.zeros(B, N, D, device=DEV)
+    dyc = rnd(B, D, seed=45).to(dy_dtype)
+    ops.layernorm_bwd(dyc.to(DEV), xd[:, 0], mc, rc, w.to(DEV), None, None, dx=dxs[:, 0])
+    xc = x[:, 0].clone().requires_grad_()
+    F.layer_norm(xc, (D,), w, b, 1e-6).backward(dyc.float())
+    assert rel(dxs[:, 0], xc.grad) < 1e-5
+    assert dxs[:, 1:].abs().max().item() == 0.0
 
 
 def test_layernorm_strided_rows():

@@ -99,3 +99,46 @@ def test_adam_per_tensor_on_arena_params_refreshes_bf16_shadow():
     model(img)                                          # the forward refreshes the shadow if stale
     torch.cuda.synchronize()
     assert torch.equal(arena.flat_lp, arena.flat.to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+def test_adam_arena_skips_frozen_parameters():
+    """a parameter frozen after it has been trained (stale m / v) and a parameter whose
+    gradient is None after zero_grad(set_to_none) stay bit-identical through the fused arena
+    step, as with torch / Keras; the others still follow the float32 oracle bit for bit, and the
+    bf16 shadow stays equal to bf16(params)."""
+    from vitmi.config import ViTConfig
+    from vitmi.modules import VisionTransformer, cross_entropy
+    cfg = ViTConfig(img_size=32, patch_size=8, in_chans=3, num_classes=2, embed_dim=128, depth=2, num_heads=2,
+                    dtype="bf16")
+    model = VisionTransformer(cfg).to(DEV)
+    model.reset_parameters(seed=5)
+    opt = optim.Adam(model, learning_rate=1e-3)
+    arena = model.arena()
+    g = torch.Generator().manual_seed(6)
+    img = torch.rand(4, 3, 32, 32, generator=g).to(DEV)
+    tgt = torch.randint(0, 2, (4,), generator=g).to(DEV)
+    opt.zero_grad()
+    cross_entropy(model(img), tgt).backward()
+    opt.step()                                           # every parameter trained once: m, v != 0
+    frozen = model.blocks[0].mlp.fc1.weight
+    frozen.requires_grad_(False)
+    before = {k: p.detach().clone() for k, p in model.named_parameters()}
+    m0, v0 = opt._m.cpu().numpy().copy(), opt._v.cpu().numpy().copy()
+    p0 = arena.flat.cpu().numpy().copy()
+    opt.zero_grad()
+    cross_entropy(model(img), tgt).backward()
+    head_b = model.head.bias
+    head_b.grad = None                                   # a parameter without a gradient this step
+    grad = arena.grad.cpu().numpy().copy()
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(frozen.detach(), before["blocks.0.mlp.fc1.weight"])
+    assert torch.equal(head_b.detach(), before["head.bias"])
+    ref, _, _ = optim_ref.adam_step(p0, grad, m0, v0, 1e-3, 2)
+    keep = np.ones(arena.numel, dtype=bool)
+    for p in (frozen, head_b):
+        o = arena.offsets[id(p)]
+        keep[o:o + p.numel()] = False
+    assert np.array_equal(arena.flat.cpu().numpy()[keep], ref[keep])
+    assert torch.equal(arena.flat_lp, arena.flat.to(torch.bfloat16))

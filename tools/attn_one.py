@@ -1,5 +1,6 @@
 """Run the bf16 whole-sequence attention forward + backward at the ViT-B/16 bs=256 shape a few
-times (the target of a rocprofv3 --pmc pass).  usage: python tools/attn_one.py [iters]"""
+times (the target of a rocprofv3 --pmc pass).  usage: python tools/attn_one.py [iters] [B N H]
+(default shape ViT-B/16 bs 256: 256 197 12; C5 is 64 577 16)"""
 import os
 import sys
 
@@ -12,7 +13,7 @@ from vitmi import ops  # noqa: E402
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    B, N, H = 256, 197, 12
+    B, N, H = (int(a) for a in sys.argv[2:5]) if len(sys.argv) >= 5 else (256, 197, 12)
     D = 64 * H
     g = torch.Generator(device="cuda").manual_seed(0)
     qkv = (torch.randn(B * N, 3 * D, device="cuda", generator=g) * 0.5).to(torch.bfloat16)

@@ -12,12 +12,22 @@
 // would each start their own proxy threads and IPC state.  No RCCL symbol is linked, so
 // the library still loads (and every other entry point works) where RCCL is absent.
 //
-// Thread safety: every entry point that touches the communicator holds g_mu, so the DP
-// watchdog's abort (vitmi_comm_destroy(1) from its own thread, vitmi/dp.py CommWatchdog) never
-// frees the communicator between another thread's null check and its ncclAllReduce.
+// RCCL is taken from VITMI_RCCL_LIB when that is set (a specific build; the CPU tests' stub).
+//
+// Thread safety: g_mu guards only the bookkeeping (which communicator is current, its users),
+// never an RCCL call.  An enqueue takes a reference to the current communicator under the lock,
+// drops the lock and calls RCCL; vitmi_comm_destroy(1) (the DP watchdog's abort, from its own
+// thread: vitmi/dp.py CommWatchdog) detaches the communicator under the lock and calls
+// ncclCommAbort WITHOUT waiting for in-flight enqueues, since an enqueue blocked on a dead peer
+// is exactly what the abort has to release (ncclCommAbort is meant to be called while another
+// thread is inside the communicator).  The wrapper object is freed by whichever of the abort and
+// the last in-flight call finishes last (a reference count), so no call touches a freed handle;
+// a graceful vitmi_comm_destroy(0) waits for in-flight calls before ncclCommDestroy.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <condition_variable>
 #include <mutex>
+#include <stdlib.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <string.h>
@@ -39,9 +49,43 @@ struct Rccl {
 };
 
 Rccl g_rccl;
-std::mutex g_mu;   // guards g_rccl loading, g_comm, g_rank, g_world
-ncclComm_t g_comm = nullptr;
-int g_rank = -1, g_world = 0;
+std::mutex g_mu;                 // guards g_rccl loading, g_cur and every Comm's users / detached
+std::condition_variable g_idle;  // a Comm's users dropped to 0 (graceful destroy waits for it)
+
+// One communicator and the calls currently inside it.
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int rank = -1, world = 0;
+  int users = 0;           // enqueues in flight (between acquire and release)
+  bool detached = false;   // no longer current: destroy / abort took it
+  bool released = false;   // its RCCL handle is gone (aborted or destroyed)
+};
+Comm* g_cur = nullptr;
+
+// A reference to the current communicator for one RCCL call, or null.
+Comm* acquire() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_cur) return nullptr;
+  ++g_cur->users;
+  return g_cur;
+}
+
+// Drop a reference; the last one out of a detached and released communicator frees it.
+void release(Comm* c) {
+  bool free_it = false;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    free_it = --c->users == 0 && c->detached && c->released;
+    if (c->users == 0) g_idle.notify_all();
+  }
+  if (free_it) delete c;
+}
+
+struct Ref {   // scope guard around acquire / release
+  Comm* c;
+  Ref() : c(acquire()) {}
+  ~Ref() { if (c) release(c); }
+};
 
 template <typename F>
 bool sym(void* h, const char* name, F& out) {
@@ -49,8 +93,16 @@ bool sym(void* h, const char* name, F& out) {
   return out != nullptr;
 }
 
+int bind_rccl(void* h);
+
 int load_rccl() {
   if (g_rccl.handle) return VITMI_OK;
+  const char* pinned = getenv("VITMI_RCCL_LIB");
+  if (pinned && *pinned) {
+    void* hp = dlopen(pinned, RTLD_NOW | RTLD_LOCAL);
+    if (!hp) return fail(VITMI_ERR_COMM, "comm: cannot load VITMI_RCCL_LIB=%s (%s)", pinned, dlerror());
+    return bind_rccl(hp);
+  }
   // already mapped (torch's bundled copy is loaded by its file name, it has no SONAME)?
   const char* names[] = {"librccl.so", "librccl.so.1"};
   void* h = nullptr;
@@ -60,6 +112,10 @@ int load_rccl() {
     for (const char* n : names)
       if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
   if (!h) return fail(VITMI_ERR_COMM, "comm: cannot load librccl.so (%s)", dlerror());
+  return bind_rccl(h);
+}
+
+int bind_rccl(void* h) {
   Rccl r;
   r.handle = h;
   if (!sym(h, "ncclGetUniqueId", r.get_unique_id) || !sym(h, "ncclCommInitRank", r.init_rank) ||
@@ -104,7 +160,7 @@ extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
   VITMI_CHECK_ARG(uid != nullptr, "comm_init: uid is null");
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    VITMI_CHECK_ARG(g_comm == nullptr, "comm_init: a communicator already exists (vitmi_comm_destroy first)");
+    VITMI_CHECK_ARG(g_cur == nullptr, "comm_init: a communicator already exists (vitmi_comm_destroy first)");
     if (int rc = load_rccl()) return rc;
   }
   ncclUniqueId id;
@@ -113,14 +169,17 @@ extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
   // the communicator binds to the calling thread's current HIP device; the rendezvous with the
   // other ranks runs without the lock held
   if (ncclResult_t r = g_rccl.init_rank(&c, world, id, rank)) return nccl_fail("ncclCommInitRank", r);
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (g_comm != nullptr) {
+  std::unique_lock<std::mutex> lk(g_mu);
+  if (g_cur != nullptr) {
+    lk.unlock();
     g_rccl.destroy(c);
     return fail(VITMI_ERR_INVALID, "comm_init: a communicator was created concurrently");
   }
-  g_comm = c;
-  g_rank = rank;
-  g_world = world;
+  Comm* n = new Comm;
+  n->comm = c;
+  n->rank = rank;
+  n->world = world;
+  g_cur = n;
   return VITMI_OK;
 }
 
@@ -137,19 +196,19 @@ extern "C" int vitmi_comm_library(char* path, int len) {
 
 extern "C" int vitmi_comm_info(int* rank, int* world) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (rank) *rank = g_rank;
-  if (world) *world = g_world;
-  return g_comm ? VITMI_OK : fail(VITMI_ERR_INVALID, "comm_info: no communicator");
+  if (rank) *rank = g_cur ? g_cur->rank : -1;
+  if (world) *world = g_cur ? g_cur->world : 0;
+  return g_cur ? VITMI_OK : fail(VITMI_ERR_INVALID, "comm_info: no communicator");
 }
 
 extern "C" int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, int op, vitmi_stream_t side,
                                           void* ready_event) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  VITMI_CHECK_ARG(g_comm != nullptr, "comm_allreduce_async: no communicator (never initialised, or aborted)");
   VITMI_CHECK_ARG(count >= 0, "comm_allreduce_async: negative count");
   VITMI_CHECK_ARG(op == VITMI_REDUCE_SUM || op == VITMI_REDUCE_AVG, "comm_allreduce_async: bad op %d", op);
   ncclDataType_t t;
   VITMI_CHECK_ARG(dtype_of(dtype, t), "comm_allreduce_async: bad dtype %d", dtype);
+  Ref ref;
+  VITMI_CHECK_ARG(ref.c != nullptr, "comm_allreduce_async: no communicator (never initialised, or aborted)");
   if (count == 0) return VITMI_OK;
   VITMI_CHECK_ARG(ptr != nullptr, "comm_allreduce_async: null buffer");
   hipStream_t s = (hipStream_t)side;
@@ -158,38 +217,46 @@ extern "C" int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, i
     if (e != hipSuccess) return fail(VITMI_ERR_HIP, "comm_allreduce_async: hipStreamWaitEvent: %s", hipGetErrorString(e));
   }
   const ncclRedOp_t rop = op == VITMI_REDUCE_AVG ? ncclAvg : ncclSum;
-  if (ncclResult_t r = g_rccl.all_reduce(ptr, ptr, (size_t)count, t, rop, g_comm, s)) return nccl_fail("ncclAllReduce", r);
+  // no lock held: an abort from another thread may release this call (it then fails here)
+  if (ncclResult_t r = g_rccl.all_reduce(ptr, ptr, (size_t)count, t, rop, ref.c->comm, s)) return nccl_fail("ncclAllReduce", r);
   return VITMI_OK;
 }
 
 extern "C" int vitmi_comm_broadcast(void* ptr, int64_t count, int dtype, int root, vitmi_stream_t stream) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  VITMI_CHECK_ARG(g_comm != nullptr, "comm_broadcast: vitmi_comm_init first");
-  VITMI_CHECK_ARG(root >= 0 && root < g_world, "comm_broadcast: bad root %d", root);
   ncclDataType_t t;
   VITMI_CHECK_ARG(dtype_of(dtype, t), "comm_broadcast: bad dtype %d", dtype);
+  Ref ref;
+  VITMI_CHECK_ARG(ref.c != nullptr, "comm_broadcast: vitmi_comm_init first");
+  VITMI_CHECK_ARG(root >= 0 && root < ref.c->world, "comm_broadcast: bad root %d", root);
   if (count == 0) return VITMI_OK;
-  if (ncclResult_t r = g_rccl.broadcast(ptr, ptr, (size_t)count, t, root, g_comm, (hipStream_t)stream))
+  if (ncclResult_t r = g_rccl.broadcast(ptr, ptr, (size_t)count, t, root, ref.c->comm, (hipStream_t)stream))
     return nccl_fail("ncclBroadcast", r);
   return VITMI_OK;
 }
 
 extern "C" int vitmi_comm_check(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_comm) return VITMI_OK;
+  Ref ref;
+  if (!ref.c) return VITMI_OK;
   ncclResult_t a = ncclSuccess;
-  if (ncclResult_t r = g_rccl.async_err(g_comm, &a)) return nccl_fail("ncclCommGetAsyncError", r);
+  if (ncclResult_t r = g_rccl.async_err(ref.c->comm, &a)) return nccl_fail("ncclCommGetAsyncError", r);
   if (a != ncclSuccess && a != ncclInProgress) return nccl_fail("asynchronous error", a);
   return VITMI_OK;
 }
 
 extern "C" int vitmi_comm_destroy(int abort) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_comm) return VITMI_OK;
-  ncclComm_t c = g_comm;
-  g_comm = nullptr;
-  g_rank = -1;
-  g_world = 0;
-  ncclResult_t r = abort ? g_rccl.abort(c) : g_rccl.destroy(c);
+  std::unique_lock<std::mutex> lk(g_mu);
+  Comm* c = g_cur;
+  if (!c) return VITMI_OK;
+  g_cur = nullptr;          // new calls see no communicator from here on
+  c->detached = true;
+  // graceful: ncclCommDestroy must not run under an in-flight call; abort: do not wait
+  if (!abort) g_idle.wait(lk, [c] { return c->users == 0; });
+  lk.unlock();
+  ncclResult_t r = abort ? g_rccl.abort(c->comm) : g_rccl.destroy(c->comm);
+  lk.lock();
+  c->released = true;
+  const bool free_it = c->users == 0;
+  lk.unlock();
+  if (free_it) delete c;
   return r ? nccl_fail(abort ? "ncclCommAbort" : "ncclCommDestroy", r) : VITMI_OK;
 }

@@ -28,6 +28,13 @@ int fail(int code, const char* fmt, ...);
     if (!(cond)) return ::vitmi::fail(VITMI_ERR_INVALID, __VA_ARGS__); \
   } while (0)
 
+#define VITMI_HIP_CHECK(call, what)                                           \
+  do {                                                                        \
+    hipError_t e_ = (call);                                                   \
+    if (e_ != hipSuccess)                                                     \
+      return ::vitmi::fail(VITMI_ERR_HIP, "%s: %s", what, hipGetErrorString(e_)); \
+  } while (0)
+
 #define VITMI_LAUNCH_CHECK(what)                                              \
   do {                                                                        \
     hipError_t e_ = hipGetLastError();                                        \

@@ -200,6 +200,17 @@ thread_local FoldBatch t_batch;
 thread_local int t_njobs = 0;
 thread_local bool t_defer = false;
 thread_local hipStream_t t_stream = nullptr;
+// streams that ran folds since vitmi_fold_begin (vitmi_fold_end orders its stream after them)
+constexpr int FOLD_STREAMS = 8;
+thread_local hipStream_t t_fold_streams[FOLD_STREAMS];
+thread_local int t_nfold_streams = 0;
+thread_local hipEvent_t t_fold_events[FOLD_STREAMS] = {};
+
+void note_fold_stream(hipStream_t s) {
+  for (int i = 0; i < t_nfold_streams; ++i)
+    if (t_fold_streams[i] == s) return;
+  if (t_nfold_streams < FOLD_STREAMS) t_fold_streams[t_nfold_streams++] = s;
+}
 
 int launch_folds(const FoldBatch& b, int n, hipStream_t s) {
   if (n == 0) return VITMI_OK;
@@ -219,6 +230,7 @@ int launch_folds(const FoldBatch& b, int n, hipStream_t s) {
 int flush_folds() {
   const int n = t_njobs;
   t_njobs = 0;
+  if (n > 0) note_fold_stream(t_stream);
   return launch_folds(t_batch, n, t_stream);
 }
 }  // namespace
@@ -591,11 +603,22 @@ extern "C" uint32_t vitmi_dropout_hash(uint32_t seed, uint32_t site, uint32_t ro
 
 extern "C" int vitmi_fold_begin(void) {
   t_defer = true;
+  t_nfold_streams = 0;
   return VITMI_OK;
 }
 
 extern "C" int vitmi_fold_end(vitmi_stream_t stream) {
-  (void)stream;   // the queued folds run on the stream their producers ran on
   t_defer = false;
-  return flush_folds();
+  // the queued folds run on the stream their producers ran on; `stream` then waits for each such
+  // stream other than itself, so the gradients are final in `stream` order
+  if (int rc = flush_folds()) return rc;
+  const hipStream_t s = (hipStream_t)stream;
+  for (int i = 0; i < t_nfold_streams; ++i) {
+    if (t_fold_streams[i] == s) continue;
+    if (!t_fold_events[i]) VITMI_HIP_CHECK(hipEventCreateWithFlags(&t_fold_events[i], hipEventDisableTiming), "fold_end");
+    VITMI_HIP_CHECK(hipEventRecord(t_fold_events[i], t_fold_streams[i]), "fold_end");
+    VITMI_HIP_CHECK(hipStreamWaitEvent(s, t_fold_events[i], 0), "fold_end");
+  }
+  t_nfold_streams = 0;
+  return VITMI_OK;
 }

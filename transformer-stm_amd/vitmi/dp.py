@@ -46,9 +46,11 @@ REDUCE_SUM, REDUCE_AVG = 0, 1
 class VitmiComm:
     """The library's RCCL communicator (one per process, bound to the current HIP device).
 
-    Every call into the library's comm entry points holds ``self._lock`` (and the library holds
-    its own mutex around the communicator): the CommWatchdog thread's abort can never interleave
-    with the training thread's enqueue of an all-reduce on the same communicator."""
+    No lock is held across a library call: the CommWatchdog thread's abort must be able to run
+    while the training thread is blocked inside an all-reduce enqueue (a dead peer), which the
+    abort then releases with an error.  The library reference-counts the communicator, so an
+    abort never frees it under a call in flight (csrc/comm.cpp).  ``self._lock`` only makes
+    ``destroy`` happen once."""
 
     def __init__(self, rank: int, world: int, uid: bytes):
         if len(uid) != UID_BYTES:
@@ -65,8 +67,7 @@ class VitmiComm:
 
     def _call(self, name: str, *args) -> int:
         from ._lib import lib
-        with self._lock:
-            return getattr(lib(), name)(*args)
+        return getattr(lib(), name)(*args)
 
     @staticmethod
     def unique_id() -> bytes:
@@ -84,7 +85,8 @@ class VitmiComm:
         from ._lib import check
         assert buf.is_cuda and buf.is_contiguous() and buf.dtype in _DT
         dt = _DT[buf.dtype]
-        check(self._call("vitmi_comm_allreduce_async", buf.data_ptr(), buf.numel(), dt, op, side.cuda_stream,
+        check(self._call("vitmi_comm_allreduce_async", buf.data_ptr(), buf.numel(), dt, op,
+                         side.cuda_stream if side is not None else None,
                          ready.cuda_event if ready is not None else None), "comm_allreduce_async")
 
     def broadcast(self, buf: torch.Tensor, root: int = 0) -> None:
@@ -122,8 +124,7 @@ class VitmiComm:
             if not self._live:
                 return
             self._live = False
-            rc = lib().vitmi_comm_destroy(int(abort))
-        check(rc, "comm_destroy")
+        check(lib().vitmi_comm_destroy(int(abort)), "comm_destroy")
 
 
 def exchange_unique_id(rank: int, world: int, store=None, key: str = "vitmi_comm_uid") -> bytes:
@@ -279,7 +280,7 @@ class GradReducer:
         self._prev_reserve: Optional[int] = None
         self.launch_log: List[Tuple[int, int]] = []   # (ready prefix, bucket index) for tests
         self.readiness: Optional["ArenaReadiness"] = None   # set by attach()
-        # the watchdog thread only aborts the communicator (whose entry points are locked); the CU
+        # the watchdog thread only aborts the communicator (which releases a blocked enqueue); the CU
         # reservation is a training-thread global, restored by finish()/start()/abort()
         self.watchdog = (CommWatchdog(timeout_s, self._abort_comm)
                          if comm is not None and timeout_s and timeout_s > 0 else None)

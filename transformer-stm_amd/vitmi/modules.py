@@ -724,13 +724,13 @@ class ParamArena:
             return self.view(self.grad, p)
         return None
 
-    def bind_grads(self) -> None:
+    def bind_grads(self, fill_missing: bool = True) -> None:
         """Make every ``.grad`` the parameter's view of the flat gradient buffer (copying a
-        gradient that lives elsewhere; a missing one counts as zero): the fused optimizer and
-        the DP buckets read the flat buffer.  After a backward from ``begin_step`` this only
-        checks pointers."""
+        gradient that lives elsewhere): the fused optimizer and the DP buckets read the flat
+        buffer.  A missing gradient counts as zero (``fill_missing``) or is left missing.  After a
+        backward from ``begin_step`` this only checks pointers."""
         ps, views = self.params, self._grad_views
-        if all(p.grad is None for p in ps):
+        if fill_missing and all(p.grad is None for p in ps):
             self.grad.zero_()
             for p, v in zip(ps, views):
                 p.grad = v
@@ -738,11 +738,27 @@ class ParamArena:
         for p, v in zip(ps, views):
             g = p.grad
             if g is None:
-                v.zero_()
-                p.grad = v
+                if fill_missing:
+                    v.zero_()
+                    p.grad = v
             elif g.data_ptr() != v.data_ptr():
                 v.copy_(g)
                 p.grad = v
+
+    def runs(self, select: List[bool]) -> List[tuple]:
+        """(start, end) element ranges of the flat buffers covering the selected parameters, one per
+        run of consecutive selected parameters (alignment padding included: it holds zeros)."""
+        out: List[tuple] = []
+        for p, sel in zip(self.params, select):
+            if not sel:
+                continue
+            o = self.offsets[id(p)]
+            e = o + (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+            if out and out[-1][1] == o:
+                out[-1] = (out[-1][0], e)
+            else:
+                out.append((o, e))
+        return out
 
 
 # ======================================================================= model

@@ -85,12 +85,22 @@ class Adam:
                 raise RuntimeError("vitmi Adam: the model's parameter arena was rebuilt after the optimizer "
                                    "was created (model moved?); create the optimizer after placing the model")
             # the launch reads the flat gradient buffer: every .grad must be its arena view (they
-            # are after a backward from an arena forward; a gradient set elsewhere is copied in)
-            arena.bind_grads()
+            # are after a backward from an arena forward; a gradient set elsewhere is copied in).
+            # Parameters with no gradient (frozen, or zero_grad(set_to_none) and no backward) are
+            # not stepped, as in torch / Keras: the launch covers the runs of the arena between them
+            stepping = [p.requires_grad and p.grad is not None for p in arena.params]
+            if not any(stepping):
+                return
             lp = arena.flat_lp
-            check(lib().vitmi_adam_step(arena.numel, ops._p(arena.flat), ops._p(arena.grad), ops._p(self._m),
-                                        ops._p(self._v), ops._p(lp), alpha, self.beta_1, self.beta_2, self.epsilon,
-                                        self.grad_scale, ops._s()), "adam_step")
+            if not all(stepping):
+                arena.refresh_lp()          # the skipped parameters' shadow must be current too
+            arena.bind_grads(fill_missing=all(stepping))
+            for s0, e0 in arena.runs(stepping):
+                n = e0 - s0
+                check(lib().vitmi_adam_step(n, ops._p(arena.flat[s0:]), ops._p(arena.grad[s0:]), ops._p(self._m[s0:]),
+                                            ops._p(self._v[s0:]), ops._p(lp[s0:]) if lp is not None else None, alpha,
+                                            self.beta_1, self.beta_2, self.epsilon, self.grad_scale, ops._s()),
+                      "adam_step")
             arena.mark_lp_fresh()
             return
         for p, m, v in zip(self.params, self._m, self._v):
