@@ -5,6 +5,7 @@ rounding r(x) = float(bf16(x)) inserted exactly where the GPU path rounds an ope
 activation, one class of roundings switched on or off at a time:
 
     W     every GEMM weight (patch, qkv, proj, fc1, fc2)      -- the bf16 operand shadow
+    WB    the block GEMM weights (qkv, proj, fc1, fc2)
     WP    the patch-embedding weight alone
     P     the im2col patches                                   -- patch GEMM A operand
     LN    the LayerNorm outputs h1, h2                         -- qkv / fc1 A operands
@@ -39,6 +40,7 @@ from oracle import vit_ref  # noqa: E402
 from vitmi.config import preset  # noqa: E402
 
 ALL = ("W", "P", "LN", "QKV", "PR", "O", "ACT")
+BLOCK_W = ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight")
 
 
 def r(x, on):
@@ -49,6 +51,7 @@ def forward(img, p, cfg, rnd):
     R = lambda key, x: r(x, key in rnd)  # noqa: E731
     w = {k: (R("W", v) if k.endswith("weight") and ("proj" in k or "qkv" in k or "fc" in k) else v) for k, v in p.items()}
     w["patch_embed.proj.weight"] = R("WP", w["patch_embed.proj.weight"])   # WP: the patch weight alone
+    w = {k: (R("WB", v) if k.endswith(BLOCK_W) else v) for k, v in w.items()}
     B = img.shape[0]
     D, H = cfg.embed_dim, cfg.num_heads
     dh = D // H
@@ -90,6 +93,12 @@ SETTINGS = [
     ("bf16x3 on W, LN, O, ACT; patches, q/k/v and P bf16", {"QKV", "PR", "P"}),
     ("bf16x3 on the block GEMMs; the patch GEMM (patches, weight) bf16", {"QKV", "PR", "P", "WP"}),
     ("the patch weight only", {"WP"}),
+    ("block weights only", {"WB"}),
+    ("split O, GELU, patch GEMM; LN outputs and block weights bf16", {"QKV", "PR", "LN", "WB"}),
+    ("split W, O, GELU, patch GEMM; LN outputs bf16", {"QKV", "PR", "LN"}),
+    ("split LN, O, GELU, patch GEMM; block weights bf16", {"QKV", "PR", "WB"}),
+    ("split GELU, patch GEMM; LN, O, block weights bf16", {"QKV", "PR", "LN", "WB", "O"}),
+    ("split O, GELU, W; LN outputs and the patches bf16", {"QKV", "PR", "LN", "P"}),
     ("none (GEMM operands split and attention in fp32)", set()),
 ]
 
