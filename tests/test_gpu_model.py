@@ -24,6 +24,9 @@ BF16_VITB_LOGITS = 7e-3      # measured 2.7e-3 (bs 2, default init) / 3.6e-3 (ra
 BF16_C1_LOGITS = 5e-3        # measured 2.2e-3
 BF16_VITL_LOGITS = 1e-2      # measured 4.9e-3 (ViT-L/16@384, depth 4)
 BF16_GRADS = 1.5e-2          # worst relative grad error measured 6.9e-3 (C1) / 7.5e-3 (ViT-B depth 12)
+# ||d|| / sum_i ||g_i|| (per-image contributions, vit_ref.per_image_grad_scale): the bf16 backward's
+# rounding relative to what it rounds; first GPU measurement sets the bound at about 2x (round 5)
+BF16_GRADS_COND = 1e-2
 
 
 def gpu_step(cfg, params, img, tgt):
@@ -389,12 +392,20 @@ def test_bf16x3_knob_streamed_attention_n290():
 def test_bf16x3_knob_small_model_matches_oracle():
     """bf16x3 on the C1 shape (ViT-Ti/16 64^2, N = 17) and on a ragged token count (48^2, N = 10):
     logits within the north star's 1e-3 (C1 measures 3.3e-4: the bf16 q, k, v and P), gradients
-    (the bf16 backward) at SURVEY §8d's bf16 bound 2e-2 (the worst, block 0's norm1.bias at 5
-    images, measures 1.7e-2: a column sum over 50 rows)."""
+    (the bf16 backward) at SURVEY §8d's bf16 bound 2e-2 against the oracle (the worst, block 0's
+    norm1.bias at 5 images, measured 1.7e-2).  These batches are mildly ill-conditioned (labels
+    3:2 and 4:1, kappa up to 7, oracle.vit_ref.per_image_grad_scale), so the bf16 rounding of
+    each image's contribution is also held to the conditioned bound ||d|| <= tol * sum_i ||g_i||
+    with a tighter tol (BF16_GRADS_COND)."""
     for cfg in (config_c1(dtype="bf16x3"), config_c1(dtype="bf16x3", img_size=48)):
         params = vit_ref.init_params(cfg, seed=3)
         img, tgt = vit_ref.synthetic_batch(cfg, 5)
-        e3, w3 = compare(cfg, params, img, tgt, logit_tol=1e-3, grad_tol=2e-2, loss_tol=1e-3)
-        eb, wb = compare(cfg.replace(dtype="bf16"), params, img, tgt, logit_tol=5e-3, grad_tol=2e-2, loss_tol=2e-2)
-        print(f"{cfg.img_size}px: logits bf16x3 {e3:.3e}, bf16 {eb:.3e}; "
-              f"worst grad bf16x3 {w3[1]} {w3[0]:.3e}, bf16 {wb[1]} {wb[0]:.3e}")
+        scale = vit_ref.per_image_grad_scale(img, tgt, params, cfg)
+        _, _, g_ref = vit_ref.forward_backward(img, tgt, params, cfg)
+        for c, ltol, lstol in ((cfg, 1e-3, 1e-3), (cfg.replace(dtype="bf16"), 5e-3, 2e-2)):
+            e, w = compare(c, params, img, tgt, logit_tol=ltol, grad_tol=2e-2, loss_tol=lstol)
+            _, _, g = gpu_step(c, params, img, tgt)
+            cond = max(((g[k] - g_ref[k]).double().norm().item() / scale[k], k) for k in g_ref)
+            print(f"{cfg.img_size}px {c.dtype}: logits {e:.3e}; worst grad {w[1]} {w[0]:.3e}; "
+                  f"conditioned {cond[1]} {cond[0]:.3e}")
+            assert cond[0] <= BF16_GRADS_COND, cond
