@@ -25,7 +25,8 @@ BF16_C1_LOGITS = 5e-3        # measured 2.2e-3
 BF16_VITL_LOGITS = 1e-2      # measured 4.9e-3 (ViT-L/16@384, depth 4)
 BF16_GRADS = 1.5e-2          # worst relative grad error measured 6.9e-3 (C1) / 7.5e-3 (ViT-B depth 12)
 # ||d|| / sum_i ||g_i|| (per-image contributions, vit_ref.per_image_grad_scale): the bf16 backward's
-# rounding relative to what it rounds; first GPU measurement sets the bound at about 2x (round 5)
+# rounding relative to what it rounds; measured <= 4.5e-3 (C1 / 48 px / N = 290, bf16 and bf16x3,
+# round 5), the bound about 2x that
 BF16_GRADS_COND = 1e-2
 
 
@@ -355,14 +356,14 @@ def test_bf16x3_knob_streamed_attention_n290():
     vitmi/modules.py _forward_x3).  Logits of the knob within 1e-3 of the fp32 oracle.
 
     Gradients, against the ORACLE, two ways (SURVEY §8d bf16 bound 2e-2):
-      * a well-conditioned batch (both images labelled 0): ||d|| / ||g|| <= 2e-2 per tensor;
+      * a well-conditioned batch (both images labelled 0): ||d|| / ||g|| <= 1.2e-2 per tensor;
       * the seed's own labels (0, 1): the two images' gradients nearly cancel here (the model
         gives both noise images almost the same logits, so g = g_0 + g_1 with ||g_i|| up to 75 x
         ||g||: kappa, oracle.vit_ref.per_image_grad_scale).  A backward that rounds each image's
         contribution to bf16 (2^-9) cannot meet 2e-2 of ||g|| there: even the fp32 path's error grows
         by the same factor (6e-7 at N = 197 -> 4.6e-5 here; tools/diag_grad_precision.py).  The bound
-        is applied to what the rounding acts on: ||d|| <= 2e-2 * sum_i ||g_i|| (the same bound at
-        kappa = 1), and kappa is asserted so the case stays the ill-conditioned one."""
+        is applied to what the rounding acts on: ||d|| <= tol * sum_i ||g_i|| (BF16_GRADS_COND; the
+        same bound at kappa = 1), and kappa is asserted so the case stays the ill-conditioned one."""
     cfg = config_c1(dtype="bf16x3", img_size=272, depth=4)
     params = vit_ref.init_params(cfg, seed=8)
     img, tgt = vit_ref.synthetic_batch(cfg, 2)
@@ -381,22 +382,24 @@ def test_bf16x3_knob_streamed_attention_n290():
                 err = (l - l_ref).abs().max().item()
                 print(f"   bf16x3 logits max-abs {err:.3e}")
                 assert err <= 1e-3
-            if labels.sum() == 0:
+            if labels.sum() == 0:       # measured 5.8e-3 (bf16), 5.4e-3 (bf16x3)
                 assert kappa < 1.5
-                assert plain[0] <= 2e-2, plain
-            else:
+                assert plain[0] <= 1.2e-2, plain
+            else:                        # kappa 92; conditioned 4.1e-3 (bf16), 3.4e-3 (bf16x3)
                 assert kappa > 30
-                assert cond[0] <= 2e-2, cond
+                assert cond[0] <= BF16_GRADS_COND, cond
 
 
 def test_bf16x3_knob_small_model_matches_oracle():
     """bf16x3 on the C1 shape (ViT-Ti/16 64^2, N = 17) and on a ragged token count (48^2, N = 10):
-    logits within the north star's 1e-3 (C1 measures 3.3e-4: the bf16 q, k, v and P), gradients
+    logits within the north star's 1e-3 (C1 measures 3.4e-4: the bf16 q, k, v and P), gradients
     (the bf16 backward) at SURVEY §8d's bf16 bound 2e-2 against the oracle (the worst, block 0's
-    norm1.bias at 5 images, measured 1.7e-2).  These batches are mildly ill-conditioned (labels
-    3:2 and 4:1, kappa up to 7, oracle.vit_ref.per_image_grad_scale), so the bf16 rounding of
-    each image's contribution is also held to the conditioned bound ||d|| <= tol * sum_i ||g_i||
-    with a tighter tol (BF16_GRADS_COND)."""
+    norm1.bias at 5 images, measures 1.98e-2 for the knob and 1.92e-2 for bf16; a CPU emulation of
+    the same roundings, tools/precision_emulate_bwd.py, finds no single bf16 rounding whose removal
+    brings it under 1.1e-2: profiles/r05_precision/).  These batches are mildly ill-conditioned
+    (labels 3:2 and 4:1, kappa up to 7, oracle.vit_ref.per_image_grad_scale), so the bf16 rounding
+    of each image's contribution is also held to the conditioned bound ||d|| <= tol * sum_i ||g_i||
+    with a tighter tol (BF16_GRADS_COND; measured <= 4.5e-3)."""
     for cfg in (config_c1(dtype="bf16x3"), config_c1(dtype="bf16x3", img_size=48)):
         params = vit_ref.init_params(cfg, seed=3)
         img, tgt = vit_ref.synthetic_batch(cfg, 5)

@@ -16,7 +16,7 @@ bf16 rounding inserted where the GPU path rounds, one class at a time:
 
 Prints, per setting, the worst and the median relative gradient error over all parameter
 tensors against the unrounded fp32 oracle, plus the logits error.
-usage: python tools/precision_emulate_bwd.py [--config c1|vitb] [--batch B] [--labels zero|seed]"""
+usage: python tools/precision_emulate_bwd.py [--config c1|vitb] [--batch B] [--labels zero|seed] [--knob]"""
 from __future__ import annotations
 
 import argparse
@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--batch", type=int, default=5)
     ap.add_argument("--labels", choices=["seed", "zero"], default="seed")
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--knob", action="store_true", help="settings around the bf16x3 knob's roundings")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     if args.config == "c1":
@@ -127,6 +128,9 @@ def main():
                 ("backward gradient roundings only", set(BWD))]
     settings += [(f"only {k}", {k}) for k in FWD + BWD]
     settings += [(f"all but {k}", set(FWD + BWD) - {k}) for k in FWD + BWD]
+    if args.knob:   # the bf16x3 knob: split (unrounded) W and A, bf16 q/k/v/P and bf16 backward
+        knob = {"QKV"} | set(BWD)
+        settings = [("knob (QKV + backward)", knob)] + [(f"knob but {k}", knob - {k}) for k in ("QKV",) + BWD]
     print(f"{args.config} bs {args.batch} labels {tgt.tolist()}")
     print(f"{'bf16 rounding of':<40} {'worst grad rel':>14} {'(tensor)':<28} {'median':>9} {'logits':>9}")
     for name, on in settings:
