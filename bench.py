@@ -272,10 +272,11 @@ def main():
                     help="c3: ViT-B/16 224px bs 256/GPU (the headline metric); c5: ViT-L/16 384px bs 64/GPU "
                          "(BASELINE config 5, N = 577 tokens); c2: ViT-S/16 224px bs 128 fp32 (BASELINE config "
                          "2). c2 and c5 are secondary lines, not the headline")
-    ap.add_argument("--dtype", choices=["bf16", "bf16x3", "fp32"], default=None,
+    ap.add_argument("--dtype", choices=["bf16", "bf16x3", "bf16f8", "fp32"], default=None,
                     help="override the config's compute dtype (the precision knob: bf16x3 = split-bf16 forward "
-                         "GEMM operands + fp32 attention forward, fp32 = exact-fp32 MFMA everywhere; both keep the "
-                         "logits within 1e-3 of the CPU oracle at ViT-B depth 12)")
+                         "GEMM operands, bf16f8 = the same with the correction products in block-scaled e4m3, "
+                         "fp32 = exact-fp32 MFMA everywhere; all keep the logits within 1e-3 of the CPU oracle "
+                         "at ViT-B depth 12)")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5, "
                                                              "128 for c2)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
@@ -388,8 +389,10 @@ def main():
     if world > 1:
         dist.barrier()
     M, F_, D = B * cfg.seq_len, cfg.mlp_dim, cfg.embed_dim
-    # the bf16x3 knob's fc1 GEMM runs over K' = 3D ([hi|hi|lo] x [hi|lo|hi] operand rows)
+    # the bf16x3 knob's fc1 GEMM runs over K' = 3D ([hi|hi|lo] x [hi|lo|hi] operand rows); the
+    # bf16f8 one over D bf16 + 2D e4m3 k (2D bf16-equivalent MFMA work; its launch is keyed by D)
     KD = 3 * D if cfg.dtype == "bf16x3" else D
+    KW = 2 * D if cfg.dtype == "bf16f8" else KD
     events = ops.set_probe((M, F_, KD))       # fc1 forward GEMM launches
     if args.stats_out:
         _lib.lib().vitmi_stats_enable(1)
@@ -421,7 +424,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     imgs = B * world * args.steps / elapsed
     kern_ms = sum(a.elapsed_time(b) for a, b in events) / max(1, len(events))
-    kflop = 2.0 * M * F_ * KD                 # MFMA work of the launch (3x the product's for bf16x3)
+    kflop = 2.0 * M * F_ * KW                 # MFMA work of the launch (3x / 2x the product's for bf16x3 / bf16f8)
     achieved = kflop / (kern_ms * 1e-3) / 1e12 if events else 0.0
     step_flops = cfg.flops_per_image_fwd_bwd() * B * world
     out = {
@@ -445,12 +448,14 @@ def main():
                    "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
                    "model": model_name, "global_batch": B * world, "seq_len": cfg.seq_len,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd {'fp32' if fp32 else 'bf16'} [{M}x{F_}x{KD}] +bias+GELU"
-                               + (" (bf16x3 split operands)" if KD != D else ""),
+        "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd {'fp32' if fp32 else 'bf16'} [{M}x{F_}x{KW}] +bias+GELU"
+                               + (" (bf16x3 split operands)" if KD != D else "")
+                               + (" (bf16f8: bf16 hi.hi + e4m3 corrections, bf16-equivalent K)" if KW != KD else ""),
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,
                      "launches_timed": len(events), "avg_launch_ms": round(kern_ms, 4),
-                     "algorithmic_bytes": (4 if fp32 else 2) * (M * KD + F_ * KD + (4 if KD != D else 2) * M * F_)},
+                     "algorithmic_bytes": (4 if fp32 else 2) * (M * KW + F_ * KW
+                                                                + (4 if KD != D else 3 if KW != KD else 2) * M * F_)},
         "optimizer_ms": phases_ms.get("optimizer"),
         "phases_ms": phases_ms,
         "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / (peak * world), 4),
@@ -507,6 +512,7 @@ def secondary_lines():
             # the precision knob: ViT-B/16 C3 with logits within 1e-3 of the fp32 reference, by
             # split-bf16 forward operands (bf16x3) or exact-fp32 arithmetic throughout (fp32)
             "c3_bf16x3": ["--config", "c3", "--dtype", "bf16x3", "--steps", "5", "--warmup", "2"],
+            "c3_bf16f8": ["--config", "c3", "--dtype", "bf16f8", "--steps", "5", "--warmup", "2"],
             "c3_fp32": ["--config", "c3", "--dtype", "fp32", "--steps", "3", "--warmup", "1"]}
     for cfg, extra in runs.items():
         log = os.path.join(tempfile.gettempdir(), f"vitmi_secondary_{cfg}.log")

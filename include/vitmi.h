@@ -35,8 +35,16 @@ enum {
   VITMI_F32 = 0,
   VITMI_BF16 = 1,
   VITMI_F64 = 2,    /* comm only */
-  VITMI_BF16X3 = 3  /* vitmi_layernorm_fwd's y only: bf16 rows [hi | hi | lo] of 3D columns, the
+  VITMI_BF16X3 = 3, /* vitmi_layernorm_fwd's y only: bf16 rows [hi | hi | lo] of 3D columns, the
                        split-bf16 A operand of the precision knob (vitmi_split_bf16x3) */
+  VITMI_BF16F8 = 4  /* the knob's cheaper form (ViTConfig dtype "bf16f8"): a row of K values is 4K
+                       bytes (2K bf16 units), [hi = bf16(x) | two OCP e4m3 parts of K bytes], the
+                       fp8 part [hi8 | lo8] for an A operand (activations) and [lo8 | hi8] for a
+                       weight, hi8 = e4m3(hi), lo8 = e4m3((x - hi) * 2^9) (vitmi_split_bf16f8).
+                       vitmi_linear_fwd dtype (x and w both so; K % 64 == 0, N % 16 == 0): the
+                       GEMM runs K/64 bf16 K-steps (hi.hi) and K/64 block-scaled fp8 K-steps
+                       (hi.lo + lo.hi, v_mfma_scale_f32_16x16x128_f8f6f4): 2K-equivalent MFMA
+                       work instead of bf16x3's 3K.  Also vitmi_layernorm_fwd's y dtype. */
 };
 
 /* GEMM epilogues (all apply `bias` (fp32, may be NULL) first where it applies) */
@@ -59,6 +67,9 @@ size_t vitmi_aux_tiled_bytes(int64_t rows, int64_t cols);
  * (hi = bf16(a), lo = bf16(a - hi): the split A operand of the next GEMM, vitmi_split_bf16x3
  * pattern 0); aux = gelu'(u) as for BIAS_GELU. */
 #define VITMI_EPI_SPLIT_X3 0x200
+/* OR'ed into BIAS_GELU of vitmi_linear_fwd with dtype VITMI_BF16F8 (y_dtype VITMI_BF16): y is
+ * [M][2N] bf16 units, each row the VITMI_BF16F8 A-operand layout of gelu(u); aux as for BIAS_GELU. */
+#define VITMI_EPI_SPLIT_F8 0x400
 
 enum { VITMI_LOSS_CE = 0, VITMI_LOSS_MSE = 1 };
 
@@ -149,6 +160,7 @@ size_t vitmi_bias_grad_workspace_size(int64_t M, int64_t N);
  * LayerNorm over the last dim D (layers.LayerNormalization, models/CvT(Par).py:248,328;
  * old_codes/MS_CvT.py:39-45).  x is fp32 [M][ldx]; y [M][ldy] of y_dtype; mean/rstd fp32 [M].
  * y_dtype VITMI_BF16X3: y is bf16 [M][ldy >= 3D], each row [hi | hi | lo] of the fp32 result.
+ * y_dtype VITMI_BF16F8: y is [M][ldy >= 2D] bf16 units, each row the VITMI_BF16F8 A-operand layout.
  */
 int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx, const float* gamma,
                         const float* beta, float eps, void* y, int y_dtype, int64_t ldy,
@@ -176,6 +188,10 @@ int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float scale, con
  * bf16 [B*N][3*H*dh], each row [hi | hi | lo] of the fp32 output (the out-projection GEMM's
  * split A operand, vitmi_split_bf16x3 pattern 0).  N <= 256 (the whole-sequence kernel). */
 int vitmi_attention_fwd_x3(int B, int N, int H, int dh, float scale, const void* qkv, void* o, void* o3,
+                           float* lse, vitmi_stream_t stream);
+/* As vitmi_attention_fwd_x3 for the VITMI_BF16F8 knob: o8 is [B*N][2*H*dh] bf16 units, each row the
+ * VITMI_BF16F8 A-operand layout [hi | hi8 | lo8] of the fp32 output. */
+int vitmi_attention_fwd_f8(int B, int N, int H, int dh, float scale, const void* qkv, void* o, void* o8,
                            float* lse, vitmi_stream_t stream);
 int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, const void* qkv,
                         const void* o, const void* dout, const float* lse, void* dqkv,
@@ -383,6 +399,10 @@ int vitmi_gather_rows(int64_t n, int64_t row_bytes, const void* src, int64_t n_s
  * The activation operands come split straight from their producers: vitmi_layernorm_fwd (y dtype
  * VITMI_BF16X3), vitmi_attention_fwd_x3 and the fc1 epilogue (VITMI_EPI_SPLIT_X3). */
 int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
+                       int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
+/* VITMI_BF16F8 rows: src fp32 [rows][ld_src] -> dst [rows][ld_dst >= 2K bf16 units], pattern 0 the
+ * A-operand layout [hi | hi8 | lo8], pattern 1 the weight layout [hi | lo8 | hi8]; hi_copy as above. */
+int vitmi_split_bf16f8(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
                        int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
 
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */

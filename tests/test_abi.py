@@ -68,6 +68,31 @@ def test_precision_knob_entry_points_validate_on_the_host():
     assert lib.vitmi_split_bf16x3(4, 8, 16, 8, 16, 24, 2, None, 0, None) == 1
 
 
+def test_bf16f8_knob_entry_points_validate_on_the_host():
+    """The VITMI_BF16F8 paths (the knob's e4m3-correction form) reject bad arguments before any launch."""
+    lib = _lib.lib()
+    # LayerNorm VITMI_BF16F8 output rows are 2D bf16 units
+    rc = lib.vitmi_layernorm_fwd(4, 64, 16, 64, 16, 16, 1e-6, 16, 4, 64, 16, 16, None)
+    assert rc == 1 and b"2D" in lib.vitmi_last_error()
+    # linear_fwd on VITMI_BF16F8 operands: K % 64 and N % 16
+    rc = lib.vitmi_linear_fwd(4, 128, 128, 96, 16, 16, None, 16, 0, 0, None, None, None, 0, None)
+    assert rc == 1 and b"K % 64" in lib.vitmi_last_error()
+    rc = lib.vitmi_linear_fwd(4, 128, 120, 128, 16, 16, None, 16, 0, 0, None, None, None, 0, None)
+    assert rc == 1 and b"N % 16" in lib.vitmi_last_error()
+    # VITMI_EPI_SPLIT_F8 needs VITMI_BF16F8 operands
+    rc = lib.vitmi_linear_fwd(1, 128, 128, 128, 16, 16, None, 16, 1, 0x401, 16, None, None, 0, None)
+    assert rc == 1 and b"SPLIT_F8" in lib.vitmi_last_error()
+    # the generic GEMM entry (wgrad-style split) does not take them
+    rc = lib.vitmi_gemm(4, 1, 1, 128, 128, 128, 16, 256, 16, 256, 16, 128, 0, 4, None, None, 0, None, 0,
+                        None, 0, None)
+    assert rc == 1 and b"BF16F8" in lib.vitmi_last_error()
+    # split_bf16f8: ld_dst >= 2K and the pattern
+    assert lib.vitmi_split_bf16f8(4, 8, 16, 8, 16, 12, 0, None, 0, None) == 1
+    assert lib.vitmi_split_bf16f8(4, 8, 16, 8, 16, 16, 2, None, 0, None) == 1
+    rc = lib.vitmi_attention_fwd_f8(1, 300, 2, 64, 0.125, 16, 16, 16, 16, None)
+    assert rc == 1 and b"256" in lib.vitmi_last_error()
+
+
 def test_workspace_queries_are_pure_host():
     lib = _lib.lib()
     assert lib.vitmi_attention_bwd_workspace_size(2, 197, 12) == 2 * 197 * 12 * 4

@@ -1,0 +1,136 @@
+"""Would the precision knob meet 1e-3 with its two correction products in block-scaled e4m3?
+(verdict r04 item 2; a CPU emulation, round 5)
+
+The bf16x3 knob forms every forward GEMM as hi.hi + hi.lo + lo.hi over bf16 pairs (x = hi + lo),
+3K of bf16 MFMA work.  The correction terms are 2^-9 of the main one, so they could run as ONE
+fp8 product over 2K, [hi_x | lo_x] . [lo_w | hi_w]^T, with OCP e4m3 operands and power-of-two
+(E8M0) scales per block of `block` consecutive k (v_mfma_scale_f32_16x16x128_f8f6f4: 2x the bf16
+rate, so 2K-equivalent instead of 3K).  This script emulates exactly that on the fp32 oracle's
+forward (oracle/vit_ref.py, models/CvT(Par).py:261-289 restated): per-block scale
+2^ceil(log2(amax / 448)), round to e4m3 (torch.float8_e4m3fn), products accumulated in fp32;
+q, k, v and P stay bf16 as in the knob.  Prints logits max-abs against the fp32 oracle.
+
+usage: python tools/precision_emulate_fp8.py [--depth 12] [--batch 2] [--init random|default]"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "transformer-stm_amd"))
+
+from oracle import vit_ref  # noqa: E402
+from vitmi.config import preset  # noqa: E402
+
+E4M3_MAX = 448.0
+
+
+def rb(x):
+    return x.bfloat16().float()
+
+
+def q8(x, block):
+    """x [..., K] -> e4m3 values with one power-of-two scale per `block` consecutive k (block 0:
+    one scale per row, -1: one per tensor), returned dequantised in fp32."""
+    if block < 0:
+        s = torch.exp2(torch.ceil(torch.log2(x.abs().amax().clamp_min(2.0 ** -126) / E4M3_MAX)))
+        return (x / s).to(torch.float8_e4m3fn).float() * s
+    K = x.shape[-1]
+    b = K if block == 0 else block
+    pad = (-K) % b
+    xp = F.pad(x, (0, pad)) if pad else x
+    xb = xp.reshape(*xp.shape[:-1], -1, b)
+    amax = xb.abs().amax(dim=-1, keepdim=True).clamp_min(2.0 ** -126)
+    s = torch.exp2(torch.ceil(torch.log2(amax / E4M3_MAX)))
+    q = (xb / s).to(torch.float8_e4m3fn).float() * s
+    q = q.reshape(*xp.shape)
+    return q[..., :K] if pad else q
+
+
+def q8_fixed(x, scale):
+    """e4m3 with a fixed power-of-two scale (saturating at +-448), dequantised."""
+    return (x / scale).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).float() * scale
+
+
+def make_mm(mode, block):
+    def mm(a, w):
+        """a [..., K] @ w[N, K]^T as the GPU knob would form it."""
+        if mode == "fp32":
+            return a @ w.t()
+        ha, hw = rb(a), rb(w)
+        if mode == "bf16":
+            return ha @ hw.t()
+        la, lw = a - ha, w - hw
+        if mode == "x3":
+            return ha @ hw.t() + (ha @ lw.t() + la @ hw.t())
+        if mode == "f8fixed":   # no amax anywhere: hi at scale 1, lo = x - hi at scale 2^-9
+            lo_s = 2.0 ** -9
+            return ha @ hw.t() + (q8_fixed(ha, 1.0) @ q8_fixed(lw, lo_s).t() + q8_fixed(la, lo_s) @ q8_fixed(hw, 1.0).t())
+        # fp8 corrections: [hi_a | lo_a] . [lo_w | hi_w]^T, each half its own block scales
+        return ha @ hw.t() + (q8(ha, block) @ q8(lw, block).t() + q8(la, block) @ q8(hw, block).t())
+    return mm
+
+
+def forward(img, p, cfg, mm):
+    B = img.shape[0]
+    D, H = cfg.embed_dim, cfg.num_heads
+    dh = D // H
+    Pz = cfg.patch_size
+    patches = F.unfold(img, Pz, stride=Pz).transpose(1, 2)
+    x = mm(patches, p["patch_embed.proj.weight"].reshape(D, -1)) + p["patch_embed.proj.bias"]
+    x = torch.cat([p["cls_token"].expand(B, 1, D), x], dim=1)
+    if cfg.pos_embed:
+        x = x + p["pos_embed"]
+    N = x.shape[1]
+    scale = dh ** -0.5 if cfg.attn_scale == "head" else D ** -0.5
+    for i in range(cfg.depth):
+        pre = f"blocks.{i}."
+        h = vit_ref.layer_norm(x, p[pre + "norm1.weight"], p[pre + "norm1.bias"], cfg.ln_eps)
+        qkv = rb(mm(h, p[pre + "attn.qkv.weight"]) + p[pre + "attn.qkv.bias"])        # q, k, v bf16
+        q, k, v = (t.reshape(B, N, H, dh).transpose(1, 2) for t in qkv.split(D, dim=-1))
+        a = rb(torch.softmax((q @ k.transpose(-1, -2)) * scale, dim=-1))              # P bf16
+        o = (a @ v).transpose(1, 2).reshape(B, N, D)
+        x = x + mm(o, p[pre + "attn.proj.weight"]) + p[pre + "attn.proj.bias"]
+        h2 = vit_ref.layer_norm(x, p[pre + "norm2.weight"], p[pre + "norm2.bias"], cfg.ln_eps)
+        act = F.gelu(mm(h2, p[pre + "mlp.fc1.weight"]) + p[pre + "mlp.fc1.bias"])
+        x = x + mm(act, p[pre + "mlp.fc2.weight"]) + p[pre + "mlp.fc2.bias"]
+    c = vit_ref.layer_norm(x[:, 0], p["norm.weight"], p["norm.bias"], cfg.ln_eps)
+    return c @ p["head.weight"].t() + p["head.bias"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--depth", type=int, default=12)
+    ap.add_argument("--batch", type=int, default=2)
+    ap.add_argument("--init", choices=["random", "default"], default="random")
+    ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    args = ap.parse_args()
+    torch.set_num_threads(args.threads)
+    cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype="fp32", depth=args.depth)
+    params = vit_ref.init_params(cfg, seed=0, randomize_all=args.init == "random")
+    img, _ = vit_ref.synthetic_batch(cfg, args.batch)
+    settings = [("bf16 operands (q/k/v, P bf16)", "bf16", 0),
+                ("bf16x3 knob as built", "x3", 0),
+                ("hi.hi bf16 + e4m3 corrections, scale per 32 k (MX)", "f8", 32),
+                ("hi.hi bf16 + e4m3 corrections, scale per 128 k", "f8", 128),
+                ("hi.hi bf16 + e4m3 corrections, one scale per row", "f8", 0),
+                ("hi.hi bf16 + e4m3 corrections, one scale per tensor", "f8", -1),
+                ("hi.hi bf16 + e4m3 corrections, fixed scales (hi 1, lo 2^-9)", "f8fixed", 0)]
+    with torch.no_grad():
+        ref = vit_ref.forward(img, params, cfg)
+        base = forward(img, params, cfg, make_mm("fp32", 0))
+        print(f"ViT-B/16 224px depth {args.depth} bs {args.batch}, {args.init} init; "
+              f"emulator (q/k/v, P bf16; GEMMs fp32) vs oracle: {(base - ref).abs().max().item():.2e}")
+        print(f"{'GEMM operands':<56} logits max-abs vs fp32")
+        for name, mode, block in settings:
+            err = (forward(img, params, cfg, make_mm(mode, block)) - ref).abs().max().item()
+            print(f"{name:<56} {err:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -185,6 +185,46 @@ __device__ __forceinline__ void store_tile32(char* scr, const f32x16 (&acc)[2], 
   asm volatile("" ::: "memory");
 }
 
+// The e4m3 parts of the same tile (the VITMI_BF16F8 knob, common.h split_f8): hi8 = e4m3(bf16(v)),
+// lo8 = e4m3((v - bf16(v)) 2^9) of v = acc * mul, 64 bytes per row into rs8h / rs8l, through the
+// per-wave image as 32 rows x 64 B (16 B per lane, two stores per part)
+__device__ __forceinline__ void store_tile32_f8(char* scr, const f32x16 (&acc)[2], float mul,
+                                                __amdgpu_buffer_rsrc_t rs8h, __amdgpu_buffer_rsrc_t rs8l,
+                                                int64_t ld_bytes, int row0, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  uint32_t lo8[2][4];
+#pragma unroll
+  for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      f32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[c2][4 * g4 + i] * mul;
+      bf16x4 hi;
+      uint32_t hi8;
+      split_f8(v, hi, hi8, lo8[c2][g4]);
+      *(uint32_t*)(scr + r * ST_PITCH + 32 * c2 + 8 * g4 + 4 * h) = hi8;
+    }
+  const int rr = lane >> 2, cc = lane & 3;
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const u32x4 v = *(const u32x4*)(scr + (16 * j + rr) * ST_PITCH + cc * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(v, part ? rs8l : rs8h,
+                                             (uint32_t)((int64_t)(row0 + 16 * j + rr) * ld_bytes + cc * 16), 0, 0);
+    }
+    asm volatile("" ::: "memory");
+    if (part == 0) {
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) *(uint32_t*)(scr + r * ST_PITCH + 32 * c2 + 8 * g4 + 4 * h) = lo8[c2][g4];
+    }
+  }
+}
+
 // Column sums of the rows < nvalid of the tile store_tile32 just wrote (its LDS image, as the
 // stored bf16 values): each lane adds 4 rows x 8 columns, xor-shuffles fold the 8 row groups,
 // and the block's waves (all of which must call) fold through red[wave][64] in wave order into
@@ -661,8 +701,9 @@ __device__ __forceinline__ void stage_seq_dma(char* lds, __amdgpu_buffer_rsrc_t 
 
 // grid B*H, block 64*NW.  Online softmax over key tiles of 64 (a final tile of 32 when NP is
 // an odd multiple of 32); keys >= N exist only in the last tile and are masked there.
-// X3 (the precision knob, vitmi_attention_fwd_x3): also o3 = [hi | hi | lo] rows of the fp32 O.
-template <int NPMAX, bool X3 = false>
+// XM (the precision knob): 1 (vitmi_attention_fwd_x3) also o3 = [hi | hi | lo] rows of the fp32 O;
+// 2 (vitmi_attention_fwd_f8) o3 = the VITMI_BF16F8 A-operand rows [hi | hi8 | lo8] of it.
+template <int NPMAX, int XM = 0>
 __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __restrict__ qkv,
                                                                bf16* __restrict__ o, float* __restrict__ lse,
                                                                int N, int H, float scale,
@@ -768,7 +809,17 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
   const float inv = 1.f / lt;
   store_tile32(smem + wave * ST_BYTES, oacc, inv, ro, ldo, wave * 32, lane_here());
-  if constexpr (X3) {
+  if constexpr (XM == 2) {
+    // hi (bf16) at columns [0, D) of the 2D-wide row, hi8 / lo8 (e4m3 bytes) at bytes 2D / 3D
+    const int64_t ld8 = 2 * ldo;
+    const uint32_t by8 = (uint32_t)((int64_t)N * ld8);
+    char* base8 = (char*)(o3 + (int64_t)b * N * 2 * D);
+    store_tile32(smem + wave * ST_BYTES, oacc, inv, make_rsrc(base8 + hd * DH * 2, by8 - hd * DH * 2), ld8, wave * 32,
+                 lane_here());
+    store_tile32_f8(smem + wave * ST_BYTES, oacc, inv, make_rsrc(base8 + 2 * D + hd * DH, by8 - (2 * D + hd * DH)),
+                    make_rsrc(base8 + 3 * D + hd * DH, by8 - (3 * D + hd * DH)), ld8, wave * 32, lane_here());
+  }
+  if constexpr (XM == 1) {
     // hi = bf16(O) twice, then lo = bf16(O - hi), O = oacc * inv exactly as store_tile32 forms it
     const int64_t ld3 = 3 * ldo;
     const uint32_t by3 = (uint32_t)((int64_t)N * ld3);
@@ -1598,11 +1649,25 @@ extern "C" int vitmi_attention_fwd_x3(int B, int N, int H, int dh, float scale, 
   VITMI_CHECK_ARG(N <= SEQ_MAX, "attention_fwd_x3: N must be <= %d (the whole-sequence kernel)", SEQ_MAX);
   VITMI_CHECK_ARG(qkv && o && o3 && lse, "attention_fwd_x3: null pointer");
   VITMI_CHECK_ARG((int64_t)N * 3 * H * DH * 2 < 0x7fffffffLL, "attention_fwd_x3: one batch row block exceeds 2 GiB");
-  hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, true>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
+  hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, 1>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
                      (hipStream_t)stream, (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o3);
   VITMI_LAUNCH_CHECK("attention_fwd_x3");
   const double bh = (double)B * H;
-  VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, true>), 4.0 * bh * N * N * DH, bh * N * DH * 2 * (3 + 1 + 3) + bh * N * 4);
+  VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, 1>), 4.0 * bh * N * N * DH, bh * N * DH * 2 * (3 + 1 + 3) + bh * N * 4);
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_attention_fwd_f8(int B, int N, int H, int dh, float scale, const void* qkv, void* o, void* o8,
+                                      float* lse, vitmi_stream_t stream) {
+  if (int rc = attn_check(VITMI_BF16, B, N, H, dh)) return rc;
+  VITMI_CHECK_ARG(N <= SEQ_MAX, "attention_fwd_f8: N must be <= %d (the whole-sequence kernel)", SEQ_MAX);
+  VITMI_CHECK_ARG(qkv && o && o8 && lse, "attention_fwd_f8: null pointer");
+  VITMI_CHECK_ARG((int64_t)N * 3 * H * DH * 2 < 0x7fffffffLL, "attention_fwd_f8: one batch row block exceeds 2 GiB");
+  hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, 2>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
+                     (hipStream_t)stream, (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o8);
+  VITMI_LAUNCH_CHECK("attention_fwd_f8");
+  const double bh = (double)B * H;
+  VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, 2>), 4.0 * bh * N * N * DH, bh * N * DH * 2 * (3 + 1 + 2) + bh * N * 4);
   return VITMI_OK;
 }
 

@@ -49,6 +49,38 @@ template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
+// ---------------------------------------------------------------- e4m3 (the bf16f8 knob)
+// VITMI_BF16F8 operands (the precision knob's cheaper form): x = hi + lo, hi = bf16(x); the row
+// carries hi (bf16) and two OCP e4m3 parts, hi8 = e4m3(hi) and lo8 = e4m3(lo * 2^9), so the two
+// correction products hi.lo + lo.hi run as ONE block-scaled fp8 product (the GEMM's fp8 K-steps,
+// scale 2^-9 on the weight operand).  lo = x - hi is exact in fp32 (|lo| <= 2^-9 |x|), and the
+// fixed 2^9 keeps lo8 in e4m3's range wherever x is (tools/precision_emulate_fp8.py).
+constexpr float F8_LO_SCALE = 512.f;
+constexpr int F8_E8M0_ONE = 127, F8_E8M0_LO = 127 - 9;   // E8M0 scales 1 and 2^-9
+// four floats -> four OCP e4m3 bytes (RNE; saturated to +-448 first: the conversion itself would
+// give NaN past the range), little-endian in one dword
+__device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
+  a = __builtin_amdgcn_fmed3f(a, 448.f, -448.f);
+  b = __builtin_amdgcn_fmed3f(b, 448.f, -448.f);
+  c = __builtin_amdgcn_fmed3f(c, 448.f, -448.f);
+  d = __builtin_amdgcn_fmed3f(d, 448.f, -448.f);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+// hi (bf16), hi8 and lo8 (dwords of 4 e4m3) of four fp32 values
+__device__ __forceinline__ void split_f8(f32x4 v, bf16x4& hi, uint32_t& hi8, uint32_t& lo8) {
+  f32x4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = (bf16)v[e];
+    h[e] = (float)hi[e];
+    l[e] = (v[e] - h[e]) * F8_LO_SCALE;
+  }
+  hi8 = e4m3x4(h[0], h[1], h[2], h[3]);
+  lo8 = e4m3x4(l[0], l[1], l[2], l[3]);
+}
+
 // exact-erf GELU (tf.nn.gelu default, models/CvT(Par).py:254) and its derivative
 __device__ __forceinline__ float gelu_f(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));

@@ -96,6 +96,9 @@ struct GemmArgs {
   float* colsum;
   unsigned long long* stamps;        // DIAGNOSTIC build only (VITMI_GEMM_STAMPS)
   int aux_tiled;                     // gelu' in the tile-native layout (VITMI_EPI_AUX_TILED)
+  // VITMI_BF16F8 operands (gemm256<..., F8>): K-steps >= k8 (absolute, 64-bf16 = 128-B steps) are
+  // the rows' e4m3 parts, multiplied by the block-scaled fp8 MFMA; the steps before are bf16
+  int k8;
 };
 
 // Element (row, col) of a tile-native gelu' buffer (VITMI_EPI_AUX_TILED; bf16 elements): 256x256
@@ -122,15 +125,16 @@ __device__ __forceinline__ void tile_rc(const GemmArgs& g, int tl, int& tm, int&
 
 // internal epilogues: split-K partial slab, and GELU / residual with a fused dropout
 // EPI_GELU_X3: BIAS_GELU with the activation written split, [hi | hi | lo] (VITMI_EPI_SPLIT_X3)
-enum { EPI_PARTIAL = 100, EPI_GELU_DROP = 101, EPI_RESIDUAL_DROP = 102, EPI_GELU_X3 = 103 };
+// EPI_GELU_F8: BIAS_GELU with the activation written as VITMI_BF16F8 A-operand rows (VITMI_EPI_SPLIT_F8)
+enum { EPI_PARTIAL = 100, EPI_GELU_DROP = 101, EPI_RESIDUAL_DROP = 102, EPI_GELU_X3 = 103, EPI_GELU_F8 = 104 };
 // the public epilogue an internal one extends, and whether it drops
 template <int EPI> struct EpiOf {
-  static constexpr int base = EPI == EPI_GELU_DROP || EPI == EPI_GELU_X3 ? VITMI_EPI_BIAS_GELU
+  static constexpr int base = EPI == EPI_GELU_DROP || EPI == EPI_GELU_X3 || EPI == EPI_GELU_F8 ? VITMI_EPI_BIAS_GELU
                               : EPI == EPI_RESIDUAL_DROP ? VITMI_EPI_RESIDUAL : EPI;
   static constexpr bool drop = EPI == EPI_GELU_DROP || EPI == EPI_RESIDUAL_DROP;
 };
 static inline int epi_base(int epi) {
-  return epi == EPI_GELU_DROP || epi == EPI_GELU_X3 ? VITMI_EPI_BIAS_GELU
+  return epi == EPI_GELU_DROP || epi == EPI_GELU_X3 || epi == EPI_GELU_F8 ? VITMI_EPI_BIAS_GELU
          : epi == EPI_RESIDUAL_DROP ? VITMI_EPI_RESIDUAL : epi;
 }
 // dropout factor (0 or 1/(1-p)) of output element (row, col)
@@ -256,6 +260,20 @@ struct FragReader<float, false, R> {
 
 __device__ __forceinline__ f32x4 mma(const Frag<bf16>& a, const Frag<bf16>& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, c, 0, 0, 0);
+}
+// One block-scaled fp8 MFMA over a 128-B K-step (VITMI_BF16F8): the two bf16 fragments of the
+// step (ks = 0, 1) ARE its 32 e4m3 bytes per lane.  Their k order (chunks lg and 4 + lg of the
+// 128-B row) differs from the instruction's (32 consecutive k per lane group), but A and B use the
+// same one and the scales are uniform, so the dot product is the same.  Scale 2^-9 on the first
+// operand (the weight side: exactly one factor of each product is a lo8 = lo * 2^9), 1 on the other.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mma8(const Frag<bf16>& a0, const Frag<bf16>& a1, const Frag<bf16>& b0,
+                                      const Frag<bf16>& b1, f32x4 c) {
+  const i32x8 a = __builtin_bit_cast(i32x8, __builtin_shufflevector(a0.v, a1.v, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11,
+                                                                    12, 13, 14, 15));
+  const i32x8 b = __builtin_bit_cast(i32x8, __builtin_shufflevector(b0.v, b1.v, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11,
+                                                                    12, 13, 14, 15));
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, F8_E8M0_LO, 0, F8_E8M0_ONE);
 }
 __device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b, f32x4 c) {
 #pragma unroll
@@ -578,7 +596,7 @@ __device__ __forceinline__ void gelu4(f32x4 x, f32x4& a, f32x4& gp) {
 // Waits: vmcnt(8) at P0 retires B1(s), at P1 A1(s), at P3 A0(s+1),B0(s+1); each sits
 // before a barrier that the later reader passes, with one barrier of slack for the
 // staggered group.
-template <bool AK, bool BKM, int EPI, typename TC>
+template <bool AK, bool BKM, int EPI, typename TC, bool F8 = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   using namespace g256;
   // two DMA stages + the bias of the current and the next tile (fp32, double-buffered) + one
@@ -722,6 +740,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
           FIRST && ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[MH * 4 + mt][NH * 2 + nt]);         \
     __builtin_amdgcn_s_setprio(0);                                                              \
   } while (0)
+// the fp8 K-steps of a VITMI_BF16F8 GEMM: one scaled MFMA per (mt, nt) over the step's 128 bytes
+#define MMA4F8(MH, NH, AS, BS)                                                                  \
+  do {                                                                                          \
+    __builtin_amdgcn_s_setprio(1);                                                              \
+    _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                            \
+    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                            \
+      acc[MH * 4 + mt][NH * 2 + nt] = mma8(BS[nt][0], BS[nt][1], AS[mt][0], AS[mt][1],           \
+          FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[MH * 4 + mt][NH * 2 + nt]);                   \
+    __builtin_amdgcn_s_setprio(0);                                                              \
+  } while (0)
 
   int it = jx;
   if (it >= nseq) return;
@@ -784,15 +812,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       do {                                                                                      \
         barrier();                                                                              \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                      \
-        MMA4(MH, NH, AS, BS);                                                                   \
+        if constexpr (F8STEP) MMA4F8(MH, NH, AS, BS);                                           \
+        else MMA4(MH, NH, AS, BS);                                                              \
         barrier();                                                                              \
       } while (0)
       // one K-step; FIRST (step 0 of the unit, peeled) starts the accumulators from zero
       // STEADY: t + 2 < nku is known (both prefetched steps belong to this unit), so the
       // descriptor / step selects below fold away (≈ 40 scalar instructions per K-step)
-      auto kstep = [&](auto first_tag, auto steady_tag, const int t) {
+      auto kstep = [&](auto first_tag, auto steady_tag, auto f8_tag, const int t) {
         constexpr bool FIRST = decltype(first_tag)::value;
         constexpr bool STEADY = decltype(steady_tag)::value;
+        constexpr bool F8STEP = decltype(f8_tag)::value;   // an e4m3 K-step (VITMI_BF16F8)
         // step t+1 (B1, A1 still to issue, buffer buf^1) and step t+2 (A0, B0, buffer buf)
         const bool in1 = STEADY || t + 1 < nku, in2 = STEADY || t + 2 < nku;
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
@@ -833,14 +863,27 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         COMPUTE(1, 0, ay, b0);
         buf ^= 1;
       };
-      kstep(std::true_type{}, std::false_type{}, 0);
-      int t = 1;
-      for (; t + 2 < nku; ++t) kstep(std::false_type{}, std::true_type{}, t);
-      for (; t < nku; ++t) kstep(std::false_type{}, std::false_type{}, t);
+      if constexpr (F8) {
+        // K-steps [0, t8) of this unit are bf16, [t8, nku) e4m3 (wave-uniform)
+        const int t8 = max(0, min(nku, g.k8 - ks0 - (int)(kb / BK)));
+        if (t8 > 0) kstep(std::true_type{}, std::false_type{}, std::false_type{}, 0);
+        else kstep(std::true_type{}, std::false_type{}, std::true_type{}, 0);
+        int t = 1;
+        for (; t < t8 && t + 2 < nku; ++t) kstep(std::false_type{}, std::true_type{}, std::false_type{}, t);
+        for (; t < t8; ++t) kstep(std::false_type{}, std::false_type{}, std::false_type{}, t);
+        for (; t + 2 < nku; ++t) kstep(std::false_type{}, std::true_type{}, std::true_type{}, t);
+        for (; t < nku; ++t) kstep(std::false_type{}, std::false_type{}, std::true_type{}, t);
+      } else {
+        kstep(std::true_type{}, std::false_type{}, std::false_type{}, 0);
+        int t = 1;
+        for (; t + 2 < nku; ++t) kstep(std::false_type{}, std::true_type{}, std::false_type{}, t);
+        for (; t < nku; ++t) kstep(std::false_type{}, std::false_type{}, std::false_type{}, t);
+      }
 #undef COMPUTE
 #undef WAITF
 #undef WAITV
 #undef MMA4
+#undef MMA4F8
 
     stamp(1);
     if ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) {
@@ -872,6 +915,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       if constexpr (EPI == EPI_GELU_X3) {
         rc2 = make_rsrc(cbase + g.N * 2, clamp_bytes(((g.M - m0) * g.ldc - n0 - g.N) * 2));
         rc3 = make_rsrc(cbase + g.N * 4, clamp_bytes(((g.M - m0) * g.ldc - n0 - 2 * g.N) * 2));
+      }
+      // EPI_GELU_F8: the e4m3 parts at bytes 2N + c (hi8) and 3N + c (lo8) of the 4N-byte row
+      if constexpr (EPI == EPI_GELU_F8) {
+        char* b8 = (char*)g.C + m0 * g.ldc * 2 + n0;
+        rc2 = make_rsrc(b8 + 2 * g.N, clamp_bytes((g.M - m0) * g.ldc * 2 - n0 - 2 * g.N));
+        rc3 = make_rsrc(b8 + 3 * g.N, clamp_bytes((g.M - m0) * g.ldc * 2 - n0 - 3 * g.N));
       }
       const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
       const uint32_t vbase = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldc + wn * 64 + lc4) * CES);
@@ -939,6 +988,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         lane_xchg();   // and the next writes of the image stay after these reads
       };
       [[maybe_unused]] bf16x4 lo3[4];   // EPI_GELU_X3: lo = bf16(a - hi) of the row group's fragments
+      [[maybe_unused]] uint32_t f8h[4], f8l[4];   // EPI_GELU_F8: hi8, lo8 (4 e4m3 each) of the fragments
+      // EPI_GELU_F8: the image as 16 rows x 64 e4m3 bytes -> one 16-B store per lane
+      [[maybe_unused]] auto flush8 = [&](__amdgpu_buffer_rsrc_t r, int mi) {
+        lane_xchg();
+        const int r16 = lane >> 2, c4 = lane & 3;
+        const u32x4 d = *(const u32x4*)(scr + r16 * EPI_PITCH + c4 * 16);
+        const uint32_t vo = n0 + wn * 64 + c4 * 16 < g.N
+                                ? (uint32_t)((int64_t)(wm * 128 + r16) * g.ldc * 2 + wn * 64 + c4 * 16) : 0x80000000u;
+        asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen" VITMI_ST_C16 "\n\ts_nop 1"
+                     :: "v"(d), "v"(vo), "s"(r), "s"((int)(mi * 16 * g.ldc * 2)) : "memory");
+        lane_xchg();
+      };
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand.
       // Returns the fragment of the second output (gelu') for BIAS_GELU.
       auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) -> bf16x4 {
@@ -985,6 +1046,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) lo3[ni][e] = (bf16)(v[e] - (float)o[e]);
           }
+          if constexpr (EPI == EPI_GELU_F8) {
+            bf16x4 h_;
+            split_f8(v, h_, f8h[ni], f8l[ni]);
+          }
         }
         return u;
       };
@@ -1000,6 +1065,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) lds_put(ni, lo3[ni]);
             flush(rc3, g.ldc, mi);
+          }
+          if constexpr (EPI == EPI_GELU_F8) {   // hi8 then lo8 through the same image
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) *(uint32_t*)(scr + lr * EPI_PITCH + ni * 16 + lc4) = f8h[ni];
+            flush8(rc2, mi);
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) *(uint32_t*)(scr + lr * EPI_PITCH + ni * 16 + lc4) = f8l[ni];
+            flush8(rc3, mi);
           }
           if constexpr (EB == VITMI_EPI_BIAS_GELU) {
             if (g.aux_tiled) {   // straight from the registers: 2 KiB-wide stores (aux_at)
@@ -1210,13 +1283,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       // stores only make the waits below stricter.)
       constexpr int CES2 = sizeof(TC) == 2 && EPI != EPI_PARTIAL && EB != VITMI_EPI_ACCUM &&
                            EB != VITMI_EPI_RESIDUAL;
-      constexpr int EP = CES2 ? (EPI == EPI_GELU_X3 ? 64 : EB == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU ? 32 : 16)
+      constexpr int EP = CES2 ? (EPI == EPI_GELU_X3 ? 64 : EPI == EPI_GELU_F8 ? 48
+                                 : EB == VITMI_EPI_BIAS_GELU || EPI == VITMI_EPI_DGELU ? 32 : 16)
                               : (EB == VITMI_EPI_RESIDUAL || EPI == VITMI_EPI_ACCUM ? 64
                                  : EPI == VITMI_EPI_DGELU ? 48 : 32);
       ep_ops = ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) ? 32 : EP;
     }
     if (!has_next) break;
-    it = itn; tile = next; m0 = m0n; n0 = n0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
+    it = itn; tile = next; m0 = m0n; n0 = n0n; ks0 = ks0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
   }
   // the leading group owes the staggered group its extra barrier: equal counts per wave
   if (!wm) barrier();
@@ -1467,7 +1541,7 @@ static void gemm_stat(const void* kernel, const GemmArgs& g) {
   VITMI_STAT(kernel, 2.0 * M * N * K, bytes);
 }
 
-template <typename T, bool AK, bool BKM, int EPI, typename TC>
+template <typename T, bool AK, bool BKM, int EPI, typename TC, bool F8 = false>
 static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     if (big) {
@@ -1490,7 +1564,8 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       g.ksplit = 0;
       // measured: pays off for long reductions (>= 16 K-steps) and for the DGELU epilogue
       // (whose partial units skip its aux loads); a wash or a loss for K = 768 otherwise
-      const bool tail_ok = g.k_per_split / 64 >= VITMI_TAIL_MINK || EPI == VITMI_EPI_DGELU;
+      // (EPI_GELU_F8: the fix-up kernel does not write the split-f8 rows, so its tiles stay whole)
+      const bool tail_ok = (g.k_per_split / 64 >= VITMI_TAIL_MINK || EPI == VITMI_EPI_DGELU) && EPI != EPI_GELU_F8;
       if (splits == 1 && tail_ok && EPI != EPI_PARTIAL && EPI != VITMI_EPI_ACCUM && g.tail_ws &&
           tail_plan(nwg, gx, (int)(g.k_per_split / 64), S, ks, ntail) &&
           g.tail_ws_bytes >= (size_t)ntail * S * 256 * 256 * sizeof(float)) {
@@ -1502,10 +1577,10 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
 #ifdef VITMI_GEMM_STAMPS
       g.stamps = g_stamps;
 #endif
-      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
+      hipLaunchKernelGGL((gemm256_kernel<AK, BKM, EPI, TC, F8>), dim3(gx, 1, splits), dim3(512), 0, s, g, units);
       VITMI_LAUNCH_CHECK("gemm256_kernel");
-      gemm_stat<T, EPI, TC>((const void*)gemm256_kernel<AK, BKM, EPI, TC>, g);
-      if (units != nwg) {
+      gemm_stat<T, EPI, TC>((const void*)gemm256_kernel<AK, BKM, EPI, TC, F8>, g);
+      if constexpr (EPI != EPI_GELU_F8) if (units != nwg) {
         const int blocks = (ntail * 256 * 64 + 255) / 256;
         hipLaunchKernelGGL((gemm_tail_fixup_kernel<T, TC, EPI>), dim3(blocks), dim3(256), 0, s, g, ntail);
         VITMI_LAUNCH_CHECK("gemm_tail_fixup_kernel");
@@ -1519,6 +1594,7 @@ static int launch_t(GemmArgs g, int splits, bool big, hipStream_t s) {
       return VITMI_OK;
     }
   }
+  if constexpr (F8) return fail(VITMI_ERR_UNSUPPORTED, "gemm: VITMI_BF16F8 operands need the 256x256 kernel");
   constexpr int BM = 128, BN = 128, WM = 2, WN = 2;
   g.tiles_n = (int)((g.N + BN - 1) / BN);
   const int tiles_m = (int)((g.M + BM - 1) / BM);
@@ -1577,6 +1653,20 @@ static int dispatch(int ak, int bk, int c_dtype, int epi, GemmArgs g, int splits
   return fail(VITMI_ERR_INVALID, "gemm: unknown epilogue %d", epi);
 }
 
+// VITMI_BF16F8 operands (the forward linear layers of the bf16f8 knob): gemm256 only
+static int dispatch_f8(int c_dtype, int epi, GemmArgs g, hipStream_t s) {
+  switch (epi) {
+    case VITMI_EPI_STORE:
+      return c_dtype == VITMI_BF16 ? launch_t<bf16, true, true, VITMI_EPI_STORE, bf16, true>(g, 1, true, s)
+                                   : launch_t<bf16, true, true, VITMI_EPI_STORE, float, true>(g, 1, true, s);
+    case VITMI_EPI_RESIDUAL:
+      return launch_t<bf16, true, true, VITMI_EPI_RESIDUAL, float, true>(g, 1, true, s);
+    case EPI_GELU_F8:
+      return launch_t<bf16, true, true, EPI_GELU_F8, bf16, true>(g, 1, true, s);
+  }
+  return fail(VITMI_ERR_UNSUPPORTED, "gemm: VITMI_BF16F8 operands take STORE, RESIDUAL or BIAS_GELU|SPLIT_F8 (got %d)", epi);
+}
+
 static int bk_of(int dtype) { return dtype == VITMI_BF16 ? 64 : 32; }
 
 // split count for a reduction-heavy GEMM (wgrad): about one full round of blocks
@@ -1609,7 +1699,26 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   if (colsum_done) *colsum_done = false;
   const bool aux_tiled = (epi & VITMI_EPI_AUX_TILED) != 0;
   const bool x3 = (epi & VITMI_EPI_SPLIT_X3) != 0;
-  epi &= ~(VITMI_EPI_AUX_TILED | VITMI_EPI_SPLIT_X3);
+  const bool sf8 = (epi & VITMI_EPI_SPLIT_F8) != 0;
+  epi &= ~(VITMI_EPI_AUX_TILED | VITMI_EPI_SPLIT_X3 | VITMI_EPI_SPLIT_F8);
+  // VITMI_BF16F8: rows of 2K bf16 units ([hi | e4m3 parts]); the kernel sees bf16 operands over
+  // K' = 2K with the e4m3 K-steps from K/64 on (GemmArgs::k8)
+  const bool f8 = dtype == VITMI_BF16F8;
+  int64_t k8 = 0;
+  if (f8) {
+    VITMI_CHECK_ARG(ak && bk && !allow_split, "gemm: VITMI_BF16F8 operands: forward linear layers (k-major A and B) only");
+    VITMI_CHECK_ARG(K % 64 == 0 && N % 16 == 0, "gemm: VITMI_BF16F8 needs K %% 64 == 0 and N %% 16 == 0");
+    VITMI_CHECK_ARG(lda >= 2 * K && ldb >= 2 * K, "gemm: VITMI_BF16F8 rows are 2K bf16 units (lda, ldb >= 2K)");
+    k8 = K / 64;
+    K *= 2;
+    dtype = VITMI_BF16;
+  }
+  if (sf8) {
+    VITMI_CHECK_ARG(f8 && epi == VITMI_EPI_BIAS_GELU && c_dtype == VITMI_BF16,
+                    "gemm: SPLIT_F8 needs BIAS_GELU, VITMI_BF16F8 operands and a bf16 output");
+    VITMI_CHECK_ARG(ldc >= 2 * N, "gemm: SPLIT_F8 needs ldc >= 2N (bf16 units)");
+    epi = EPI_GELU_F8;
+  }
   if (x3) {
     VITMI_CHECK_ARG(epi == VITMI_EPI_BIAS_GELU && dtype == VITMI_BF16 && c_dtype == VITMI_BF16 && ak && bk,
                     "gemm: SPLIT_X3 needs BIAS_GELU, bf16 operands and output, k-major A and B");
@@ -1645,7 +1754,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   // 32-bit buffer offsets: one block's panel must stay under 2 GiB
   VITMI_CHECK_ARG((ak ? 128 * lda : K * lda) * es < 0x7fffffffLL, "gemm: A panel exceeds 2 GiB");
 
-  const bool big = use256(dtype, M, N, K, allow_split && epi == VITMI_EPI_ACCUM);
+  const bool big = f8 || use256(dtype, M, N, K, allow_split && epi == VITMI_EPI_ACCUM);
   if (big) {
     init_cus();
     VITMI_CHECK_ARG(ldc % 8 == 0 && (ldr % 4) == 0 && (ldaux % 8) == 0 && ((uintptr_t)C % 16) == 0,
@@ -1658,6 +1767,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.bias = bias; g.aux = aux; g.ldaux = ldaux;
   g.residual = residual; g.ldr = ldr;
   g.aux_tiled = aux_tiled;
+  g.k8 = (int)k8;
   if (drop) {
     g.drop_seed = drop->drop_seed; g.drop_site = drop->drop_site;
     g.drop_thresh = drop->drop_thresh; g.drop_scale = drop->drop_scale;
@@ -1697,6 +1807,10 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
     if (colsum && big_ok && dtype == VITMI_BF16 && epi == VITMI_EPI_DGELU) {
       g.colsum = colsum;      // fused column sums (gemm256 DGELU epilogue only)
       if (colsum_done) *colsum_done = true;
+    }
+    if (f8) {
+      VITMI_CHECK_ARG(big_ok, "gemm: VITMI_BF16F8 needs >= 2 K-steps");
+      return dispatch_f8(c_dtype, epi, g, s);
     }
     if (dtype == VITMI_BF16) return dispatch<bf16>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
     return dispatch<float>(ak, bk, c_dtype, epi, g, 1, big_ok, s);
@@ -1771,6 +1885,7 @@ extern "C" size_t vitmi_aux_tiled_bytes(int64_t rows, int64_t cols) {
 }
 
 extern "C" size_t vitmi_linear_fwd_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
+  if (dtype == VITMI_BF16F8) return tail_ws_bytes(M, N, 2 * K);   // (K' = 2K bf16 units)
   return use256(dtype, M, N) ? tail_ws_bytes(M, N, K) : 0;
 }
 
@@ -1778,11 +1893,12 @@ extern "C" int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, cons
                                 const void* w, const float* bias, void* y, int y_dtype,
                                 int epilogue, void* aux, const float* residual, void* workspace,
                                 size_t ws_bytes, vitmi_stream_t stream) {
-  const int eb = epilogue & ~(VITMI_EPI_AUX_TILED | VITMI_EPI_SPLIT_X3);
+  const int eb = epilogue & ~(VITMI_EPI_AUX_TILED | VITMI_EPI_SPLIT_X3 | VITMI_EPI_SPLIT_F8);
   VITMI_CHECK_ARG(eb == VITMI_EPI_STORE || eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_RESIDUAL,
                   "linear_fwd: bad epilogue %d", epilogue);
-  const int64_t ldy = (epilogue & VITMI_EPI_SPLIT_X3) ? 3 * N : N;
-  return gemm_impl(dtype, 1, 1, M, N, K, x, K, w, K, y, ldy, y_dtype, epilogue, bias, aux, N,
+  const int64_t ldy = (epilogue & VITMI_EPI_SPLIT_X3) ? 3 * N : (epilogue & VITMI_EPI_SPLIT_F8) ? 2 * N : N;
+  const int64_t ldk = dtype == VITMI_BF16F8 ? 2 * K : K;   // VITMI_BF16F8 rows: 2K bf16 units
+  return gemm_impl(dtype, 1, 1, M, N, K, x, ldk, w, ldk, y, ldy, y_dtype, epilogue, bias, aux, N,
                    residual, N, workspace, ws_bytes, (hipStream_t)stream, false);
 }
 

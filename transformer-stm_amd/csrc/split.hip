@@ -12,6 +12,12 @@
 // The weights (and the patch-embedding im2col rows) are split here; the activation operands come
 // split from their producers (LayerNorm, attention, the fc1 epilogue).  An HBM-bound stream:
 // 16-B loads, 8-B stores, 4 columns per thread.
+//
+// The knob's cheaper form (dtype "bf16f8", VITMI_BF16F8): hi stays bf16 and the two correction
+// products run as ONE block-scaled e4m3 product over 2K, so each row carries [hi | hi8 | lo8]
+// (A operand) or [hi | lo8 | hi8] (weight), hi8 = e4m3(hi), lo8 = e4m3((x - hi) * 2^9) (common.h
+// split_f8): 2K-equivalent MFMA work instead of 3K (tools/precision_emulate_fp8.py: logits
+// 1.8-2.3e-4 at ViT-B depth 12, measured 2.2e-4).
 #include "common.h"
 
 namespace vitmi {
@@ -41,6 +47,26 @@ __global__ __launch_bounds__(256) void split3_kernel(int64_t rows, int64_t K, co
   }
 }
 
+// VITMI_BF16F8 rows (common.h split_f8): [hi (K bf16) | fp8 part (2K bytes)], the fp8 part
+// pattern 0 (A operand) [hi8 | lo8], pattern 1 (weights) [lo8 | hi8]; ld_dst in bf16 units
+__global__ __launch_bounds__(256) void split_f8_kernel(int64_t rows, int64_t K, const float* __restrict__ src,
+                                                       int64_t ld_src, bf16* __restrict__ dst, int64_t ld_dst,
+                                                       int pattern, bf16* __restrict__ copy, int64_t ld_copy) {
+  const int64_t K4 = K / 4, total = rows * K4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / K4, c = (i - r * K4) * 4;
+    bf16x4 hi;
+    uint32_t hi8, lo8;
+    split_f8(*(const f32x4*)(src + r * ld_src + c), hi, hi8, lo8);
+    bf16* d = dst + r * ld_dst;
+    *(bf16x4*)(d + c) = hi;
+    uint8_t* f8 = (uint8_t*)(d + K);
+    *(uint32_t*)(f8 + c) = pattern == 0 ? hi8 : lo8;
+    *(uint32_t*)(f8 + K + c) = pattern == 0 ? lo8 : hi8;
+    if (copy) *(bf16x4*)(copy + r * ld_copy + c) = hi;
+  }
+}
+
 static unsigned grid_of(int64_t items) {
   int64_t b = (items + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -65,5 +91,23 @@ extern "C" int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int
                      ld_src, (bf16*)dst, ld_dst, pattern, (bf16*)hi_copy, ld_copy);
   VITMI_LAUNCH_CHECK("split_bf16x3");
   VITMI_STAT(split3_kernel, 0, (double)rows * K * (4 + 6 + (hi_copy ? 2 : 0)));
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_split_bf16f8(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst,
+                                  int64_t ld_dst, int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(rows >= 0 && K > 0 && K % 4 == 0, "split_bf16f8: K must be a positive multiple of 4");
+  VITMI_CHECK_ARG(pattern == 0 || pattern == 1, "split_bf16f8: pattern must be 0 (A: [hi|hi8|lo8]) or 1 (W: [hi|lo8|hi8])");
+  VITMI_CHECK_ARG(ld_src >= K && ld_src % 4 == 0 && ld_dst >= 2 * K && ld_dst % 4 == 0,
+                  "split_bf16f8: strides must be multiples of 4, ld_src >= K, ld_dst >= 2K (bf16 units)");
+  VITMI_CHECK_ARG(!hi_copy || (ld_copy >= K && ld_copy % 4 == 0), "split_bf16f8: bad ld_copy");
+  if (rows == 0) return VITMI_OK;
+  VITMI_CHECK_ARG(src && dst, "split_bf16f8: null pointer");
+  VITMI_CHECK_ARG(((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % 8) == 0 && ((uintptr_t)hi_copy % 8) == 0,
+                  "split_bf16f8: src 16-byte, dst/copy 8-byte alignment required");
+  hipLaunchKernelGGL(split_f8_kernel, dim3(grid_of(rows * K / 4)), dim3(256), 0, (hipStream_t)stream, rows, K, src,
+                     ld_src, (bf16*)dst, ld_dst, pattern, (bf16*)hi_copy, ld_copy);
+  VITMI_LAUNCH_CHECK("split_bf16f8");
+  VITMI_STAT(split_f8_kernel, 0, (double)rows * K * (4 + 4 + (hi_copy ? 2 : 0)));
   return VITMI_OK;
 }

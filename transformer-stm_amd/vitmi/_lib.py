@@ -49,6 +49,7 @@ SIGNATURES = {
     "vitmi_layernorm_bwd_workspace_size": (S, [L, I]),
     "vitmi_attention_fwd": (I, [I, I, I, I, I, F, P, P, P, P]),
     "vitmi_attention_fwd_x3": (I, [I, I, I, I, F, P, P, P, P, P]),
+    "vitmi_attention_fwd_f8": (I, [I, I, I, I, F, P, P, P, P, P]),
     "vitmi_attention_bwd": (I, [I, I, I, I, I, F, P, P, P, P, P, P, S, P]),
     "vitmi_attention_bwd_workspace_size": (S, [I, I, I]),
     "vitmi_patch_im2col": (I, [I, I, I, I, I, P, P, P]),
@@ -59,6 +60,7 @@ SIGNATURES = {
     "vitmi_loss_fwd_bwd": (I, [I, I, I, P, P, P, P, P]),
     "vitmi_cast_f32_bf16": (I, [L, P, P, P]),
     "vitmi_split_bf16x3": (I, [L, L, P, L, P, L, I, P, L, P]),
+    "vitmi_split_bf16f8": (I, [L, L, P, L, P, L, I, P, L, P]),
     "vitmi_fold_begin": (I, []),
     "vitmi_fold_end": (I, [P]),
     "vitmi_dropout_hash": (U, [U, U, U, U]),

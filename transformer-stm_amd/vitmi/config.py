@@ -49,7 +49,9 @@ class ViTConfig:
     # compute dtype of the device path: 'bf16' (MFMA bf16, fp32 accumulate and
     # fp32 residual stream), 'bf16x3' (the precision knob: as bf16, with the forward GEMMs'
     # weights, LayerNorm outputs, attention output and GELU output carried as split hi + lo
-    # bf16 pairs and the attention forward in fp32; logits within 1e-3 of the fp32 reference)
+    # bf16 pairs and the attention forward in fp32; logits within 1e-3 of the fp32 reference),
+    # 'bf16f8' (the same knob with the two correction products as one block-scaled e4m3 GEMM
+    # product: 2K- instead of 3K-equivalent forward GEMM work, include/vitmi.h VITMI_BF16F8)
     # or 'fp32' (f32-input MFMA, exact fp32 products)
     dtype: str = "bf16"
 

@@ -361,7 +361,7 @@ class _BlockFn(torch.autograd.Function):
         ctx.prev_bias, ctx.bias_done, ctx.drop = prev_fc2_bias, fc2_bias_done, drop
         ctx.handover = handover
         ctx.aux_tiled = T != F32
-        if blk.dtype == "bf16x3":
+        if blk.dtype in ("bf16x3", "bf16f8"):
             out = _BlockFn._forward_x3(ctx, x2, blk, B, N, D, H, drop, (wq, wo, w1, w2))
             return out.view(B, N, D)
         h1, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, T)
@@ -387,34 +387,41 @@ class _BlockFn(torch.autograd.Function):
         and attention kernels write their outputs split (VITMI_BF16X3, vitmi_attention_fwd_x3);
         q, k, v and the softmax P are bf16 (emulated cost 1.5-1.8e-4 of logits at depth 12).  The
         backward is the bf16 one, on the hi parts (row-strided views of the split operands) and
-        the attention forward's own bf16 O and lse (so P's rows in the backward sum to 1)."""
+        the attention forward's own bf16 O and lse (so P's rows in the backward sum to 1).
+
+        dtype 'bf16f8' (tools/precision_emulate_fp8.py): the same operands as VITMI_BF16F8 rows,
+        [hi | e4m3 hi8, lo8 * 2^9]: hi.hi in bf16 and both corrections as one block-scaled fp8
+        product, 2K-equivalent MFMA work instead of 3K (emulated 1.8-2.3e-4 at depth 12)."""
+        f8 = blk.dtype == "bf16f8"
         if drop is not None:
-            raise ValueError("vitmi: dtype 'bf16x3' is the parity / evaluation knob; dropout is not supported")
+            raise ValueError(f"vitmi: dtype '{blk.dtype}' is the parity / evaluation knob; dropout is not supported")
         n1, n2 = blk.norm1, blk._norm2
         a_, mlp = blk.attn, blk.mlp
+        split = ops.split_bf16f8 if f8 else ops.split_bf16x3
+        ln_out = ops.BF16F8 if f8 else ops.BF16X3
 
         def w3(p):
-            return ops.split_bf16x3(p.detach(), 1)[0]
-        h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, ops.BF16X3)
+            return split(p.detach(), 1)[0]
+        h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, ln_out)
         if N <= ops.ATTN_SEQ_MAX:   # q, k, v leave the GEMM epilogue in bf16
-            qkv = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, torch.bfloat16)
-            o, o3, lse = ops.attention_fwd_x3(qkv, B, N, H, a_.scale)
+            qkv = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, torch.bfloat16, f8=f8)
+            o, o3, lse = (ops.attention_fwd_f8 if f8 else ops.attention_fwd_x3)(qkv, B, N, H, a_.scale)
         else:   # streamed kernels (N > 256): O from the fp32 kernel, o / lse from the bf16 one
-            qkvf = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, F32)
+            qkvf = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, F32, f8=f8)
             qkv = ops.cast_bf16(qkvf)
             of, _ = ops.attention_fwd(qkvf, B, N, H, a_.scale)
             del qkvf
-            o3, _ = ops.split_bf16x3(of, 0)
+            o3, _ = split(of, 0)
             del of
             o, lse = ops.attention_fwd(qkv, B, N, H, a_.scale)
-        x1 = ops.linear_fwd(o3, w3(a_.proj.weight), a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2)
+        x1 = ops.linear_fwd(o3, w3(a_.proj.weight), a_.proj.bias, F32, ops.EPI_RESIDUAL, residual=x2, f8=f8)
         del o3
-        h2_3, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, ops.BF16X3)
-        # GELU in the fc1 epilogue, its output split there (VITMI_EPI_SPLIT_X3); gelu' saved in
-        # the tile-native layout of the bf16 path
+        h2_3, m2, r2 = ops.layernorm_fwd(x1, n2.weight, n2.bias, blk.eps, ln_out)
+        # GELU in the fc1 epilogue, its output split there (VITMI_EPI_SPLIT_X3 / _F8); gelu' saved
+        # in the tile-native layout of the bf16 path
         act3, dg = ops.linear_fwd(h2_3, w3(mlp.fc1.weight), mlp.fc1.bias, torch.bfloat16, ops.EPI_BIAS_GELU,
-                                  aux_tiled=True, split_x3=True)
-        out = ops.linear_fwd(act3, w3(mlp.fc2.weight), mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1)
+                                  aux_tiled=True, split_x3=not f8, split_f8=f8, f8=f8)
+        out = ops.linear_fwd(act3, w3(mlp.fc2.weight), mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, f8=f8)
         # the bf16 backward's operands: hi parts of the split activations (row-strided views)
         h1, h2, act = h1_3[:, :D], h2_3[:, :D], act3[:, :mlp.fc1.weight.shape[0]]
         ctx.aux_tiled = True
@@ -518,14 +525,16 @@ class _EmbedFn(torch.autograd.Function):
         w = _lp(emb, emb.proj.weight, T).reshape(D, -1)
         cls_ = cls.detach().reshape(-1) if cls is not None else None
         pos_ = pos.detach().reshape(-1) if pos is not None else None
-        if emb.norm is None and emb.dtype == "bf16x3":
+        if emb.norm is None and emb.dtype in ("bf16x3", "bf16f8"):
             # the precision knob: patches and weight as split-bf16 pairs (tools/precision_emulate.py:
             # the bf16 patch weight alone costs 1.1e-3 of ViT-B logits error); the backward reads hi
+            f8 = emb.dtype == "bf16f8"
+            split = ops.split_bf16f8 if f8 else ops.split_bf16x3
             pf = ops.patch_im2col(img.contiguous().float(), P, F32)
-            p3, patches = ops.split_bf16x3(pf, 0, hi_copy=True)
+            p3, patches = split(pf, 0, hi_copy=True)
             del pf
-            w3, _ = ops.split_bf16x3(emb.proj.weight.detach().reshape(D, -1), 1)
-            tok = ops.linear_fwd(p3, w3, emb.proj.bias, F32)
+            w3, _ = split(emb.proj.weight.detach().reshape(D, -1), 1)
+            tok = ops.linear_fwd(p3, w3, emb.proj.bias, F32, f8=f8)
             x = ops.tokens_assemble(tok, B, np_, cls_, pos_)
             saved = [patches]
         elif emb.norm is None:

@@ -20,6 +20,8 @@ F32, BF16 = 0, 1
 EPI_STORE, EPI_BIAS_GELU, EPI_RESIDUAL, EPI_DGELU, EPI_ACCUM = 0, 1, 2, 3, 4
 EPI_AUX_TILED = 0x100   # gelu' in the library's tile-native layout (include/vitmi.h)
 EPI_SPLIT_X3 = 0x200    # BIAS_GELU output as [hi | hi | lo] rows (the precision knob)
+EPI_SPLIT_F8 = 0x400    # BIAS_GELU output as VITMI_BF16F8 A-operand rows (the knob's bf16f8 form)
+BF16F8_DT = 4           # VITMI_BF16F8: rows of 2K bf16 units, [hi | e4m3 parts] (include/vitmi.h)
 LOSS_CE, LOSS_MSE = 0, 1
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
@@ -33,8 +35,9 @@ def dt(t: torch.dtype) -> int:
 
 
 def torch_dtype(name: str) -> torch.dtype:
-    """The compute dtype of a ViTConfig.dtype ("bf16x3": bf16 MFMA with split forward operands)."""
-    return {"bf16": torch.bfloat16, "bf16x3": torch.bfloat16, "fp32": torch.float32}[name]
+    """The compute dtype of a ViTConfig.dtype ("bf16x3" / "bf16f8": bf16 MFMA with split forward
+    operands; the backward is bf16)."""
+    return {"bf16": torch.bfloat16, "bf16x3": torch.bfloat16, "bf16f8": torch.bfloat16, "fp32": torch.float32}[name]
 
 
 def _s() -> int:
@@ -112,7 +115,7 @@ def dropout_params(p: float):
 
 def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dtype,
                epilogue: int = EPI_STORE, residual: Optional[Tensor] = None, dropout=None,
-               aux_tiled: bool = False, split_x3: bool = False):
+               aux_tiled: bool = False, split_x3: bool = False, f8: bool = False, split_f8: bool = False):
     """y = x W^T + b (+GELU, +residual).  x [M,K], w [N,K] (same dtype).  Returns y
     (and gelu'(pre-activation), the saved GELU derivative, for EPI_BIAS_GELU).
     ``dropout`` = (seed, site, rate) fuses the dropout of the GELU output / of the branch
@@ -120,13 +123,20 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
     ``aux_tiled`` (bf16): gelu' comes back as an opaque buffer in the tile-native layout, for a
     linear_dgrad(..., EPI_DGELU, aux_tiled=True) of the same [M, N].
     ``split_x3`` (EPI_BIAS_GELU, bf16): y is [M, 3N], each row [hi | hi | lo] of the fp32 GELU
-    output (VITMI_EPI_SPLIT_X3, the precision knob's fc2 A operand)."""
+    output (VITMI_EPI_SPLIT_X3, the precision knob's fc2 A operand).
+    ``f8``: x [M, 2K] and w [N, 2K] are VITMI_BF16F8 rows (split_bf16f8 patterns 0 / 1; the bf16f8
+    knob); ``split_f8`` (with f8, EPI_BIAS_GELU): y is [M, 2N] in the A-operand layout."""
     assert x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N = w.shape[0]
     assert w.shape[1] == K
     assert not split_x3 or (epilogue == EPI_BIAS_GELU and dropout is None)
-    y = torch.empty(*x.shape[:-1], 3 * N if split_x3 else N, dtype=out_dtype, device=x.device)
+    assert not split_f8 or (f8 and epilogue == EPI_BIAS_GELU and dropout is None)
+    if f8:
+        assert x.dtype == torch.bfloat16 and K % 2 == 0 and dropout is None
+        K //= 2
+    y = torch.empty(*x.shape[:-1], 3 * N if split_x3 else 2 * N if split_f8 else N, dtype=out_dtype,
+                    device=x.device)
     aux = None
     aux_tiled = aux_tiled and epilogue == EPI_BIAS_GELU
     if aux_tiled:
@@ -136,13 +146,16 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
         aux = torch.empty(*x.shape[:-1], N, dtype=x.dtype, device=x.device)
     if split_x3:
         epilogue |= EPI_SPLIT_X3
+    if split_f8:
+        epilogue |= EPI_SPLIT_F8
     if residual is not None:
         assert residual.is_contiguous() and residual.dtype == torch.float32
     probe = _PROBE is not None and _PROBE["key"] == (M, N, K)
     if probe:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    nws = lib().vitmi_linear_fwd_workspace_size(dt(x.dtype), M, N, K)
+    xdt = BF16F8_DT if f8 else dt(x.dtype)
+    nws = lib().vitmi_linear_fwd_workspace_size(xdt, M, N, K)
     ws = _ws(nws, x) if nws else None
     if dropout is not None and dropout[2] > 0:
         seed, site, rate = dropout
@@ -151,12 +164,12 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
                                              dt(out_dtype), epilogue, _p(aux), _p(residual), _p(ws), nws,
                                              seed & 0xFFFFFFFF, site, thresh, scale, _s()), "linear_fwd_dropout")
     else:
-        check(lib().vitmi_linear_fwd(dt(x.dtype), M, N, K, _p(x), _p(w), _p(bias), _p(y), dt(out_dtype),
+        check(lib().vitmi_linear_fwd(xdt, M, N, K, _p(x), _p(w), _p(bias), _p(y), dt(out_dtype),
                                      epilogue, _p(aux), _p(residual), _p(ws), nws, _s()), "linear_fwd")
     if probe:
         e1.record()
         _PROBE["events"].append((e0, e1))
-    return (y, aux) if epilogue & ~(EPI_AUX_TILED | EPI_SPLIT_X3) == EPI_BIAS_GELU else y
+    return (y, aux) if epilogue & ~(EPI_AUX_TILED | EPI_SPLIT_X3 | EPI_SPLIT_F8) == EPI_BIAS_GELU else y
 
 
 def dropout_apply(x: Tensor, seed: int, site: int, rate: float, out_dtype: torch.dtype) -> Tensor:
@@ -246,20 +259,24 @@ def gemm(a: Tensor, b: Tensor, a_kmajor: bool, b_kmajor: bool, M: int, N: int, K
 
 # ---------------------------------------------------------------- LayerNorm
 BF16X3 = "bf16x3"   # layernorm_fwd out_dtype of the precision knob (VITMI_BF16X3)
+BF16F8 = "bf16f8"   # ... of its bf16f8 form (VITMI_BF16F8 A-operand rows)
 ATTN_SEQ_MAX = 256  # largest N of the whole-sequence attention kernels (csrc/attention.hip SEQ_MAX)
 
 
 def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype):
     """x fp32 [..., D] (rows may be strided) -> (y [rows, D] contiguous, mean, rstd).
-    out_dtype BF16X3: y is bf16 [rows, 3D], each row [hi | hi | lo] of the fp32 result."""
+    out_dtype BF16X3: y is bf16 [rows, 3D], each row [hi | hi | lo] of the fp32 result;
+    BF16F8: y is [rows, 2D] bf16 units, each row the VITMI_BF16F8 A-operand layout."""
     assert x.dtype == torch.float32
     M, ldx = _rows(x)
     D = x.shape[-1]
-    x3 = out_dtype == BF16X3
-    y = torch.empty(M, 3 * D if x3 else D, dtype=torch.bfloat16 if x3 else out_dtype, device=x.device)
+    x3, f8 = out_dtype == BF16X3, out_dtype == BF16F8
+    width = 3 * D if x3 else 2 * D if f8 else D
+    y = torch.empty(M, width, dtype=torch.bfloat16 if x3 or f8 else out_dtype, device=x.device)
     mean = torch.empty(M, dtype=torch.float32, device=x.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x.device)
-    check(lib().vitmi_layernorm_fwd(M, D, _p(x), ldx, _p(w), _p(b), float(eps), _p(y), 3 if x3 else dt(out_dtype),
+    code = 3 if x3 else BF16F8_DT if f8 else dt(out_dtype)
+    check(lib().vitmi_layernorm_fwd(M, D, _p(x), ldx, _p(w), _p(b), float(eps), _p(y), code,
                                     y.shape[1], _p(mean), _p(rstd), _s()), "layernorm_fwd")
     return y, mean, rstd
 
@@ -322,6 +339,19 @@ def attention_fwd_x3(qkv: Tensor, B: int, N: int, H: int, scale: float):
     check(lib().vitmi_attention_fwd_x3(B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(o3), _p(lse), _s()),
           "attention_fwd_x3")
     return o, o3, lse
+
+
+def attention_fwd_f8(qkv: Tensor, B: int, N: int, H: int, scale: float):
+    """As attention_fwd_x3 for the bf16f8 knob: o8 is [B*N, 2*H*64] bf16 units, each row the
+    VITMI_BF16F8 A-operand layout of the fp32 output."""
+    D = qkv.shape[-1] // 3
+    assert qkv.is_contiguous() and qkv.dtype == torch.bfloat16 and qkv.numel() == B * N * 3 * D
+    o = torch.empty(B * N, D, dtype=torch.bfloat16, device=qkv.device)
+    o8 = torch.empty(B * N, 2 * D, dtype=torch.bfloat16, device=qkv.device)
+    lse = torch.empty(B * H, N, dtype=torch.float32, device=qkv.device)
+    check(lib().vitmi_attention_fwd_f8(B, N, H, D // H, float(scale), _p(qkv), _p(o), _p(o8), _p(lse), _s()),
+          "attention_fwd_f8")
+    return o, o8, lse
 
 
 def attention_bwd(qkv: Tensor, o: Tensor, do: Tensor, lse: Tensor, B: int, N: int, H: int,
@@ -500,6 +530,20 @@ def split_bf16x3(x: Tensor, pattern: int, hi_copy: bool = False):
     check(lib().vitmi_split_bf16x3(rows, K, _p(x), ld, _p(x3), 3 * K, int(pattern), _p(hi), K, _s()),
           "split_bf16x3")
     return x3, hi
+
+
+def split_bf16f8(x: Tensor, pattern: int, hi_copy: bool = False):
+    """x fp32 [rows, K] (rows may be strided) -> (x8 [rows, 2K] bf16 units, the VITMI_BF16F8 rows
+    [hi | hi8 | lo8] (pattern 0, a GEMM's A operand) or [hi | lo8 | hi8] (pattern 1, its weight),
+    hi bf16 [rows, K] or None) (vitmi_split_bf16f8; hi8 = e4m3(hi), lo8 = e4m3((x - hi) 2^9))."""
+    assert x.dtype == torch.float32
+    rows, ld = _rows(x)
+    K = x.shape[-1]
+    x8 = torch.empty(rows, 2 * K, dtype=torch.bfloat16, device=x.device)
+    hi = torch.empty(rows, K, dtype=torch.bfloat16, device=x.device) if hi_copy else None
+    check(lib().vitmi_split_bf16f8(rows, K, _p(x), ld, _p(x8), 2 * K, int(pattern), _p(hi), K, _s()),
+          "split_bf16f8")
+    return x8, hi
 
 
 def cast_f32(src: Tensor, dst: Optional[Tensor] = None) -> Tensor:
