@@ -38,9 +38,10 @@ enum {
   VITMI_BF16X3 = 3, /* vitmi_layernorm_fwd's y only: bf16 rows [hi | hi | lo] of 3D columns, the
                        split-bf16 A operand of the precision knob (vitmi_split_bf16x3) */
   VITMI_BF16F8 = 4  /* the knob's cheaper form (ViTConfig dtype "bf16f8"): a row of K values is 4K
-                       bytes (2K bf16 units), [hi = bf16(x) | two OCP e4m3 parts of K bytes], the
-                       fp8 part [hi8 | lo8] for an A operand (activations) and [lo8 | hi8] for a
-                       weight, hi8 = e4m3(hi), lo8 = e4m3((x - hi) * 2^9) (vitmi_split_bf16f8).
+                       bytes (2K bf16 units), [hi = bf16(x) (K bf16) | OCP e4m3 part (2K bytes)],
+                       the e4m3 part in 64-k blocks of 128 B, [hi8 | lo8] for an A operand
+                       (activations) and [lo8 | hi8] for a weight, hi8 = e4m3(hi), lo8 =
+                       e4m3((x - hi) * 2^9) (vitmi_split_bf16f8; K % 64 == 0).
                        vitmi_linear_fwd dtype (x and w both so; K % 64 == 0, N % 16 == 0): the
                        GEMM runs K/64 bf16 K-steps (hi.hi) and K/64 block-scaled fp8 K-steps
                        (hi.lo + lo.hi, v_mfma_scale_f32_16x16x128_f8f6f4): 2K-equivalent MFMA
@@ -67,8 +68,8 @@ size_t vitmi_aux_tiled_bytes(int64_t rows, int64_t cols);
  * (hi = bf16(a), lo = bf16(a - hi): the split A operand of the next GEMM, vitmi_split_bf16x3
  * pattern 0); aux = gelu'(u) as for BIAS_GELU. */
 #define VITMI_EPI_SPLIT_X3 0x200
-/* OR'ed into BIAS_GELU of vitmi_linear_fwd with dtype VITMI_BF16F8 (y_dtype VITMI_BF16): y is
- * [M][2N] bf16 units, each row the VITMI_BF16F8 A-operand layout of gelu(u); aux as for BIAS_GELU. */
+/* OR'ed into BIAS_GELU of vitmi_linear_fwd with dtype VITMI_BF16F8 (y_dtype VITMI_BF16; N % 64 == 0):
+ * y is [M][2N] bf16 units, each row the VITMI_BF16F8 A-operand layout of gelu(u); aux as for BIAS_GELU. */
 #define VITMI_EPI_SPLIT_F8 0x400
 
 enum { VITMI_LOSS_CE = 0, VITMI_LOSS_MSE = 1 };
@@ -400,8 +401,9 @@ int vitmi_gather_rows(int64_t n, int64_t row_bytes, const void* src, int64_t n_s
  * VITMI_BF16X3), vitmi_attention_fwd_x3 and the fc1 epilogue (VITMI_EPI_SPLIT_X3). */
 int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
                        int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
-/* VITMI_BF16F8 rows: src fp32 [rows][ld_src] -> dst [rows][ld_dst >= 2K bf16 units], pattern 0 the
- * A-operand layout [hi | hi8 | lo8], pattern 1 the weight layout [hi | lo8 | hi8]; hi_copy as above. */
+/* VITMI_BF16F8 rows: src fp32 [rows][ld_src] (K % 64 == 0) -> dst [rows][ld_dst >= 2K bf16 units],
+ * pattern 0 the A-operand layout (e4m3 blocks [hi8 | lo8]), pattern 1 the weight layout ([lo8 | hi8]);
+ * hi_copy as above. */
 int vitmi_split_bf16f8(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
                        int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
 

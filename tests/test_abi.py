@@ -86,9 +86,13 @@ def test_bf16f8_knob_entry_points_validate_on_the_host():
     rc = lib.vitmi_gemm(4, 1, 1, 128, 128, 128, 16, 256, 16, 256, 16, 128, 0, 4, None, None, 0, None, 0,
                         None, 0, None)
     assert rc == 1 and b"BF16F8" in lib.vitmi_last_error()
-    # split_bf16f8: ld_dst >= 2K and the pattern
-    assert lib.vitmi_split_bf16f8(4, 8, 16, 8, 16, 12, 0, None, 0, None) == 1
-    assert lib.vitmi_split_bf16f8(4, 8, 16, 8, 16, 16, 2, None, 0, None) == 1
+    # split_bf16f8: K % 64, ld_dst >= 2K and the pattern
+    assert lib.vitmi_split_bf16f8(4, 8, 16, 8, 16, 16, 0, None, 0, None) == 1
+    assert lib.vitmi_split_bf16f8(4, 64, 16, 64, 16, 96, 0, None, 0, None) == 1
+    assert lib.vitmi_split_bf16f8(4, 64, 16, 64, 16, 128, 2, None, 0, None) == 1
+    # LayerNorm VITMI_BF16F8 output needs D % 64
+    rc = lib.vitmi_layernorm_fwd(4, 96, 16, 96, 16, 16, 1e-6, 16, 4, 192, 16, 16, None)
+    assert rc == 1 and b"64" in lib.vitmi_last_error()
     rc = lib.vitmi_attention_fwd_f8(1, 300, 2, 64, 0.125, 16, 16, 16, 16, None)
     assert rc == 1 and b"256" in lib.vitmi_last_error()
 

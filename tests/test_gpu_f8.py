@@ -32,16 +32,18 @@ def ref_parts(x):
 
 
 def parts(y8, K):
-    """(hi bf16 [rows, K], first e4m3 part, second e4m3 part) of VITMI_BF16F8 rows [rows, 2K]."""
-    b = y8.contiguous().cpu().view(torch.uint8)
-    return y8[:, :K].cpu(), b[:, 2 * K:3 * K], b[:, 3 * K:]
+    """(hi bf16 [rows, K], first e4m3 part, second e4m3 part) of VITMI_BF16F8 rows [rows, 2K]; the
+    e4m3 part is laid out in 64-k blocks [first | second] (common.h f8_off)."""
+    rows = y8.shape[0]
+    b = y8.contiguous().cpu().view(torch.uint8)[:, 2 * K:].reshape(rows, K // 64, 2, 64)
+    return y8[:, :K].cpu(), b[:, :, 0].reshape(rows, K), b[:, :, 1].reshape(rows, K)
 
 
 def deq(b):
     return b.view(E4).double()
 
 
-@pytest.mark.parametrize("rows,K", [(197 * 3, 768), (37, 3072), (5, 4)])
+@pytest.mark.parametrize("rows,K", [(197 * 3, 768), (37, 3072), (5, 64)])
 def test_split_bf16f8_bytes(rows, K):
     """vitmi_split_bf16f8: hi, hi8 and lo8 bit for bit the CPU conversions, in the A ([hi|hi8|lo8]) and
     weight ([hi|lo8|hi8]) layouts, from a row-strided source; values spread over 2^-12 .. 2^10 so

@@ -28,7 +28,14 @@ def main():
     gy = r(M, D)
     _, aux = ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU)
     dw = torch.zeros(F, D, device="cuda")
+    # the bf16f8 knob's operand rows (VITMI_BF16F8)
+    x8, _ = ops.split_bf16f8(x.float(), 0)
+    w18, _ = ops.split_bf16f8(w1.float(), 1)
     cases = {
+        "fc1+GELU f8": lambda: ops.linear_fwd(x8, w18, b1, BF, ops.EPI_BIAS_GELU, aux_tiled=True, split_f8=True,
+                                              f8=True),
+        "fc1 store f8": lambda: ops.linear_fwd(x8, w18, b1, BF, f8=True),
+        "fc1+GELU tiled": lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU, aux_tiled=True),
         "fc1+GELU": lambda: ops.linear_fwd(x, w1, b1, BF, ops.EPI_BIAS_GELU),
         "fc1 store": lambda: ops.linear_fwd(x, w1, b1, BF),
         "qkv store": lambda: ops.linear_fwd(x, wq, bq, BF),

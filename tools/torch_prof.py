@@ -1,5 +1,5 @@
 """torch.profiler view of the bench step (ViT-B/16, bs from argv): which host call sites
-launch the non-vitmi kernels (fills, copies).  usage: python tools/torch_prof.py [batch]"""
+launch the non-vitmi kernels (fills, copies).  usage: python tools/torch_prof.py [batch] [dtype]"""
 import os
 import sys
 
@@ -15,7 +15,7 @@ from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-    cfg = config_c3()
+    cfg = config_c3(dtype=sys.argv[2]) if len(sys.argv) > 2 else config_c3()
     model = VisionTransformer(cfg).cuda()
     model.reset_parameters(seed=0)
     opt = optim.Adam(model, learning_rate=1e-3)
@@ -36,7 +36,11 @@ def main():
             step()
         torch.cuda.synchronize()
     print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=25), flush=True)
-    print(prof.key_averages(group_by_stack_n=6).table(sort_by="count", row_limit=30), flush=True)
+    for ev in prof.key_averages(group_by_stack_n=8):
+        if any(t in ev.key for t in ("fill", "copy", "Fill", "Copy", "zero")):
+            print(f"== {ev.key}  count {ev.count}  cuda {ev.device_time_total:.0f} us")
+            for fr in ev.stack[:8]:
+                print("     ", fr)
 
 
 if __name__ == "__main__":

@@ -185,14 +185,12 @@ __device__ __forceinline__ void store_tile32(char* scr, const f32x16 (&acc)[2], 
   asm volatile("" ::: "memory");
 }
 
-// The e4m3 parts of the same tile (the VITMI_BF16F8 knob, common.h split_f8): hi8 = e4m3(bf16(v)),
-// lo8 = e4m3((v - bf16(v)) 2^9) of v = acc * mul, 64 bytes per row into rs8h / rs8l, through the
-// per-wave image as 32 rows x 64 B (16 B per lane, two stores per part)
+// The e4m3 block of the same tile (the VITMI_BF16F8 knob, common.h split_f8 / f8_off): the head's
+// 64 columns are one 64-k block, [hi8 | lo8] = 128 B per row, hi8 = e4m3(bf16(v)), lo8 =
+// e4m3((v - bf16(v)) 2^9) of v = acc * mul; the image goes out as whole lines like store_tile32's
 __device__ __forceinline__ void store_tile32_f8(char* scr, const f32x16 (&acc)[2], float mul,
-                                                __amdgpu_buffer_rsrc_t rs8h, __amdgpu_buffer_rsrc_t rs8l,
-                                                int64_t ld_bytes, int row0, int lane) {
+                                                __amdgpu_buffer_rsrc_t rs8, int64_t ld_bytes, int row0, int lane) {
   const int r = lane & 31, h = lane >> 5;
-  uint32_t lo8[2][4];
 #pragma unroll
   for (int c2 = 0; c2 < 2; ++c2)
 #pragma unroll
@@ -201,28 +199,20 @@ __device__ __forceinline__ void store_tile32_f8(char* scr, const f32x16 (&acc)[2
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[c2][4 * g4 + i] * mul;
       bf16x4 hi;
-      uint32_t hi8;
-      split_f8(v, hi, hi8, lo8[c2][g4]);
-      *(uint32_t*)(scr + r * ST_PITCH + 32 * c2 + 8 * g4 + 4 * h) = hi8;
+      uint32_t hi8, lo8;
+      split_f8(v, hi, hi8, lo8);
+      char* p = scr + r * ST_PITCH + 32 * c2 + 8 * g4 + 4 * h;
+      *(uint32_t*)p = hi8;
+      *(uint32_t*)(p + 64) = lo8;
     }
-  const int rr = lane >> 2, cc = lane & 3;
+  asm volatile("" ::: "memory");
+  const int rr = lane >> 3, cc = lane & 7;
 #pragma unroll
-  for (int part = 0; part < 2; ++part) {
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const u32x4 v = *(const u32x4*)(scr + (16 * j + rr) * ST_PITCH + cc * 16);
-      __builtin_amdgcn_raw_buffer_store_b128(v, part ? rs8l : rs8h,
-                                             (uint32_t)((int64_t)(row0 + 16 * j + rr) * ld_bytes + cc * 16), 0, 0);
-    }
-    asm volatile("" ::: "memory");
-    if (part == 0) {
-#pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) *(uint32_t*)(scr + r * ST_PITCH + 32 * c2 + 8 * g4 + 4 * h) = lo8[c2][g4];
-    }
+  for (int j = 0; j < 4; ++j) {
+    const u32x4 v = *(const u32x4*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs8, (uint32_t)((int64_t)(row0 + 8 * j + rr) * ld_bytes + cc * 16), 0, 0);
   }
+  asm volatile("" ::: "memory");
 }
 
 // Column sums of the rows < nvalid of the tile store_tile32 just wrote (its LDS image, as the
@@ -810,14 +800,15 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   const float inv = 1.f / lt;
   store_tile32(smem + wave * ST_BYTES, oacc, inv, ro, ldo, wave * 32, lane_here());
   if constexpr (XM == 2) {
-    // hi (bf16) at columns [0, D) of the 2D-wide row, hi8 / lo8 (e4m3 bytes) at bytes 2D / 3D
+    // hi (bf16) at columns [0, D) of the 2D-wide row, the head's e4m3 block [hi8 | lo8] at byte
+    // 2D + 128 hd
     const int64_t ld8 = 2 * ldo;
     const uint32_t by8 = (uint32_t)((int64_t)N * ld8);
     char* base8 = (char*)(o3 + (int64_t)b * N * 2 * D);
     store_tile32(smem + wave * ST_BYTES, oacc, inv, make_rsrc(base8 + hd * DH * 2, by8 - hd * DH * 2), ld8, wave * 32,
                  lane_here());
-    store_tile32_f8(smem + wave * ST_BYTES, oacc, inv, make_rsrc(base8 + 2 * D + hd * DH, by8 - (2 * D + hd * DH)),
-                    make_rsrc(base8 + 3 * D + hd * DH, by8 - (3 * D + hd * DH)), ld8, wave * 32, lane_here());
+    store_tile32_f8(smem + wave * ST_BYTES, oacc, inv, make_rsrc(base8 + 2 * D + hd * 128, by8 - (2 * D + hd * 128)),
+                    ld8, wave * 32, lane_here());
   }
   if constexpr (XM == 1) {
     // hi = bf16(O) twice, then lo = bf16(O - hi), O = oacc * inv exactly as store_tile32 forms it

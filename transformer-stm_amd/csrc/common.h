@@ -55,6 +55,11 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 // correction products hi.lo + lo.hi run as ONE block-scaled fp8 product (the GEMM's fp8 K-steps,
 // scale 2^-9 on the weight operand).  lo = x - hi is exact in fp32 (|lo| <= 2^-9 |x|), and the
 // fixed 2^9 keeps lo8 in e4m3's range wherever x is (tools/precision_emulate_fp8.py).
+// The e4m3 part (2K bytes after the K bf16 of hi) interleaves per 64 k: block j = [hi8 of k
+// 64j..64j+63 | lo8 of the same k] for an A operand, [lo8 | hi8] for a weight, so one 128-B GEMM
+// K-step pairs hi8.lo8 and lo8.hi8 of the same 64 k, and a producer's 64-column tile leaves as
+// whole 128-B lines (K % 64 == 0).
+__host__ __device__ constexpr int64_t f8_off(int64_t c) { return (c >> 6) * 128 + (c & 63); }
 constexpr float F8_LO_SCALE = 512.f;
 constexpr int F8_E8M0_ONE = 127, F8_E8M0_LO = 127 - 9;   // E8M0 scales 1 and 2^-9
 // four floats -> four OCP e4m3 bytes (RNE; saturated to +-448 first: the conversion itself would

@@ -916,12 +916,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         rc2 = make_rsrc(cbase + g.N * 2, clamp_bytes(((g.M - m0) * g.ldc - n0 - g.N) * 2));
         rc3 = make_rsrc(cbase + g.N * 4, clamp_bytes(((g.M - m0) * g.ldc - n0 - 2 * g.N) * 2));
       }
-      // EPI_GELU_F8: the e4m3 parts at bytes 2N + c (hi8) and 3N + c (lo8) of the 4N-byte row
-      if constexpr (EPI == EPI_GELU_F8) {
-        char* b8 = (char*)g.C + m0 * g.ldc * 2 + n0;
-        rc2 = make_rsrc(b8 + 2 * g.N, clamp_bytes((g.M - m0) * g.ldc * 2 - n0 - 2 * g.N));
-        rc3 = make_rsrc(b8 + 3 * g.N, clamp_bytes((g.M - m0) * g.ldc * 2 - n0 - 3 * g.N));
-      }
+      // EPI_GELU_F8: the e4m3 part from byte 2N of the 4N-byte row, 64-column blocks [hi8 | lo8]
+      // (common.h f8_off): a wave's 64 columns are one block, 128 B per row at 2 n0 + 128 wn --
+      // the same byte offsets as its bf16 hi, so `flush` writes it unchanged from its own base
+      if constexpr (EPI == EPI_GELU_F8)
+        rc2 = make_rsrc((char*)g.C + m0 * g.ldc * 2 + 2 * g.N + n0 * 2,
+                        clamp_bytes((g.M - m0) * g.ldc * 2 - 2 * g.N - n0 * 2));
       const int rstride = (int)(16 * g.ldc * CES);     // bytes between mi row groups
       const uint32_t vbase = (uint32_t)(((int64_t)(wm * 128 + lr) * g.ldc + wn * 64 + lc4) * CES);
       // Branch-free ragged N (straight-line epilogue code schedules far better): lanes past
@@ -989,17 +989,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       };
       [[maybe_unused]] bf16x4 lo3[4];   // EPI_GELU_X3: lo = bf16(a - hi) of the row group's fragments
       [[maybe_unused]] uint32_t f8h[4], f8l[4];   // EPI_GELU_F8: hi8, lo8 (4 e4m3 each) of the fragments
-      // EPI_GELU_F8: the image as 16 rows x 64 e4m3 bytes -> one 16-B store per lane
-      [[maybe_unused]] auto flush8 = [&](__amdgpu_buffer_rsrc_t r, int mi) {
-        lane_xchg();
-        const int r16 = lane >> 2, c4 = lane & 3;
-        const u32x4 d = *(const u32x4*)(scr + r16 * EPI_PITCH + c4 * 16);
-        const uint32_t vo = n0 + wn * 64 + c4 * 16 < g.N
-                                ? (uint32_t)((int64_t)(wm * 128 + r16) * g.ldc * 2 + wn * 64 + c4 * 16) : 0x80000000u;
-        asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen" VITMI_ST_C16 "\n\ts_nop 1"
-                     :: "v"(d), "v"(vo), "s"(r), "s"((int)(mi * 16 * g.ldc * 2)) : "memory");
-        lane_xchg();
-      };
       // one output fragment (row group mi, column group ni); `ld` = the epilogue's loaded operand.
       // Returns the fragment of the second output (gelu') for BIAS_GELU.
       auto emit = [&](int mi, int ni, f32x4 ldv, bf16x4 ldb) -> bf16x4 {
@@ -1066,13 +1055,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
             for (int ni = 0; ni < 4; ++ni) lds_put(ni, lo3[ni]);
             flush(rc3, g.ldc, mi);
           }
-          if constexpr (EPI == EPI_GELU_F8) {   // hi8 then lo8 through the same image
+          if constexpr (EPI == EPI_GELU_F8) {   // the [hi8 | lo8] block image, 128 B per row
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) *(uint32_t*)(scr + lr * EPI_PITCH + ni * 16 + lc4) = f8h[ni];
-            flush8(rc2, mi);
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) *(uint32_t*)(scr + lr * EPI_PITCH + ni * 16 + lc4) = f8l[ni];
-            flush8(rc3, mi);
+            for (int ni = 0; ni < 4; ++ni) {
+              *(uint32_t*)(scr + lr * EPI_PITCH + ni * 16 + lc4) = f8h[ni];
+              *(uint32_t*)(scr + lr * EPI_PITCH + 64 + ni * 16 + lc4) = f8l[ni];
+            }
+            flush(rc2, g.ldc, mi);
           }
           if constexpr (EB == VITMI_EPI_BIAS_GELU) {
             if (g.aux_tiled) {   // straight from the registers: 2 KiB-wide stores (aux_at)
@@ -1716,7 +1705,7 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   if (sf8) {
     VITMI_CHECK_ARG(f8 && epi == VITMI_EPI_BIAS_GELU && c_dtype == VITMI_BF16,
                     "gemm: SPLIT_F8 needs BIAS_GELU, VITMI_BF16F8 operands and a bf16 output");
-    VITMI_CHECK_ARG(ldc >= 2 * N, "gemm: SPLIT_F8 needs ldc >= 2N (bf16 units)");
+    VITMI_CHECK_ARG(ldc >= 2 * N && N % 64 == 0, "gemm: SPLIT_F8 needs N %% 64 == 0 and ldc >= 2N (bf16 units)");
     epi = EPI_GELU_F8;
   }
   if (x3) {

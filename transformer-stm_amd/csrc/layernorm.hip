@@ -102,9 +102,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
         uint32_t hi8, lo8;
         split_f8(o, hi, hi8, lo8);
         put((bf16x4*)(yr + c), hi);
-        uint8_t* f8 = (uint8_t*)(yr + D);
-        *(uint32_t*)(f8 + c) = hi8;
-        *(uint32_t*)(f8 + D + c) = lo8;
+        uint8_t* f8 = (uint8_t*)(yr + D) + f8_off(c);
+        *(uint32_t*)f8 = hi8;
+        *(uint32_t*)(f8 + 64) = lo8;
       } else {
         store4<TY>(y + row * ldy + c, o);
       }
@@ -376,6 +376,7 @@ extern "C" int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx
                   "layernorm_fwd: y dtype must be VITMI_F32, VITMI_BF16, VITMI_BF16X3 or VITMI_BF16F8");
   VITMI_CHECK_ARG(ldx >= D && ldy >= (y_dtype == VITMI_BF16X3 ? 3LL * D : y_dtype == VITMI_BF16F8 ? 2LL * D : (int64_t)D),
                   "layernorm_fwd: ldx >= D and ldy >= D (3D for VITMI_BF16X3, 2D for VITMI_BF16F8) required");
+  VITMI_CHECK_ARG(y_dtype != VITMI_BF16F8 || D % 64 == 0, "layernorm_fwd: VITMI_BF16F8 needs D %% 64 == 0");
   if (M == 0) return VITMI_OK;
   VITMI_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;

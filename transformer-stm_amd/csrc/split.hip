@@ -47,8 +47,9 @@ __global__ __launch_bounds__(256) void split3_kernel(int64_t rows, int64_t K, co
   }
 }
 
-// VITMI_BF16F8 rows (common.h split_f8): [hi (K bf16) | fp8 part (2K bytes)], the fp8 part
-// pattern 0 (A operand) [hi8 | lo8], pattern 1 (weights) [lo8 | hi8]; ld_dst in bf16 units
+// VITMI_BF16F8 rows (common.h split_f8, f8_off): [hi (K bf16) | e4m3 part (2K bytes)], the e4m3
+// part in 64-k blocks [hi8 | lo8] (pattern 0, A operand) or [lo8 | hi8] (pattern 1, weights);
+// ld_dst in bf16 units
 __global__ __launch_bounds__(256) void split_f8_kernel(int64_t rows, int64_t K, const float* __restrict__ src,
                                                        int64_t ld_src, bf16* __restrict__ dst, int64_t ld_dst,
                                                        int pattern, bf16* __restrict__ copy, int64_t ld_copy) {
@@ -60,9 +61,9 @@ __global__ __launch_bounds__(256) void split_f8_kernel(int64_t rows, int64_t K, 
     split_f8(*(const f32x4*)(src + r * ld_src + c), hi, hi8, lo8);
     bf16* d = dst + r * ld_dst;
     *(bf16x4*)(d + c) = hi;
-    uint8_t* f8 = (uint8_t*)(d + K);
-    *(uint32_t*)(f8 + c) = pattern == 0 ? hi8 : lo8;
-    *(uint32_t*)(f8 + K + c) = pattern == 0 ? lo8 : hi8;
+    uint8_t* f8 = (uint8_t*)(d + K) + f8_off(c);   // (common.h: 64-k blocks, [first | second])
+    *(uint32_t*)f8 = pattern == 0 ? hi8 : lo8;
+    *(uint32_t*)(f8 + 64) = pattern == 0 ? lo8 : hi8;
     if (copy) *(bf16x4*)(copy + r * ld_copy + c) = hi;
   }
 }
@@ -96,7 +97,7 @@ extern "C" int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int
 
 extern "C" int vitmi_split_bf16f8(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst,
                                   int64_t ld_dst, int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream) {
-  VITMI_CHECK_ARG(rows >= 0 && K > 0 && K % 4 == 0, "split_bf16f8: K must be a positive multiple of 4");
+  VITMI_CHECK_ARG(rows >= 0 && K > 0 && K % 64 == 0, "split_bf16f8: K must be a positive multiple of 64");
   VITMI_CHECK_ARG(pattern == 0 || pattern == 1, "split_bf16f8: pattern must be 0 (A: [hi|hi8|lo8]) or 1 (W: [hi|lo8|hi8])");
   VITMI_CHECK_ARG(ld_src >= K && ld_src % 4 == 0 && ld_dst >= 2 * K && ld_dst % 4 == 0,
                   "split_bf16f8: strides must be multiples of 4, ld_src >= K, ld_dst >= 2K (bf16 units)");
