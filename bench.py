@@ -334,10 +334,20 @@ def main():
     torch.manual_seed(0)
     model = VisionTransformer(cfg).to(dev)
     model.reset_parameters(seed=0)
-    comm = dp.VitmiComm.from_store(rank, world) if (world > 1 and args.comm == "vitmi") else None
-    red = dp.attach(model, bucket_mb=args.bucket_mb, comm=comm, grad_dtype=args.grad_dtype,
+    comm, group, comm_leg = None, None, args.comm
+    if world > 1 and args.comm == "vitmi":
+        # the library's own RCCL communicator, or (RCCL refused it on some rank) torch.distributed's
+        # RCCL process group: the line then says so instead of the multi-GPU run ending without one
+        comm, group, err = dp.comm_or_fallback(rank, world)
+        if comm is None:
+            comm_leg = "torch (fallback: vitmi comm init failed)"
+            print(f"[bench] rank {rank}: vitmi comm init failed ({err or 'on another rank'}); "
+                  f"gradients go through torch.distributed nccl (RCCL)", file=sys.stderr, flush=True)
+    if world > 1 and args.grad_dtype != "fp32" and comm is None:
+        raise SystemExit("bench: --grad-dtype bf16 needs the vitmi comm leg")
+    red = dp.attach(model, bucket_mb=args.bucket_mb, group=group, comm=comm, grad_dtype=args.grad_dtype,
                     reserve_cus=args.reserve_cus if world > 1 else 0, timeout_s=args.comm_timeout)
-    dp.broadcast_parameters(model, comm=comm)
+    dp.broadcast_parameters(model, group=group, comm=comm)
     if args.optimizer == "vitmi":
         opt = optim.Adam(model, learning_rate=1e-3)     # keras.optimizers.Adam(1e-3), models/CvT(Par).py:458
     else:
@@ -442,7 +452,7 @@ def main():
         "data": "synthetic (torch.rand images in [0,1), randint labels; random-init trunc_normal(.02) weights)",
         "config": {"workload": f"{ {'c2': 'ViT-S/16 224', 'c3': 'ViT-B/16 224', 'c5': 'ViT-L/16 384'}[args.config]}x"
                                f"{cfg.img_size}x3 fwd + CE loss + bwd"
-                               + (f" + {args.grad_dtype} grad all-reduce ({args.comm} RCCL, "
+                               + (f" + {args.grad_dtype} grad all-reduce ({comm_leg} RCCL, "
                                   f"{args.bucket_mb:g} MiB buckets)" if world > 1 else "")
                                + " + Adam step",
                    "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
@@ -469,7 +479,7 @@ def main():
         # parameters (MAX == MIN over ranks of the arena checksums)
         out["rccl"] = dp.comm_report(red)
         out["allreduce_exposed_ms"] = phases_ms.get("allreduce_wait")
-        out.update(dp.replica_report(arena.flat))
+        out.update(dp.replica_report(arena.flat, group))
     red.close()                               # the comm watchdog thread (the step loop is over)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps, model, dev)

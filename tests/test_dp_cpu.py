@@ -91,6 +91,46 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _fallback_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # no GPU here: the library's RCCL communicator cannot be created (rank 0 fails to make the
+        # id and says so through the store, so rank 1 fails instead of waiting); both ranks agree
+        # on the fallback group and the exchange runs there
+        comm, group, err = dp.comm_or_fallback(rank, world, make_group=lambda: dist.new_group(backend="gloo"))
+        flat = torch.full((1000,), float(rank + 1))
+        red = dp.GradReducer(flat, bucket_mb=1000 * 4 / (1 << 20) / 3, group=group)
+        red.start()
+        red.mark_ready(1000)
+        red.finish()
+        q.put((rank, {"comm": comm is None, "group": group is not None, "err": err is not None,
+                      "mean": float(flat.mean()), "report": dp.comm_report(red)["backend"]}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_comm_or_fallback_agrees_across_ranks():
+    """bench.py's multi-GPU exchange: when the library's RCCL communicator cannot be created, every
+    rank falls back to the same torch.distributed group (decided together) and the average still
+    comes out right; the report names the backend that ran."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fallback_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for r in range(world):
+        o = res[r]
+        assert o["comm"] and o["group"] and o["err"], o
+        assert o["mean"] == 1.5 and o["report"] == "torch.distributed gloo", o
+
+
 @pytest.mark.timeout(180)
 def test_grad_reducer_gloo_world2():
     world, port = 2, _free_port()

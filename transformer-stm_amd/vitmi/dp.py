@@ -134,10 +134,16 @@ def exchange_unique_id(rank: int, world: int, store=None, key: str = "vitmi_comm
         return VitmiComm.unique_id()
     store = store if store is not None else dist.distributed_c10d._get_default_store()
     if rank == 0:
-        uid = VitmiComm.unique_id()
+        try:
+            uid = VitmiComm.unique_id()
+        except Exception as e:
+            store.set(key, b"ERR:" + str(e).encode()[:200])   # (the other ranks fail too, not wait)
+            raise
         store.set(key, uid)
         return uid
     uid = bytes(store.get(key))
+    if uid.startswith(b"ERR:"):
+        raise RuntimeError(f"vitmi comm: rank 0 could not create the id ({uid[4:].decode(errors='replace')})")
     if len(uid) != UID_BYTES:
         raise RuntimeError(f"vitmi comm: id from the store has {len(uid)} bytes, not {UID_BYTES}")
     return uid
@@ -578,6 +584,27 @@ def comm_report(red: GradReducer) -> dict:
         out.update(backend=f"torch.distributed {red.backend}", ranks=red.world,
                    library=f"ProcessGroup {red.backend}" if red.backend else None)
     return out
+
+
+def comm_or_fallback(rank: int, world: int, make_group=None):
+    """The library's RCCL communicator for the job, or -- when creating it fails on ANY rank (the
+    ranks agree over the default, bootstrap process group) -- a torch.distributed process group
+    from ``make_group`` (default: a new ``nccl`` group, i.e. torch's RCCL) for the same exchange.
+    Returns (comm or None, group or None, this rank's error text or None)."""
+    err = None
+    comm = None
+    try:
+        comm = VitmiComm.from_store(rank, world)
+    except Exception as e:   # noqa: BLE001 -- any init failure of the comm leg
+        err = f"{type(e).__name__}: {e}"
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if ok.item() == 1:
+        return comm, None, None
+    if comm is not None:
+        comm.destroy()
+    group = make_group() if make_group is not None else dist.new_group(backend="nccl")
+    return None, group, err
 
 
 def broadcast_parameters(model, src: int = 0, group=None, comm: Optional[VitmiComm] = None) -> None:
