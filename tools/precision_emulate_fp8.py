@@ -57,6 +57,20 @@ def q8_fixed(x, scale):
     return (x / scale).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).float() * scale
 
 
+def q6(x, block=32):
+    """OCP MX FP6 e2m3 with one power-of-two scale per `block` consecutive k (amax -> [4, 8)),
+    round-to-nearest-even on the 3-bit mantissa, subnormals at 1/8, saturating at 7.5."""
+    K = x.shape[-1]
+    xb = x.reshape(*x.shape[:-1], K // block, block)
+    amax = xb.abs().amax(dim=-1, keepdim=True).clamp_min(2.0 ** -126)
+    s = torch.exp2(torch.floor(torch.log2(amax)) - 2)
+    v = (xb / s).clamp(-7.5, 7.5)
+    e = torch.floor(torch.log2(v.abs().clamp_min(1.0)))          # >= 0 (subnormals share e = 0)
+    step = torch.exp2(e - 3)
+    q = torch.round(v / step) * step                                 # (round-half-even)
+    return (q.clamp(-7.5, 7.5) * s).reshape(x.shape)
+
+
 def make_mm(mode, block):
     def mm(a, w):
         """a [..., K] @ w[N, K]^T as the GPU knob would form it."""
@@ -68,6 +82,10 @@ def make_mm(mode, block):
         la, lw = a - ha, w - hw
         if mode == "x3":
             return ha @ hw.t() + (ha @ lw.t() + la @ hw.t())
+        if mode == "f6":        # both correction operands in MX FP6 e2m3 (4x the bf16 MFMA rate)
+            return ha @ hw.t() + (q6(ha) @ q6(lw).t() + q6(la) @ q6(hw).t())
+        if mode == "f8f6":      # hi in e4m3 (fixed scale), lo in MX FP6
+            return ha @ hw.t() + (q8_fixed(ha, 1.0) @ q6(lw).t() + q6(la) @ q8_fixed(hw, 1.0).t())
         if mode == "f8fixed":   # no amax anywhere: hi at scale 1, lo = x - hi at scale 2^-9
             lo_s = 2.0 ** -9
             return ha @ hw.t() + (q8_fixed(ha, 1.0) @ q8_fixed(lw, lo_s).t() + q8_fixed(la, lo_s) @ q8_fixed(hw, 1.0).t())
@@ -120,7 +138,9 @@ def main():
                 ("hi.hi bf16 + e4m3 corrections, scale per 128 k", "f8", 128),
                 ("hi.hi bf16 + e4m3 corrections, one scale per row", "f8", 0),
                 ("hi.hi bf16 + e4m3 corrections, one scale per tensor", "f8", -1),
-                ("hi.hi bf16 + e4m3 corrections, fixed scales (hi 1, lo 2^-9)", "f8fixed", 0)]
+                ("hi.hi bf16 + e4m3 corrections, fixed scales (hi 1, lo 2^-9)", "f8fixed", 0),
+                ("hi.hi bf16 + MX FP6 (e2m3, per 32 k) corrections", "f6", 0),
+                ("hi.hi bf16 + e4m3 hi x MX FP6 lo corrections", "f8f6", 0)]
     with torch.no_grad():
         ref = vit_ref.forward(img, params, cfg)
         base = forward(img, params, cfg, make_mm("fp32", 0))
