@@ -406,6 +406,10 @@ int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int64_t ld_src
  * hi_copy as above. */
 int vitmi_split_bf16f8(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
                        int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
+/* Up to 8 dense weights (srcs[j] fp32 [rows[j]][K[j]]) to pattern-1 VITMI_BF16F8 rows (dsts[j]
+ * [rows[j]][2 K[j]] bf16 units) in one launch (the knob's per-forward weight split). */
+int vitmi_split_bf16f8_weights(int n, const float* const* srcs, void* const* dsts, const int64_t* rows,
+                               const int64_t* K, vitmi_stream_t stream);
 
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);

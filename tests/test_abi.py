@@ -93,6 +93,11 @@ def test_bf16f8_knob_entry_points_validate_on_the_host():
     # LayerNorm VITMI_BF16F8 output needs D % 64
     rc = lib.vitmi_layernorm_fwd(4, 96, 16, 96, 16, 16, 1e-6, 16, 4, 192, 16, 16, None)
     assert rc == 1 and b"64" in lib.vitmi_last_error()
+    import ctypes
+    one = (ctypes.c_int64 * 1)(96)
+    ptr = (ctypes.c_void_p * 1)(16)
+    assert lib.vitmi_split_bf16f8_weights(0, ptr, ptr, one, one, None) == 1            # n in 1..8
+    assert lib.vitmi_split_bf16f8_weights(1, ptr, ptr, one, one, None) == 1            # K % 64
     rc = lib.vitmi_attention_fwd_f8(1, 300, 2, 64, 0.125, 16, 16, 16, 16, None)
     assert rc == 1 and b"256" in lib.vitmi_last_error()
 

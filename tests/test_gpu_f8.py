@@ -169,3 +169,14 @@ def test_attention_fwd_f8_output(B, N, H):
     lo8 = deq(p2) / 512.0
     # (lo8 / 2^9 resolves 2^-18 at the bottom of e4m3's subnormal range)
     assert ((lo8 - lo3).abs() <= lo3.abs() * 2.0 ** -3 + o.double().cpu().abs() * 2.0 ** -16 + 2.0 ** -18).all()
+
+
+def test_split_bf16f8_weights_batch_matches_single():
+    """vitmi_split_bf16f8_weights (one launch for a block's four weights) writes what
+    split_bf16f8(w, 1) writes for each, bit for bit."""
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
+    ws = [(rnd(*s, seed=60 + i) * 0.05).to(DEV) for i, s in enumerate(shapes)]
+    outs = ops.split_bf16f8_weights(ws)
+    for w, o in zip(ws, outs):
+        ref, _ = ops.split_bf16f8(w, 1)
+        assert o.shape == ref.shape and torch.equal(o, ref)

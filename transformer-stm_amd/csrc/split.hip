@@ -68,6 +68,33 @@ __global__ __launch_bounds__(256) void split_f8_kernel(int64_t rows, int64_t K, 
   }
 }
 
+// Several dense weights ([rows][K] fp32 -> [rows][2K] pattern-1 rows) in one launch: the
+// bf16f8 knob splits a block's four GEMM weights per forward (one launch instead of four)
+struct SplitBatch {
+  const float* src[8];
+  bf16* dst[8];
+  int64_t K[8];
+  int64_t start[9];   // prefix sums of rows * K / 4 (thread items)
+  int n;
+};
+__global__ __launch_bounds__(256) void split_f8_batch_kernel(SplitBatch b) {
+  const int64_t total = b.start[b.n];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int j = 0;
+    while (j + 1 < b.n && i >= b.start[j + 1]) ++j;
+    const int64_t K = b.K[j], K4 = K / 4, li = i - b.start[j];
+    const int64_t r = li / K4, c = (li - r * K4) * 4;
+    bf16x4 hi;
+    uint32_t hi8, lo8;
+    split_f8(*(const f32x4*)(b.src[j] + r * K + c), hi, hi8, lo8);
+    bf16* d = b.dst[j] + r * 2 * K;
+    *(bf16x4*)(d + c) = hi;
+    uint8_t* f8 = (uint8_t*)(d + K) + f8_off(c);
+    *(uint32_t*)f8 = lo8;
+    *(uint32_t*)(f8 + 64) = hi8;
+  }
+}
+
 static unsigned grid_of(int64_t items) {
   int64_t b = (items + 255) / 256;
   return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -92,6 +119,26 @@ extern "C" int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int
                      ld_src, (bf16*)dst, ld_dst, pattern, (bf16*)hi_copy, ld_copy);
   VITMI_LAUNCH_CHECK("split_bf16x3");
   VITMI_STAT(split3_kernel, 0, (double)rows * K * (4 + 6 + (hi_copy ? 2 : 0)));
+  return VITMI_OK;
+}
+
+extern "C" int vitmi_split_bf16f8_weights(int n, const float* const* srcs, void* const* dsts, const int64_t* rows,
+                                          const int64_t* K, vitmi_stream_t stream) {
+  VITMI_CHECK_ARG(n >= 1 && n <= 8 && srcs && dsts && rows && K, "split_bf16f8_weights: 1..8 weights");
+  SplitBatch b{};
+  b.n = n;
+  for (int j = 0; j < n; ++j) {
+    VITMI_CHECK_ARG(rows[j] > 0 && K[j] > 0 && K[j] % 64 == 0, "split_bf16f8_weights: weight %d: K %% 64 and rows", j);
+    VITMI_CHECK_ARG(srcs[j] && dsts[j] && ((uintptr_t)srcs[j] % 16) == 0 && ((uintptr_t)dsts[j] % 16) == 0,
+                    "split_bf16f8_weights: weight %d: null or unaligned pointer", j);
+    b.src[j] = srcs[j];
+    b.dst[j] = (bf16*)dsts[j];
+    b.K[j] = K[j];
+    b.start[j + 1] = b.start[j] + rows[j] * K[j] / 4;
+  }
+  hipLaunchKernelGGL(split_f8_batch_kernel, dim3(grid_of(b.start[n])), dim3(256), 0, (hipStream_t)stream, b);
+  VITMI_LAUNCH_CHECK("split_bf16f8_weights");
+  VITMI_STAT(split_f8_batch_kernel, 0, (double)b.start[n] * 4 * 8);
   return VITMI_OK;
 }
 

@@ -400,8 +400,12 @@ class _BlockFn(torch.autograd.Function):
         split = ops.split_bf16f8 if f8 else ops.split_bf16x3
         ln_out = ops.BF16F8 if f8 else ops.BF16X3
 
+        weights = (a_.qkv.weight, a_.proj.weight, mlp.fc1.weight, mlp.fc2.weight)
+        if f8:   # the block's four weights split in one launch
+            split_w = dict(zip(map(id, weights), ops.split_bf16f8_weights(weights)))
+
         def w3(p):
-            return split(p.detach(), 1)[0]
+            return split_w[id(p)] if f8 else split(p.detach(), 1)[0]
         h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, ln_out)
         if N <= ops.ATTN_SEQ_MAX:   # q, k, v leave the GEMM epilogue in bf16
             qkv = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, torch.bfloat16, f8=f8)

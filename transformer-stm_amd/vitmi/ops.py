@@ -532,6 +532,22 @@ def split_bf16x3(x: Tensor, pattern: int, hi_copy: bool = False):
     return x3, hi
 
 
+def split_bf16f8_weights(ws):
+    """Dense fp32 weights [N_j, K_j] (up to 8) -> their pattern-1 VITMI_BF16F8 rows [N_j, 2 K_j], one
+    launch (vitmi_split_bf16f8_weights)."""
+    import ctypes
+    ws = [w.detach() for w in ws]
+    n = len(ws)
+    assert 1 <= n <= 8 and all(w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2 for w in ws)
+    outs = [torch.empty(w.shape[0], 2 * w.shape[1], dtype=torch.bfloat16, device=w.device) for w in ws]
+    srcs = (ctypes.c_void_p * n)(*[_p(w) for w in ws])
+    dsts = (ctypes.c_void_p * n)(*[_p(o) for o in outs])
+    rows = (ctypes.c_int64 * n)(*[w.shape[0] for w in ws])
+    ks = (ctypes.c_int64 * n)(*[w.shape[1] for w in ws])
+    check(lib().vitmi_split_bf16f8_weights(n, srcs, dsts, rows, ks, _s()), "split_bf16f8_weights")
+    return outs
+
+
 def split_bf16f8(x: Tensor, pattern: int, hi_copy: bool = False):
     """x fp32 [rows, K] (rows may be strided) -> (x8 [rows, 2K] bf16 units, the VITMI_BF16F8 rows
     [hi | hi8 | lo8] (pattern 0, a GEMM's A operand) or [hi | lo8 | hi8] (pattern 1, its weight),
