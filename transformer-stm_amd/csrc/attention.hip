@@ -679,6 +679,25 @@ __device__ __forceinline__ float asm_load4(__amdgpu_buffer_rsrc_t rs, uint32_t v
   return v;
 }
 
+#ifdef VITMI_ATTN_STAMPS
+// DIAGNOSTIC build only: [kernel 0 fwd / 1 dQ][pair][8] = s_memrealtime at start, operands
+// landed, loop done, end; then HW_ID and XCC_ID (tools/attn_stamps.py)
+__device__ unsigned long long* d_attn_stamps;
+#define ATTN_STAMP(kern, k)                                                                          \
+  do {                                                                                               \
+    if (d_attn_stamps && threadIdx.x == 0) {                                                         \
+      unsigned long long* p_ = d_attn_stamps + ((int64_t)(kern) * 65536 + blockIdx.x) * 8;           \
+      p_[k] = __builtin_amdgcn_s_memrealtime();                                                      \
+      if ((k) == 0) {                                                                                \
+        p_[4] = __builtin_amdgcn_s_getreg(4 | (31 << 11));                                           \
+        p_[5] = __builtin_amdgcn_s_getreg(20 | (15 << 11));                                          \
+      }                                                                                              \
+    }                                                                                                \
+  } while (0)
+#else
+#define ATTN_STAMP(kern, k) do {} while (0)
+#endif
+
 // stage_seq with the pieces issued by dma_piece (no compiler-visible LDS-DMA; see there)
 __device__ __forceinline__ void stage_seq_dma(char* lds, __amdgpu_buffer_rsrc_t rs, int64_t ld_bytes, int np,
                                               int nw, int wave, int lane) {
@@ -714,6 +733,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
   __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
   __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  ATTN_STAMP(0, 0);
   char* kt = smem;
   char* vt = smem + NP * 128;
   stage_seq(kt, rk, ldb, NP, nw, wave, lane);
@@ -724,6 +744,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   for (int s = 0; s < 4; ++s) qf[s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ATTN_STAMP(0, 1);
 
   const float c2 = scale * LOG2E;
   float m = -INFINITY, l = 0.f;
@@ -795,10 +816,12 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   if (q < N && h == 0) lse[(int64_t)bh * N + q] = (m + log2f(lt)) * LN2;
   // O through the (now free) K/V image: every wave must be done reading it
   __syncthreads();
+  ATTN_STAMP(0, 2);
   const int64_t ldo = (int64_t)D * 2;
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
   const float inv = 1.f / lt;
   store_tile32(smem + wave * ST_BYTES, oacc, inv, ro, ldo, wave * 32, lane_here());
+  ATTN_STAMP(0, 3);
   if constexpr (XM == 2) {
     // hi (bf16) at columns [0, D) of the 2D-wide row, the head's e4m3 block [hi8 | lo8] at byte
     // 2D + 128 hd
@@ -862,6 +885,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
   __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
   __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  ATTN_STAMP(1, 0);
   char* kt = smem;
   char* vt = smem + NP * 128;
   stage_seq(kt, rk, ldb, NP, nw, wave, lane);
@@ -893,6 +917,7 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   const float L2 = qok ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;   // q >= N -> p = 0
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ATTN_STAMP(1, 1);
 
   const float c2 = scale * LOG2E;
   f32x16 dqt[2] = {zero16(), zero16()};
@@ -933,9 +958,11 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   // dQ through the (now free) K/V image: every wave must be done reading it.  With colsum,
   // also this head's q-bias gradient partial colsum[b][hd*64 ..] (column sums of the stored dQ)
   __syncthreads();
+  ATTN_STAMP(1, 2);
   const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv + (int64_t)b * N * ld + hd * DH, bytes - hd * DH * 2);
   const int ln = lane_here();
   store_tile32(smem + wave * ST_BYTES, dqt, scale, rdq, ldb, wave * 32, ln);
+  ATTN_STAMP(1, 3);
   if (colsum) {
     __shared__ float red[NPMAX / 32][64];
     tile32_colsum(smem + wave * ST_BYTES, wave * 32, N, colsum + (int64_t)b * 3 * D + hd * DH, red, wave, nw, ln);
@@ -1661,6 +1688,13 @@ extern "C" int vitmi_attention_fwd_f8(int B, int N, int H, int dh, float scale, 
   VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, 2>), 4.0 * bh * N * N * DH, bh * N * DH * 2 * (3 + 1 + 2) + bh * N * 4);
   return VITMI_OK;
 }
+
+#ifdef VITMI_ATTN_STAMPS
+extern "C" int vitmi_attn_set_stamps(void* buf) {
+  VITMI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(d_attn_stamps), &buf, sizeof(buf)), "attn stamps");
+  return 0;
+}
+#endif
 
 extern "C" size_t vitmi_attention_bwd_workspace_size(int B, int N, int H) {
   return (size_t)B * H * N * sizeof(float);
