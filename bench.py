@@ -277,6 +277,9 @@ def main():
                          "GEMM operands, bf16f8 = the same with the correction products in block-scaled e4m3, "
                          "fp32 = exact-fp32 MFMA everywhere; all keep the logits within 1e-3 of the CPU oracle "
                          "at ViT-B depth 12)")
+    ap.add_argument("--split-qkv", choices=["auto", "yes", "no"], default="auto",
+                    help="the precision knobs' qkv GEMM on split operands or plain bf16 (auto: split for "
+                         "bf16x3, plain for bf16f8; ViTConfig.split_qkv)")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default 256 for c3, 64 for c5, "
                                                              "128 for c2)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
@@ -322,6 +325,8 @@ def main():
     cfg = {"c2": config_c2, "c3": config_c3, "c5": config_c5}[args.config]()
     if args.dtype is not None:
         cfg = cfg.replace(dtype=args.dtype)
+    if args.split_qkv != "auto":
+        cfg = cfg.replace(split_qkv=args.split_qkv == "yes")
     B = args.batch or {"c2": 128, "c3": 256, "c5": 64}[args.config]
     model_name = {"c2": "vit_small_16", "c3": "vit_base_16", "c5": "vit_large_16"}[args.config]
     metric = {"c3": METRIC,
@@ -457,7 +462,10 @@ def main():
                                + " + Adam step",
                    "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
                    "model": model_name, "global_batch": B * world, "seq_len": cfg.seq_len,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   **({"knob_qkv": "split" if (cfg.split_qkv if cfg.split_qkv is not None
+                                               else cfg.dtype == "bf16x3") else "bf16"}
+                      if cfg.dtype in ("bf16x3", "bf16f8") else {})},
         "roofline": {"bound": "mfma", "kernel": f"gemm fc1 fwd {'fp32' if fp32 else 'bf16'} [{M}x{F_}x{KW}] +bias+GELU"
                                + (" (bf16x3 split operands)" if KD != D else "")
                                + (" (bf16f8: bf16 hi.hi + e4m3 corrections, bf16-equivalent K)" if KW != KD else ""),

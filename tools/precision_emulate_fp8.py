@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "transformer-stm_amd"))
 
 from oracle import vit_ref  # noqa: E402
-from vitmi.config import preset  # noqa: E402
+from vitmi.config import config_c1, preset  # noqa: E402
 
 E4M3_MAX = 448.0
 
@@ -94,13 +94,16 @@ def make_mm(mode, block):
     return mm
 
 
-def forward(img, p, cfg, mm):
+def forward(img, p, cfg, mm, per=None):
+    """per: optional {GEMM class: mm} overriding `mm` for "patch", "qkv", "proj", "fc1", "fc2"."""
+    per = per or {}
+    g = lambda c: per.get(c, mm)  # noqa: E731
     B = img.shape[0]
     D, H = cfg.embed_dim, cfg.num_heads
     dh = D // H
     Pz = cfg.patch_size
     patches = F.unfold(img, Pz, stride=Pz).transpose(1, 2)
-    x = mm(patches, p["patch_embed.proj.weight"].reshape(D, -1)) + p["patch_embed.proj.bias"]
+    x = g("patch")(patches, p["patch_embed.proj.weight"].reshape(D, -1)) + p["patch_embed.proj.bias"]
     x = torch.cat([p["cls_token"].expand(B, 1, D), x], dim=1)
     if cfg.pos_embed:
         x = x + p["pos_embed"]
@@ -109,14 +112,14 @@ def forward(img, p, cfg, mm):
     for i in range(cfg.depth):
         pre = f"blocks.{i}."
         h = vit_ref.layer_norm(x, p[pre + "norm1.weight"], p[pre + "norm1.bias"], cfg.ln_eps)
-        qkv = rb(mm(h, p[pre + "attn.qkv.weight"]) + p[pre + "attn.qkv.bias"])        # q, k, v bf16
+        qkv = rb(g("qkv")(h, p[pre + "attn.qkv.weight"]) + p[pre + "attn.qkv.bias"])        # q, k, v bf16
         q, k, v = (t.reshape(B, N, H, dh).transpose(1, 2) for t in qkv.split(D, dim=-1))
         a = rb(torch.softmax((q @ k.transpose(-1, -2)) * scale, dim=-1))              # P bf16
         o = (a @ v).transpose(1, 2).reshape(B, N, D)
-        x = x + mm(o, p[pre + "attn.proj.weight"]) + p[pre + "attn.proj.bias"]
+        x = x + g("proj")(o, p[pre + "attn.proj.weight"]) + p[pre + "attn.proj.bias"]
         h2 = vit_ref.layer_norm(x, p[pre + "norm2.weight"], p[pre + "norm2.bias"], cfg.ln_eps)
-        act = F.gelu(mm(h2, p[pre + "mlp.fc1.weight"]) + p[pre + "mlp.fc1.bias"])
-        x = x + mm(act, p[pre + "mlp.fc2.weight"]) + p[pre + "mlp.fc2.bias"]
+        act = F.gelu(g("fc1")(h2, p[pre + "mlp.fc1.weight"]) + p[pre + "mlp.fc1.bias"])
+        x = x + g("fc2")(act, p[pre + "mlp.fc2.weight"]) + p[pre + "mlp.fc2.bias"]
     c = vit_ref.layer_norm(x[:, 0], p["norm.weight"], p["norm.bias"], cfg.ln_eps)
     return c @ p["head.weight"].t() + p["head.bias"]
 
@@ -126,12 +129,21 @@ def main():
     ap.add_argument("--depth", type=int, default=12)
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--init", choices=["random", "default"], default="random")
+    ap.add_argument("--c1", action="store_true", help="C1 (ViT-Ti/16 64 px, seed 3, 5 images; --img for 48)")
+    ap.add_argument("--img", type=int, default=64)
+    ap.add_argument("--classes", action="store_true",
+                    help="fixed-scale e4m3 corrections with one GEMM class at a time in plain bf16")
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
-    cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype="fp32", depth=args.depth)
-    params = vit_ref.init_params(cfg, seed=0, randomize_all=args.init == "random")
-    img, _ = vit_ref.synthetic_batch(cfg, args.batch)
+    if args.c1:
+        cfg = config_c1(dtype="fp32", img_size=args.img)
+        params = vit_ref.init_params(cfg, seed=3)
+        img, _ = vit_ref.synthetic_batch(cfg, 5)
+    else:
+        cfg = preset("vit_base_16", img_size=224, num_classes=2, dtype="fp32", depth=args.depth)
+        params = vit_ref.init_params(cfg, seed=0, randomize_all=args.init == "random")
+        img, _ = vit_ref.synthetic_batch(cfg, args.batch)
     settings = [("bf16 operands (q/k/v, P bf16)", "bf16", 0),
                 ("bf16x3 knob as built", "x3", 0),
                 ("hi.hi bf16 + e4m3 corrections, scale per 32 k (MX)", "f8", 32),
@@ -144,8 +156,16 @@ def main():
     with torch.no_grad():
         ref = vit_ref.forward(img, params, cfg)
         base = forward(img, params, cfg, make_mm("fp32", 0))
-        print(f"ViT-B/16 224px depth {args.depth} bs {args.batch}, {args.init} init; "
+        print(f"{'C1 ' + str(args.img) + 'px' if args.c1 else f'ViT-B/16 224px depth {args.depth} bs {args.batch}, {args.init} init'}; "
               f"emulator (q/k/v, P bf16; GEMMs fp32) vs oracle: {(base - ref).abs().max().item():.2e}")
+        if args.classes:
+            f8, b16 = make_mm("f8fixed", 0), make_mm("bf16", 0)
+            print(f"{'GEMM class in plain bf16 (rest bf16f8)':<56} logits max-abs vs fp32")
+            for cls in ("none", "patch", "qkv", "proj", "fc1", "fc2", "proj+fc2", "qkv+proj"):
+                per = {c: b16 for c in cls.split("+") if c != "none"}
+                err = (forward(img, params, cfg, f8, per) - ref).abs().max().item()
+                print(f"{cls:<56} {err:.2e}", flush=True)
+            return
         print(f"{'GEMM operands':<56} logits max-abs vs fp32")
         for name, mode, block in settings:
             err = (forward(img, params, cfg, make_mm(mode, block)) - ref).abs().max().item()

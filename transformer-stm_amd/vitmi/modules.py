@@ -321,6 +321,12 @@ class Block(nn.Module):
             self.norm2 = LayerNorm(dim, eps)
         self.mlp = Mlp(dim, int(dim * mlp_ratio), dtype)
         self.dtype = dtype
+        # the precision knobs' qkv GEMM: split operands (True) or plain bf16 (False).  q, k and v
+        # are rounded to bf16 right after it, so its corrections buy little: depth-12 logits
+        # 1.8e-4 -> 6.4e-4 (random init) / 2.3e-4 -> 7.5e-4 (default init) for 'bf16f8' in
+        # emulation (tools/precision_emulate_fp8.py --classes).  Default: split for 'bf16x3', plain
+        # for 'bf16f8' (ViTConfig.split_qkv overrides)
+        self.split_qkv = dtype == "bf16x3"
         self.eps = eps
         self.drop_rate = 0.0     # set by VisionTransformer / the caller (Keras default 0.1)
         self.drop_seed: Optional[int] = None   # fixed seed (tests); None = drawn per forward
@@ -391,8 +397,12 @@ class _BlockFn(torch.autograd.Function):
 
         dtype 'bf16f8' (tools/precision_emulate_fp8.py): the same operands as VITMI_BF16F8 rows,
         [hi | e4m3 hi8, lo8 * 2^9]: hi.hi in bf16 and both corrections as one block-scaled fp8
-        product, 2K-equivalent MFMA work instead of 3K (emulated 1.8-2.3e-4 at depth 12)."""
+        product, 2K-equivalent MFMA work instead of 3K (emulated 1.8-2.3e-4 at depth 12).
+
+        blk.split_qkv False: the qkv GEMM runs on plain bf16 operands (LN1 writes bf16, the
+        weight's bf16 shadow); the other three GEMMs as above."""
         f8 = blk.dtype == "bf16f8"
+        sq = blk.split_qkv
         if drop is not None:
             raise ValueError(f"vitmi: dtype '{blk.dtype}' is the parity / evaluation knob; dropout is not supported")
         n1, n2 = blk.norm1, blk._norm2
@@ -400,18 +410,20 @@ class _BlockFn(torch.autograd.Function):
         split = ops.split_bf16f8 if f8 else ops.split_bf16x3
         ln_out = ops.BF16F8 if f8 else ops.BF16X3
 
-        weights = (a_.qkv.weight, a_.proj.weight, mlp.fc1.weight, mlp.fc2.weight)
-        if f8:   # the block's four weights split in one launch
+        weights = ((a_.qkv.weight,) if sq else ()) + (a_.proj.weight, mlp.fc1.weight, mlp.fc2.weight)
+        if f8:   # the block's split weights in one launch
             split_w = dict(zip(map(id, weights), ops.split_bf16f8_weights(weights)))
 
         def w3(p):
             return split_w[id(p)] if f8 else split(p.detach(), 1)[0]
-        h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, ln_out)
+        h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, ln_out if sq else torch.bfloat16)
+        # the qkv GEMM's operands: split, or plain bf16 (h1 and the weight's bf16 shadow)
+        qa, qw, qf8 = (h1_3, w3(a_.qkv.weight), f8) if sq else (h1_3, wlp[0], False)
         if N <= ops.ATTN_SEQ_MAX:   # q, k, v leave the GEMM epilogue in bf16
-            qkv = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, torch.bfloat16, f8=f8)
+            qkv = ops.linear_fwd(qa, qw, a_.qkv.bias, torch.bfloat16, f8=qf8)
             o, o3, lse = (ops.attention_fwd_f8 if f8 else ops.attention_fwd_x3)(qkv, B, N, H, a_.scale)
         else:   # streamed kernels (N > 256): O from the fp32 kernel, o / lse from the bf16 one
-            qkvf = ops.linear_fwd(h1_3, w3(a_.qkv.weight), a_.qkv.bias, F32, f8=f8)
+            qkvf = ops.linear_fwd(qa, qw, a_.qkv.bias, F32, f8=qf8)
             qkv = ops.cast_bf16(qkvf)
             of, _ = ops.attention_fwd(qkvf, B, N, H, a_.scale)
             del qkvf
@@ -427,7 +439,7 @@ class _BlockFn(torch.autograd.Function):
                                   aux_tiled=True, split_x3=not f8, split_f8=f8, f8=f8)
         out = ops.linear_fwd(act3, w3(mlp.fc2.weight), mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, f8=f8)
         # the bf16 backward's operands: hi parts of the split activations (row-strided views)
-        h1, h2, act = h1_3[:, :D], h2_3[:, :D], act3[:, :mlp.fc1.weight.shape[0]]
+        h1, h2, act = (h1_3[:, :D] if sq else h1_3), h2_3[:, :D], act3[:, :mlp.fc1.weight.shape[0]]
         ctx.aux_tiled = True
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dg, act, *wlp)
         return out
@@ -793,6 +805,9 @@ class VisionTransformer(nn.Module):
         self.blocks = nn.ModuleList([
             Block(D, cfg.num_heads, cfg.mlp_ratio, cfg.qkv_bias, cfg.ln_eps, cfg.attn_scale, cfg.tie_norms,
                   cfg.dtype) for _ in range(cfg.depth)])
+        if cfg.split_qkv is not None:
+            for blk in self.blocks:
+                blk.split_qkv = cfg.split_qkv
         self.norm = LayerNorm(D, cfg.ln_eps)
         self.head = Linear(D, cfg.num_classes)
         self._arena: Optional[ParamArena] = None
