@@ -367,6 +367,17 @@ def test_vit_b_precision_knob_bf16f8_meets_1e3(split_qkv):
     assert err <= (5e-4 if split_qkv else 1e-3)
 
 
+@pytest.mark.parametrize("knob,split_qkv", [("bf16x3", False), ("bf16f8", True)])
+def test_knob_split_qkv_override_small_model(knob, split_qkv):
+    """ViTConfig.split_qkv against each knob's default (bf16x3 with the qkv GEMM plain bf16, bf16f8
+    with it split), C1 shape: logits within 1e-3 of the fp32 oracle, gradients at the bf16 bound."""
+    cfg = config_c1(dtype=knob, split_qkv=split_qkv)
+    params = vit_ref.init_params(cfg, seed=3)
+    img, tgt = vit_ref.synthetic_batch(cfg, 5)
+    err, worst = compare(cfg, params, img, tgt, logit_tol=1e-3, grad_tol=2e-2, loss_tol=1e-3)
+    print(f"C1 {knob} split_qkv={split_qkv}: logits {err:.3e}, worst grad {worst[1]} {worst[0]:.3e}")
+
+
 @pytest.mark.parametrize("knob", ["bf16x3", "bf16f8"])
 def test_bf16x3_knob_streamed_attention_n290(knob):
     """bf16 and bf16x3 at N > 256 (ViT-Ti/16 at 272 px, N = 290, depth 4: the streamed attention
