@@ -1,5 +1,6 @@
 """torch.profiler view of the bench step (ViT-B/16, bs from argv): which host call sites
-launch the non-vitmi kernels (fills, copies).  usage: python tools/torch_prof.py [batch] [dtype]"""
+launch the non-vitmi kernels (fills, copies).  usage: python tools/torch_prof.py [batch] [dtype] [dp]
+("dp": the step as bench.py runs it, with vitmi.dp.attach's reducer and readiness hooks at N = 1)"""
 import os
 import sys
 
@@ -8,7 +9,7 @@ sys.path.insert(0, os.path.join(ROOT, "transformer-stm_amd"))
 import torch  # noqa: E402
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
-from vitmi import optim  # noqa: E402
+from vitmi import dp, optim  # noqa: E402
 from vitmi.config import config_c3  # noqa: E402
 from vitmi.modules import VisionTransformer, cross_entropy  # noqa: E402
 
@@ -19,13 +20,22 @@ def main():
     model = VisionTransformer(cfg).cuda()
     model.reset_parameters(seed=0)
     opt = optim.Adam(model, learning_rate=1e-3)
+    red = dp.attach(model) if len(sys.argv) > 3 and sys.argv[3] == "dp" else None
+    params = list(model.arena().params)
     img = torch.rand(B, 3, 224, 224, device="cuda")
     tgt = torch.randint(0, cfg.num_classes, (B,), device="cuda")
 
     def step():
-        opt.zero_grad()
+        if red is None:
+            opt.zero_grad()
+        else:                     # as bench.py's step
+            for p in params:
+                p.grad = None
+            red.start()
         loss = cross_entropy(model(img), tgt)
         loss.backward()
+        if red is not None:
+            red.finish()
         opt.step()
 
     for _ in range(3):
