@@ -853,6 +853,147 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
   }
 }
 
+#ifndef VITMI_ATTN_Q64
+#define VITMI_ATTN_Q64 1
+#endif
+// The bf16 forward (vitmi_attention_fwd, N <= 256) with 4 waves of 64 queries (two 32-query
+// blocks per wave): every K and V fragment read from LDS feeds both blocks' MFMAs, and each wave
+// carries two independent softmax chains.  Per query block the arithmetic is attn_fwd_seq_bf16's,
+// in the same order (bitwise equal outputs); 213 VGPRs, two workgroups per CU.  C3: 79.4-80.6 µs
+// against 82.7-83.6 for the 7 x 32-query form (profiles/r05_q64/).  grid B*H, block 256.
+template <int NPMAX>
+__global__ __launch_bounds__(256, 2) void attn_fwd_seq64_bf16(const bf16* __restrict__ qkv, bf16* __restrict__ o,
+                                                          float* __restrict__ lse, int N, int H, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NP = (N + 31) & ~31;
+  const int bh = gridDim.x - 1 - blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  char* kt = smem;
+  char* vt = smem + NP * 128;
+  stage_seq(kt, rk, ldb, NP, 4, wave, lane);
+  stage_seq(vt, rv, ldb, NP, 4, wave, lane);
+  const int q0 = wave * 64;
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[qb][s] = load_row16(rq, (uint32_t)((int64_t)(q0 + 32 * qb + (lane & 31)) * ldb + (16 * s + 8 * h) * 2));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  const int64_t ldo = (int64_t)D * 2;
+  auto body = [&](auto qbc) {
+    constexpr int QB = decltype(qbc)::value;
+    float m[QB], l[QB];
+    f32x16 oacc[QB][2];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      m[qb] = -INFINITY;
+      l[qb] = 0.f;
+      oacc[qb][0] = zero16();
+      oacc[qb][1] = zero16();
+    }
+    auto tile = [&](auto uc, auto mc, int k0) {
+      constexpr int U = decltype(uc)::value;
+      constexpr bool MASK = decltype(mc)::value;
+      f32x16 st[QB][U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) st[qb][u] = zero16();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = frag_row(kt, k0 + 32 * u, s, lane);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) st[qb][u] = mfma32(kf, qf[qb][s], st[qb][u]);
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        if constexpr (MASK) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (k0 + 32 * u + acc_row(r, h) >= N) st[qb][u][r] = -INFINITY;
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[qb][u][r]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mn = fmaxf(m[qb], tmax * c2);
+        const float alpha = fexp2(m[qb] - mn);
+        const bool first = m[qb] == -INFINITY;
+        m[qb] = mn;
+        float rs = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fexp2(fmaf(st[qb][u][r], c2, -mn));
+            st[qb][u][r] = p;
+            rs += p;
+          }
+        l[qb] = fmaf(l[qb], alpha, rs);
+        if (!first && __builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[qb][dt][r] *= alpha;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pb[QB];
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) pb[qb] = pack8(st[qb][u], s);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const bf16x8 vf = frag_tr(vt, k0 + 32 * u + 16 * s, 32 * dt, lane);
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) oacc[qb][dt] = mfma32(vf, pb[qb], oacc[qb][dt]);
+          }
+        }
+    };
+    int k0 = 0;
+    for (; k0 + 64 <= N; k0 += 64) tile(std::integral_constant<int, 2>{}, std::false_type{}, k0);
+    if (k0 + 64 <= NP) {
+      tile(std::integral_constant<int, 2>{}, std::true_type{}, k0);
+      k0 += 64;
+    }
+    if (k0 < NP) tile(std::integral_constant<int, 1>{}, std::true_type{}, k0);
+    float inv[QB];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const float lt = l[qb] + __shfl_xor(l[qb], 32, 64);
+      const int q = q0 + 32 * qb + (lane & 31);
+      if (q < N && h == 0) lse[(int64_t)bh * N + q] = (m[qb] + log2f(lt)) * LN2;
+      inv[qb] = 1.f / lt;
+    }
+    __syncthreads();   // O through the (now free) K/V image
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) store_tile32(smem + wave * ST_BYTES, oacc[qb], inv[qb], ro, ldo, q0 + 32 * qb, lane_here());
+  };
+  if (q0 + 32 < N) body(std::integral_constant<int, 2>{});
+  else if (q0 < N) body(std::integral_constant<int, 1>{});
+  else __syncthreads();
+}
+
 // dQ (+ delta = rowsum(dO * O)): grid B*H, block 64*NW, wave w owns queries 32w..+31, K and V
 // of the whole sequence in LDS.  Keys >= N need no mask: their K rows are zero in LDS, so
 // their dS (whatever it is) meets a zero row of K in dQ = dS K.
@@ -1634,7 +1775,10 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
   if (int rc = attn_check(dtype, B, N, H, dh)) return rc;
   VITMI_CHECK_ARG(qkv && o && lse, "attention_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VITMI_BF16 && seq_path(N)) {
+  if (dtype == VITMI_BF16 && seq_path(N) && VITMI_ATTN_Q64) {
+    hipLaunchKernelGGL(attn_fwd_seq64_bf16<SEQ_MAX>, dim3(B * H), dim3(256), 0, s, (const bf16*)qkv, (bf16*)o, lse,
+                       N, H, scale);
+  } else if (dtype == VITMI_BF16 && seq_path(N)) {
     const dim3 block(64 * ((N + 31) / 32));
     hipLaunchKernelGGL(attn_fwd_seq_bf16<SEQ_MAX>, dim3(B * H), block, 0, s, (const bf16*)qkv, (bf16*)o, lse, N,
                        H, scale);
@@ -1653,7 +1797,8 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
     // QK^T and PV: 4 N^2 dh flops per (batch, head); q/k/v read, o + lse written
     const double es = dtype == VITMI_BF16 ? 2 : 4, bh = (double)B * H;
     const double fl = 4.0 * bh * N * N * DH, by = bh * N * DH * 4 * es + bh * N * 4;
-    if (dtype == VITMI_BF16 && seq_path(N)) VITMI_STAT(attn_fwd_seq_bf16<SEQ_MAX>, fl, by);
+    if (dtype == VITMI_BF16 && seq_path(N) && VITMI_ATTN_Q64) VITMI_STAT(attn_fwd_seq64_bf16<SEQ_MAX>, fl, by);
+    else if (dtype == VITMI_BF16 && seq_path(N)) VITMI_STAT(attn_fwd_seq_bf16<SEQ_MAX>, fl, by);
     else if (dtype == VITMI_BF16) VITMI_STAT(attn_fwd_bf16, fl, by);
     else if (seq_path(N)) VITMI_STAT(attn_fwd_seq_f32<SEQ_MAX>, fl, by);
     else VITMI_STAT(attn_fwd_f32, fl, by);
