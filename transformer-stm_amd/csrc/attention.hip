@@ -1110,6 +1110,157 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_bwd_dq_seq_bf16(
   }
 }
 
+// dQ (+ delta) with 4 waves of 64 queries (two 32-query blocks per wave, as attn_fwd_seq64_bf16):
+// each K / V fragment read feeds both blocks.  NKB = ceil(N / 32) key blocks (compile time).  Per
+// query block the arithmetic is attn_bwd_dq_seq_bf16's in the same order, and the q-bias column sums
+// fold the 32-row blocks in block order as its tile32_colsum does (bitwise equal outputs).
+template <int NPMAX, int NKB>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_seq64_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
+    float scale, float* __restrict__ colsum) {
+  constexpr int SMEM = 2 * NPMAX * 128;
+  constexpr int NP = NKB * 32;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ float red[NPMAX / 32][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int bh = gridDim.x - 1 - blockIdx.x, b = bh / H, hd = bh % H;
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const bf16* base = qkv + (int64_t)b * N * ld;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  __amdgpu_buffer_rsrc_t rq = make_rsrc(base + hd * DH, bytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+  __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+  char* kt = smem;
+  char* vt = smem + NP * 128;
+  stage_seq(kt, rk, ldb, NP, 4, wave, lane);
+  stage_seq(vt, rv, ldb, NP, 4, wave, lane);
+  const int q0 = wave * 64;
+  bf16x8 qf[2][4], df[2][4];
+  float dl[2], L2[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = q0 + 32 * qb + (lane & 31);
+    bf16x8 of[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t off = (uint32_t)((int64_t)q * ldo + (16 * s + 8 * h) * 2);
+      df[qb][s] = load_row16(rdo, off);
+      of[s] = load_row16(ro, off);
+    }
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)of[s][j] * (float)df[qb][s][j];
+    dl[qb] = part + __shfl_xor(part, 32, 64);
+    if (q < N && h == 0) delta[(int64_t)bh * N + q] = dl[qb];
+  }
+  asm volatile("" ::: "memory");   // keep the Q loads after the delta reductions (registers)
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = q0 + 32 * qb + (lane & 31);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[qb][s] = load_row16(rq, (uint32_t)((int64_t)q * ldb + (16 * s + 8 * h) * 2));
+    L2[qb] = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;   // q >= N -> p = 0
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv + (int64_t)b * N * ld + hd * DH, bytes - hd * DH * 2);
+  auto body = [&](auto qbc) {
+    constexpr int QB = decltype(qbc)::value;
+    f32x16 dqt[QB][2];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) dqt[qb][0] = dqt[qb][1] = zero16();
+    auto kblock = [&](const int k0) {
+      f32x16 st[QB], dp[QB];
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        st[qb] = zero16();
+        float ndl = VITMI_ATT_DPINIT ? -dl[qb] : 0.f;
+        asm volatile("" : "+v"(ndl));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[qb][r] = ndl;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = frag_row(kt, k0, s, lane), vf = frag_row(vt, k0, s, lane);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          st[qb] = mfma32(kf, qf[qb][s], st[qb]);
+          dp[qb] = mfma32(vf, df[qb][s], dp[qb]);
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(st[qb][r], c2, -L2[qb]));
+          dp[qb][r] = VITMI_ATT_DPINIT ? p * dp[qb][r] : p * (dp[qb][r] - dl[qb]);
+        }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int d2 = 0; d2 < 2; ++d2) {
+          const bf16x8 kr = frag_tr(kt, k0 + 16 * s, 32 * d2, lane);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) dqt[qb][d2] = mfma32(kr, pack8(dp[qb], s), dqt[qb][d2]);
+        }
+    };
+#pragma unroll
+    for (int k0 = 0; k0 < NP; k0 += 32) kblock(k0);
+    __syncthreads();   // dQ through the (now free) K/V image
+    const int ln = lane_here();
+    const int rr = ln >> 3, cc = ln & 7;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const int row0 = q0 + 32 * qb;
+      store_tile32(smem + wave * ST_BYTES, dqt[qb], scale, rdq, ldb, row0, ln);
+      if (colsum) {   // this block's column sums (tile32_colsum's first half), folded below
+        float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const char* scr = smem + wave * ST_BYTES;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (row0 + 8 * j + rr < N) {
+            const bf16x8 v = *(const bf16x8*)(scr + (8 * j + rr) * ST_PITCH + cc * 16);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          cs[e] += __shfl_xor(cs[e], 8, 64);
+          cs[e] += __shfl_xor(cs[e], 16, 64);
+          cs[e] += __shfl_xor(cs[e], 32, 64);
+        }
+        if (ln < 8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) red[2 * wave + qb][ln * 8 + e] = cs[e];
+        }
+        asm volatile("" ::: "memory");   // the next store_tile32 rewrites the image these reads used
+      }
+    }
+  };
+  if (q0 + 32 < N) body(std::integral_constant<int, 2>{});
+  else if (q0 < N) body(std::integral_constant<int, 1>{});
+  else __syncthreads();
+  if (colsum) {
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float t = 0.f;
+      for (int blk = 0; blk < NKB; ++blk) t += red[blk][threadIdx.x];
+      colsum[(int64_t)b * 3 * D + hd * DH + threadIdx.x] = t;
+    }
+  }
+}
+
 // dK/dV, persistent: grid = min(B*H, CUs) workgroups of 64*NW threads, each walking the (batch,
 // head) pairs bh = blockIdx.x, + gridDim.x, ...; wave w owns keys 32w..+31 and holds their K and
 // V rows in registers, the pair's Q and dO images sit in LDS.  At 165 VGPRs a CU holds one such
@@ -1864,7 +2015,10 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
       const int npairs = B * H, cus = device_cus();
       const dim3 gkv(npairs < cus ? npairs : cus);
       const bool n7 = (N + 31) / 32 == 7;   // N in (192, 224]: the ViT-B/ViT-S shape, N = 197
-      if (n7)
+      if (n7 && VITMI_ATTN_Q64)
+        hipLaunchKernelGGL((attn_bwd_dq_seq64_bf16<SEQ_MAX, 7>), dim3(B * H), dim3(256), 0, s, (const bf16*)qkv,
+                           (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
+      else if (n7)
         hipLaunchKernelGGL((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), dim3(B * H), block, 0, s, (const bf16*)qkv,
                            (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
       else
@@ -1911,7 +2065,8 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     const double fl = 4.0 * bh * N * N * DH;
     if (dtype == VITMI_BF16 && seq_path(N)) {
       if ((N + 31) / 32 == 7) {
-        VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+        if (VITMI_ATTN_Q64) VITMI_STAT((attn_bwd_dq_seq64_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+        else VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
         VITMI_STAT((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
       } else {
         VITMI_STAT(attn_bwd_dq_seq_bf16<SEQ_MAX>, fl, t * 6 * es + bh * N * 8);
