@@ -199,7 +199,8 @@ int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, con
                         void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_attention_bwd_workspace_size(int B, int N, int H);
 /* Kernel selection (process-wide; tests): 0 = auto, 1 = always the streamed (64-key LDS-tiled)
- * kernels.  Returns the previous policy. */
+ * kernels, 2 = the whole-sequence kernels' 32-query-per-wave forward and dQ forms (auto runs their
+ * 64-query forms, bitwise equal).  Returns the previous policy. */
 int vitmi_attention_set_policy(int policy);
 /* vitmi_attention_bwd plus the qkv bias gradient: dbias[3*H*dh] += column sums of dqkv (the
  * q/k/v Dense biases, models/CvT(Par).py:132-134).  On the bf16 paths the sums come from the

@@ -179,5 +179,7 @@ def test_policy_knobs_round_trip():
     prev = lib.vitmi_attention_set_policy(1)
     assert lib.vitmi_attention_set_policy(prev) == 1
     assert lib.vitmi_attention_set_policy(7) == 1              # out of range: rejected
+    assert lib.vitmi_attention_set_policy(2) == prev           # the 32-query whole-sequence forms
+    assert lib.vitmi_attention_set_policy(prev) == 2
     prev = lib.vitmi_gemm_set_reserved_cus(8)
     assert lib.vitmi_gemm_set_reserved_cus(prev) == 8

@@ -405,6 +405,30 @@ def test_attention_persistent_many_pairs(B, N, H):
         assert rel(d[:, i], g[:, i]) < 2e-2, name
 
 
+@pytest.mark.parametrize("B,N,H", [(48, 197, 12), (3, 224, 2), (2, 193, 1), (5, 64, 3), (2, 250, 2)])
+def test_attention_64query_forms_bitwise_equal(B, N, H):
+    """The whole-sequence forward and dQ run 4 waves of 64 queries (attn_fwd_seq64_bf16,
+    attn_bwd_dq_seq64_bf16, auto policy); policy 2 runs the 32-query forms.  Per query block the
+    arithmetic and the q-bias column-sum fold order are the same, so o, lse, dqkv and the fused
+    bias gradient are bitwise equal."""
+    D = 64 * H
+    qkv = rnd(B * N, 3 * D, dtype=BF, seed=51).to(DEV)
+    do = rnd(B * N, D, dtype=BF, seed=52).to(DEV)
+    out = {}
+    prev = ops.attention_set_policy(0)
+    try:
+        for pol in (0, 2):
+            ops.attention_set_policy(pol)
+            o, lse = ops.attention_fwd(qkv, B, N, H, 0.125)
+            db = torch.zeros(3 * D, device=DEV)
+            dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, H, 0.125, bias_grad=db)
+            out[pol] = (o, lse, dqkv, db)
+    finally:
+        ops.attention_set_policy(prev)
+    for a, b, name in zip(out[0], out[2], ("o", "lse", "dqkv", "dbias")):
+        assert torch.equal(a, b), name
+
+
 @pytest.mark.parametrize("B,N,H,T", [(2, 197, 2, BF), (3, 17, 1, BF), (1, 256, 3, BF), (2, 1, 2, BF),
                                      (2, 300, 1, BF), (3, 577, 2, BF), (2, 33, 2, torch.float32)])
 def test_attention_bwd_fused_bias(B, N, H, T):

@@ -1887,7 +1887,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_f32(const float* __restrict_
 using namespace vitmi;
 
 // whole-sequence kernels for N <= SEQ_MAX (8 waves, 2 workgroups of <= 64 KiB LDS per CU).
-// Kernel policy (vitmi_attention_set_policy; tests): 0 = auto, 1 = always the streamed kernels.
+// Kernel policy (vitmi_attention_set_policy; tests): 0 = auto, 1 = always the streamed kernels,
+// 2 = the whole-sequence 32-query-per-wave forward / dQ (attn_fwd_seq_bf16 / attn_bwd_dq_seq_bf16)
+// where auto takes their 64-query forms (bitwise equal by construction; the tests compare them).
 static constexpr int SEQ_MAX = 256;
 
 static int device_cus() {   // compute units of the current device (the persistent dK/dV grid)
@@ -1904,9 +1906,10 @@ static int device_cus() {   // compute units of the current device (the persiste
 }
 static int g_attn_policy = 0;
 static bool seq_path(int N) { return N <= SEQ_MAX && g_attn_policy != 1; }
+static bool q64() { return VITMI_ATTN_Q64 && g_attn_policy != 2; }
 
 extern "C" int vitmi_attention_set_policy(int policy) {
-  VITMI_CHECK_ARG(policy == 0 || policy == 1, "attention_set_policy: policy must be 0 or 1");
+  VITMI_CHECK_ARG(policy >= 0 && policy <= 2, "attention_set_policy: policy must be 0, 1 or 2");
   const int prev = g_attn_policy;
   g_attn_policy = policy;
   return prev;
@@ -1926,7 +1929,7 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
   if (int rc = attn_check(dtype, B, N, H, dh)) return rc;
   VITMI_CHECK_ARG(qkv && o && lse, "attention_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VITMI_BF16 && seq_path(N) && VITMI_ATTN_Q64) {
+  if (dtype == VITMI_BF16 && seq_path(N) && q64()) {
     hipLaunchKernelGGL(attn_fwd_seq64_bf16<SEQ_MAX>, dim3(B * H), dim3(256), 0, s, (const bf16*)qkv, (bf16*)o, lse,
                        N, H, scale);
   } else if (dtype == VITMI_BF16 && seq_path(N)) {
@@ -1948,7 +1951,7 @@ extern "C" int vitmi_attention_fwd(int dtype, int B, int N, int H, int dh, float
     // QK^T and PV: 4 N^2 dh flops per (batch, head); q/k/v read, o + lse written
     const double es = dtype == VITMI_BF16 ? 2 : 4, bh = (double)B * H;
     const double fl = 4.0 * bh * N * N * DH, by = bh * N * DH * 4 * es + bh * N * 4;
-    if (dtype == VITMI_BF16 && seq_path(N) && VITMI_ATTN_Q64) VITMI_STAT(attn_fwd_seq64_bf16<SEQ_MAX>, fl, by);
+    if (dtype == VITMI_BF16 && seq_path(N) && q64()) VITMI_STAT(attn_fwd_seq64_bf16<SEQ_MAX>, fl, by);
     else if (dtype == VITMI_BF16 && seq_path(N)) VITMI_STAT(attn_fwd_seq_bf16<SEQ_MAX>, fl, by);
     else if (dtype == VITMI_BF16) VITMI_STAT(attn_fwd_bf16, fl, by);
     else if (seq_path(N)) VITMI_STAT(attn_fwd_seq_f32<SEQ_MAX>, fl, by);
@@ -2015,7 +2018,7 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
       const int npairs = B * H, cus = device_cus();
       const dim3 gkv(npairs < cus ? npairs : cus);
       const bool n7 = (N + 31) / 32 == 7;   // N in (192, 224]: the ViT-B/ViT-S shape, N = 197
-      if (n7 && VITMI_ATTN_Q64)
+      if (n7 && q64())
         hipLaunchKernelGGL((attn_bwd_dq_seq64_bf16<SEQ_MAX, 7>), dim3(B * H), dim3(256), 0, s, (const bf16*)qkv,
                            (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale, colsum);
       else if (n7)
@@ -2065,7 +2068,7 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     const double fl = 4.0 * bh * N * N * DH;
     if (dtype == VITMI_BF16 && seq_path(N)) {
       if ((N + 31) / 32 == 7) {
-        if (VITMI_ATTN_Q64) VITMI_STAT((attn_bwd_dq_seq64_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
+        if (q64()) VITMI_STAT((attn_bwd_dq_seq64_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
         else VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
         VITMI_STAT((attn_bwd_dkv_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
       } else {

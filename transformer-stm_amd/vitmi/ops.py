@@ -312,7 +312,8 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor, w: Tensor,
 
 # ---------------------------------------------------------------- attention
 def attention_set_policy(policy: int) -> int:
-    """0 = auto, 1 = always the streamed kernels (tests).  Returns the previous policy."""
+    """0 = auto, 1 = always the streamed kernels, 2 = the whole-sequence 32-query forward / dQ
+    forms (tests).  Returns the previous policy."""
     return lib().vitmi_attention_set_policy(int(policy))
 
 
