@@ -44,10 +44,15 @@ def main():
         "fc1 dgrad": lambda: ops.linear_dgrad(h, w1, BF),
         "fc1 wgrad": lambda: ops.linear_wgrad(h, x, dw),
     }
+    import time
     for name, fn in cases.items():
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
+        # >= 2 s of back-to-back launches first, so the stamped launch runs at the clock the chip
+        # holds under this load (DVFS)
+        t_end = time.time() + 2.0
+        while time.time() < t_end:
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize()
         lib.vitmi_gemm_set_stamps(buf.data_ptr())
         buf.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -73,6 +78,13 @@ def main():
         per_x = [(st[x::8, :, :, 1] - st[x::8, :, :, 0])[valid[x::8]].double().mean().item() for x in range(8)]
         w0 = (st[:, :, 0, 1] - st[:, :, 0, 0])[valid[:, :, 0]].double().mean().item()
         w4 = (st[:, :, 1, 1] - st[:, :, 1, 0])[valid[:, :, 1]].double().mean().item()
+        # in-kernel clock: s_memtime cycles per s_memrealtime tick (100 MHz) between consecutive
+        # K-loop starts of one wave
+        both = (st[:, 1:, :, 0] > 0) & (st[:, :-1, :, 0] > 0) & (st[:, 1:, :, 3] > st[:, :-1, :, 3])
+        dcy = (st[:, 1:, :, 0] - st[:, :-1, :, 0])[both].double()
+        drt = (st[:, 1:, :, 3] - st[:, :-1, :, 3])[both].double()
+        clk = (dcy / drt * 0.1).median().item() if dcy.numel() else float("nan")   # GHz
+        print(f"   in-kernel clock {clk:.2f} GHz (median over {dcy.numel()} tile intervals)")
         print(f"   per-iter kloop: {' '.join(f'{v:6.0f}' for v in per_it)}")
         print(f"   per-XCD  kloop: {' '.join(f'{v:6.0f}' for v in per_x)}   wave0 {w0:6.0f} wave4 {w4:6.0f}")
         print(f"{name:10s} {us:7.1f} us | tiles/block {iters.min():.0f}-{iters.max():.0f} | cycles: kloop "
