@@ -378,6 +378,20 @@ def test_knob_split_qkv_override_small_model(knob, split_qkv):
     print(f"C1 {knob} split_qkv={split_qkv}: logits {err:.3e}, worst grad {worst[1]} {worst[0]:.3e}")
 
 
+@pytest.mark.parametrize("knob,split_qkv", [("bf16x3", False), ("bf16f8", True)])
+def test_knob_split_qkv_override_streamed_n290(knob, split_qkv):
+    """The split_qkv overrides on the streamed-attention path (ViT-Ti/16 272 px, N = 290, depth 4,
+    the fp32 O of the knobs' streamed forward): logits within 1e-3 of the fp32 oracle."""
+    cfg = config_c1(dtype=knob, img_size=272, depth=4, split_qkv=split_qkv)
+    params = vit_ref.init_params(cfg, seed=8)
+    img, tgt = vit_ref.synthetic_batch(cfg, 2)
+    l_ref = vit_ref.forward(img, params, cfg)
+    logits, _, _ = gpu_step(cfg, params, img, tgt)
+    err = (logits - l_ref).abs().max().item()
+    print(f"N=290 {knob} split_qkv={split_qkv}: logits {err:.3e}")
+    assert err <= 1e-3
+
+
 @pytest.mark.parametrize("knob", ["bf16x3", "bf16f8"])
 def test_bf16x3_knob_streamed_attention_n290(knob):
     """bf16 and bf16x3 at N > 256 (ViT-Ti/16 at 272 px, N = 290, depth 4: the streamed attention
