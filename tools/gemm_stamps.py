@@ -18,7 +18,7 @@ BF = torch.bfloat16
 def main():
     lib = _lib.lib()
     lib.vitmi_gemm_set_stamps.argtypes = [ctypes.c_void_p]
-    buf = torch.zeros(256 * 16 * 2 * 4, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(256 * 16 * 2 * 8, dtype=torch.int64, device="cuda")
     g = torch.Generator(device="cuda").manual_seed(0)
     r = lambda *s: (torch.rand(*s, device="cuda", generator=g) * 2 - 1).to(BF)  # noqa: E731
     x, h = r(M, D), r(M, F)
@@ -62,7 +62,7 @@ def main():
         torch.cuda.synchronize()
         lib.vitmi_gemm_set_stamps(None)
         us = e0.elapsed_time(e1) * 1e3
-        st = buf.view(256, 16, 2, 4).cpu()
+        st = buf.view(256, 16, 2, 8).cpu()
         valid = st[..., 2] > 0
         t0 = st[..., 0][valid].min().item()
         kl = (st[..., 1] - st[..., 0])[valid].double()
@@ -78,13 +78,12 @@ def main():
         per_x = [(st[x::8, :, :, 1] - st[x::8, :, :, 0])[valid[x::8]].double().mean().item() for x in range(8)]
         w0 = (st[:, :, 0, 1] - st[:, :, 0, 0])[valid[:, :, 0]].double().mean().item()
         w4 = (st[:, :, 1, 1] - st[:, :, 1, 0])[valid[:, :, 1]].double().mean().item()
-        # in-kernel clock: s_memtime cycles per s_memrealtime tick (100 MHz) between consecutive
-        # K-loop starts of one wave
-        both = (st[:, 1:, :, 0] > 0) & (st[:, :-1, :, 0] > 0) & (st[:, 1:, :, 3] > st[:, :-1, :, 3])
-        dcy = (st[:, 1:, :, 0] - st[:, :-1, :, 0])[both].double()
-        drt = (st[:, 1:, :, 3] - st[:, :-1, :, 3])[both].double()
+        # in-kernel clock: s_memtime cycles per s_memrealtime tick (100 MHz) over each K-loop
+        kv = valid & (st[..., 4] > st[..., 3])
+        dcy = (st[..., 1] - st[..., 0])[kv].double()
+        drt = (st[..., 4] - st[..., 3])[kv].double()
         clk = (dcy / drt * 0.1).median().item() if dcy.numel() else float("nan")   # GHz
-        print(f"   in-kernel clock {clk:.2f} GHz (median over {dcy.numel()} tile intervals)")
+        print(f"   in-kernel clock {clk:.2f} GHz (median over {dcy.numel()} K-loops)")
         print(f"   per-iter kloop: {' '.join(f'{v:6.0f}' for v in per_it)}")
         print(f"   per-XCD  kloop: {' '.join(f'{v:6.0f}' for v in per_x)}   wave0 {w0:6.0f} wave4 {w4:6.0f}")
         print(f"{name:10s} {us:7.1f} us | tiles/block {iters.min():.0f}-{iters.max():.0f} | cycles: kloop "

@@ -773,14 +773,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   // than the half-tiles the first K-step waits for, so its counts may grow by that many.
   int ep_ops = 0;
 #ifdef VITMI_GEMM_STAMPS
-  // [block][iter][wave-half][4]: K-loop start, epilogue start, epilogue end (s_memtime), and
-  // s_memrealtime (100 MHz) at the K-loop start: the in-kernel clock between two iterations
+  // [block][iter][wave-half][8]: K-loop start, epilogue start, epilogue end (s_memtime), then
+  // s_memrealtime (100 MHz) at the same three points: the in-kernel clock of each K-loop
   int st_it = 0;
   auto stamp = [&](int k) {
     if (g.stamps && lane == 0 && (wave == 0 || wave == 4) && st_it < 16) {
-      unsigned long long* p_ = g.stamps + ((blockIdx.x * 16 + st_it) * 2 + (wave >> 2)) * 4;
+      unsigned long long* p_ = g.stamps + ((blockIdx.x * 16 + st_it) * 2 + (wave >> 2)) * 8;
       p_[k] = __builtin_amdgcn_s_memtime();
-      if (k == 0) p_[3] = __builtin_amdgcn_s_memrealtime();
+      p_[3 + k] = __builtin_amdgcn_s_memrealtime();
     }
   };
 #else
