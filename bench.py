@@ -18,8 +18,10 @@ Rank 0 prints ONE JSON line.  Besides the contract fields it carries, measured i
   per_kernel    a rocprofv3 --kernel-trace --stats child run of this bench (3 steps), joined
                 with the library's own per-kernel algorithmic work (vitmi_stats_*): ms/step,
                 TFLOP/s, GB/s and MFMA fraction per kernel;
-  cpu_baseline  the CPU oracle's fwd+bwd on the host cores (rank 0 at N=1 only), plus the
-                bf16 GPU logits' max-abs distance from the fp32 oracle on the same weights.
+  cpu_baseline  the CPU oracle's fwd+bwd on the host cores (rank 0 at N=1 only);
+  parity        this line's own arithmetic (dtype, knobs) against the north star's 1e-3: logits
+                max-abs of the line's full-depth model with randomised parameters on 2 images
+                vs the fp32 CPU oracle (every line, secondary ones included).
 The evidence legs run after the timed region (N=1, rank 0) and never change `value`.
 """
 from __future__ import annotations
@@ -65,7 +67,7 @@ def _lscpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(cfg, batch: int, steps: int, model=None, dev=None):
+def cpu_baseline(cfg, batch: int, steps: int):
     """The CPU oracle (oracle/vit_ref.py, fp32) timed on this host's cores: 1 warm-up step and
     `steps` timed steps at `batch` images (BASELINE.md §2 protocol).  Threads: every core of the
     affinity mask, capped by the pool's per-GPU CPU share (OMP_NUM_THREADS, set to 16 on the
@@ -90,16 +92,34 @@ def cpu_baseline(cfg, batch: int, steps: int, model=None, dev=None):
            "sample": f"oracle/vit_ref.py fp32 fwd+bwd ViT-B/16 224px, bs={batch}, 1 warm-up + {steps} timed "
                      f"steps ({dt_:.1f} s), torch CPU threads={cores} (affinity {affinity}, pool share "
                      f"OMP_NUM_THREADS={share})"}
-    if model is not None:
-        # the same weights through the bf16 GPU path and the fp32 oracle: logits distance
-        with torch.no_grad():
-            p = {k: v.detach().float().cpu() for k, v in model.named_parameters()}
-            x, _ = vit_ref.synthetic_batch(cfg, 2, seed=99)
-            ref = vit_ref.forward(x, p, cfg)
-            got = model(x.to(dev)).float().cpu()
-        out["parity_bf16_logits_max_abs"] = float((got - ref).abs().max().item())
-        out["parity_sample"] = "2 images, the bench model's weights after the timed steps, fp32 CPU oracle"
     return out
+
+
+NORTH_STAR_LOGITS = 1e-3    # BASELINE.json north_star: logits within 1e-3 of the fp32 CPU reference
+
+
+def parity_check(cfg, dev, n_img: int = 2):
+    """The north-star logits check of THIS line's arithmetic, after the timed region: the line's
+    model (its config, compute dtype and knob settings) at full depth with randomised parameters
+    (every weight, bias, LayerNorm gamma/beta drawn: vit_ref.init_params(randomize_all=True), the
+    stress case of tests/test_gpu_model.py) on `n_img` synthetic images, GPU logits against the
+    fp32 CPU oracle (oracle/vit_ref.py) on the same parameters and inputs."""
+    from oracle import vit_ref
+    t0 = time.perf_counter()
+    params = vit_ref.init_params(cfg, seed=0, randomize_all=True)
+    x, _ = vit_ref.synthetic_batch(cfg, n_img)
+    with torch.no_grad():
+        ref = vit_ref.forward(x, params, cfg)
+        model = VisionTransformer(cfg).to(dev)
+        model.load_param_dict(params)
+        got = model(x.to(dev)).float().cpu()
+    del model
+    err = float((got - ref).abs().max().item())
+    return {"logits_max_abs": err, "bound": NORTH_STAR_LOGITS, "within_bound": err <= NORTH_STAR_LOGITS,
+            "logits_max_abs_ref": float(ref.abs().max().item()),
+            "sample": f"{n_img} synthetic images, this line's model ({cfg.depth} blocks, D={cfg.embed_dim}, "
+                      f"{cfg.img_size}px, dtype {cfg.dtype}) with randomised parameters (init_params seed 0, "
+                      f"randomize_all), GPU logits vs the fp32 CPU oracle ({time.perf_counter() - t0:.1f} s)"}
 
 
 # ------------------------------------------------------------------ evidence legs (child runs)
@@ -294,6 +314,8 @@ def main():
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="CUs the persistent GEMM leaves to RCCL while buckets are in flight (N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the line's logits check against the fp32 CPU oracle (after the timed region)")
     ap.add_argument("--no-evidence", action="store_true", help="skip the rocprofv3 per-kernel / traffic legs")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -343,6 +365,7 @@ def main():
     if world > 1 and args.comm == "vitmi":
         # the library's own RCCL communicator, or (RCCL refused it on some rank) torch.distributed's
         # RCCL process group: the line then says so instead of the multi-GPU run ending without one
+        os.environ.setdefault("VITMI_COMM_INIT_TIMEOUT_S", "180")   # a peer that never joins: fall back
         comm, group, err = dp.comm_or_fallback(rank, world)
         if comm is None:
             comm_leg = "torch (fallback: vitmi comm init failed)"
@@ -489,8 +512,10 @@ def main():
         out["allreduce_exposed_ms"] = phases_ms.get("allreduce_wait")
         out.update(dp.replica_report(arena.flat, group))
     red.close()                               # the comm watchdog thread (the step loop is over)
+    if rank == 0 and not args.no_parity and not args.stats_out:
+        out["parity"] = parity_check(cfg, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
-        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps, model, dev)
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_batch, args.cpu_steps)
     if rank == 0 and world == 1 and not args.no_evidence and args.config == "c3" and not args.stats_out:
         del model, opt, arena, red, params
         torch.cuda.empty_cache()
@@ -530,6 +555,9 @@ def secondary_lines():
     # exact-fp32 arithmetic throughout
     runs = {"c3_bf16f8": ["--config", "c3", "--dtype", "bf16f8", "--steps", "10", "--warmup", "3"],
             "c3_bf16x3": ["--config", "c3", "--dtype", "bf16x3", "--steps", "10", "--warmup", "3"],
+            # the north star's host-side optimizer: torch's fused Adam on the parameters (the
+            # headline runs the reference's Keras Adam as one vitmi launch)
+            "c3_torch_adam": ["--config", "c3", "--optimizer", "torch", "--steps", "10", "--warmup", "3"],
             "c5": ["--config", "c5", "--steps", "10", "--warmup", "3"],
             "c2": ["--config", "c2", "--steps", "10", "--warmup", "3"],
             "c3_fp32": ["--config", "c3", "--dtype", "fp32", "--steps", "3", "--warmup", "1"]}
@@ -547,7 +575,9 @@ def secondary_lines():
             out[cfg] = {"error": f"child rc={rc}"}
             continue
         out[cfg] = {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "step_mfma_frac", "dtype",
-                                         "phases_ms")}
+                                         "phases_ms", "optimizer_ms") if k in line}
+        if "parity" in line:
+            out[cfg]["parity"] = line["parity"]
         out[cfg]["config"] = line["config"]
         r = line["roofline"]
         out[cfg]["dominant_kernel"] = {"kernel": r["kernel"], "avg_launch_ms": r["avg_launch_ms"],

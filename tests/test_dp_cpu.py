@@ -372,18 +372,84 @@ print("ok", round(dt, 3))
 """
 
 
-def test_watchdog_abort_releases_a_blocked_allreduce(tmp_path):
-    """ADVICE / verdict r04: the watchdog's abort must not wait behind an all-reduce enqueue that
-    blocks (a peer gone), it must release it.  A stub librccl.so (tests/stub/stub_rccl.c, loaded
-    through VITMI_RCCL_LIB) blocks ncclAllReduce until ncclCommAbort; the training thread's enqueue
-    must return an error within the watchdog's timeout, the CU reservation stays with the training
-    thread, and later calls fail cleanly (csrc/comm.cpp keeps the communicator alive until the
-    in-flight call has left)."""
+def _build_stub(tmp_path):
     import subprocess
     so = tmp_path / "stub_rccl.so"
     subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-o", str(so), os.path.join(ROOT, "tests", "stub", "stub_rccl.c"),
-                    "-lpthread"], check=True)
+                    "-lpthread", "-ldl"], check=True)
+    return so
+
+
+@pytest.mark.parametrize("blocking", [False, True], ids=["nonblocking", "blocking"])
+def test_watchdog_abort_releases_a_blocked_allreduce(tmp_path, blocking):
+    """the watchdog's abort must not wait behind an all-reduce that never
+    completes (a peer gone), it must release it, and it must never free the communicator under a
+    call in flight.  A stub librccl.so (tests/stub/stub_rccl.c, loaded through VITMI_RCCL_LIB) never
+    completes ncclAllReduce until ncclCommAbort.  Non-blocking (the library's default: its config
+    init) the enqueue returns ncclInProgress and the library polls; the stub's abort FREES and poisons
+    the communicator, so a library call that touched the handle after the abort would fail the check.
+    Blocking (the stub refuses the config: the fallback init) the enqueue blocks inside RCCL.  Either
+    way the training thread's call returns an error within the watchdog's timeout, the CU reservation
+    stays with the training thread, and later calls fail cleanly."""
+    import subprocess
+    so = _build_stub(tmp_path)
     env = dict(os.environ, VITMI_RCCL_LIB=str(so), VITMI_PKG=os.path.join(ROOT, "transformer-stm_amd"))
+    if blocking:
+        env["STUB_RCCL_NO_CONFIG"] = "1"
     r = subprocess.run([sys.executable, "-c", _ABORT_CHILD], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
     assert float(r.stdout.split()[1]) < 3.0
+
+
+_SHM_CHILD = r"""
+import os, sys
+sys.path[:0] = [os.environ["VITMI_PKG"]]
+import torch
+import torch.distributed as dist
+from vitmi import dp
+from vitmi._lib import check
+rank, world = int(sys.argv[1]), 2
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + sys.argv[2], rank=rank, world_size=world)
+comm = dp.VitmiComm.from_store(rank, world)          # vitmi_comm_init(world = 2) over the stub
+assert comm.info() == (rank, world), comm.info()
+def call(name, t, *a):
+    check(comm._call(name, t.data_ptr(), t.numel(), *a), name)
+x = torch.arange(3 * (1 << 20) + 5, dtype=torch.float32) * (rank + 1)       # > one 8 MiB stub slot
+call("vitmi_comm_allreduce_async", x, 0, dp.REDUCE_AVG, None, None)
+want = torch.arange(x.numel(), dtype=torch.float32) * 1.5
+assert torch.equal(x, want), (x[:4], want[:4])
+b = torch.full((1000,), float(rank), dtype=torch.bfloat16)
+call("vitmi_comm_allreduce_async", b, 1, dp.REDUCE_SUM, None, None)
+assert torch.equal(b, torch.full((1000,), 1.0, dtype=torch.bfloat16))
+p = torch.randn(777, generator=torch.Generator().manual_seed(rank))
+p0 = torch.randn(777, generator=torch.Generator().manual_seed(0))
+call("vitmi_comm_broadcast", p, 0, 0, None)
+assert torch.equal(p, p0)
+comm.check()
+comm.destroy()
+dist.destroy_process_group()
+print("ok", rank)
+"""
+
+
+def test_library_comm_world2_over_functional_stub(tmp_path):
+    """The library's own communicator at world 2 (vitmi_comm_init, the non-blocking init poll, the
+    enqueue under the comm lock, ncclAvg / ncclSum in fp32 and bf16, broadcast, destroy) between two
+    real processes: the stub's shm mode reduces through POSIX shared memory (host buffers here,
+    STUB_RCCL_HOST=1; tests/test_gpu_dp.py runs the same stub on device buffers)."""
+    import subprocess
+    so = _build_stub(tmp_path)
+    env = dict(os.environ, VITMI_RCCL_LIB=str(so), VITMI_PKG=os.path.join(ROOT, "transformer-stm_amd"),
+               STUB_RCCL_MODE="shm", STUB_RCCL_HOST="1")
+    port = str(_free_port())
+    procs = [subprocess.Popen([sys.executable, "-c", _SHM_CHILD, str(r), port], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=120)[0])
+        except subprocess.TimeoutExpired:
+            p.kill()
+            outs.append(p.communicate()[0])
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and f"ok {r}" in o, o

@@ -180,3 +180,27 @@ def test_split_bf16f8_weights_batch_matches_single():
     for w, o in zip(ws, outs):
         ref, _ = ops.split_bf16f8(w, 1)
         assert o.shape == ref.shape and torch.equal(o, ref)
+
+
+@pytest.mark.parametrize("amp,bound", [(200.0, "knob"), (2000.0, "bf16")])
+def test_bf16f8_gemm_large_magnitudes(amp, bound):
+    """the fixed e4m3 scales bound where the corrections hold (csrc/common.h).  With
+    activations of |x| up to ~200 (lo8 = lo * 2^9 <= 2|x| stays under e4m3's 448) the product keeps
+    the knob's accuracy, >= 10x better than plain bf16; at |x| ~ 2000 hi8 and lo8 saturate and the
+    product only keeps roughly plain-bf16 accuracy (no worse than 2x the bf16 GEMM's error)."""
+    M, N, K = 197 * 2, 768, 768
+    x = (rnd(M, K, seed=131).clamp(-3, 3) * (amp / 3)).to(DEV)
+    w = (rnd(N, K, seed=132) * 0.05).to(DEV)
+    x8, _ = ops.split_bf16f8(x, 0)
+    w8, _ = ops.split_bf16f8(w, 1)
+    y = ops.linear_fwd(x8, w8, None, torch.float32, f8=True).double().cpu()
+    exact = x.double().cpu() @ w.double().cpu().t()
+    y1 = ops.linear_fwd(x.to(BF), w.to(BF), None, torch.float32).double().cpu()
+    scale = exact.norm()
+    e8 = ((y - exact).norm() / scale).item()
+    e16 = ((y1 - exact).norm() / scale).item()
+    print(f"bf16f8 GEMM |x| <= {amp:g}: rel err {e8:.2e}, plain bf16 {e16:.2e}")
+    if bound == "knob":
+        assert e8 < 1.5e-4 and e16 > 10 * e8, (e8, e16)
+    else:
+        assert e8 < 2 * e16, (e8, e16)

@@ -14,21 +14,25 @@
 //
 // RCCL is taken from VITMI_RCCL_LIB when that is set (a specific build; the CPU tests' stub).
 //
-// Thread safety: g_mu guards only the bookkeeping (which communicator is current, its users),
-// never an RCCL call.  An enqueue takes a reference to the current communicator under the lock,
-// drops the lock and calls RCCL; vitmi_comm_destroy(1) (the DP watchdog's abort, from its own
-// thread: vitmi/dp.py CommWatchdog) detaches the communicator under the lock and calls
-// ncclCommAbort WITHOUT waiting for in-flight enqueues, since an enqueue blocked on a dead peer
-// is exactly what the abort has to release (ncclCommAbort is meant to be called while another
-// thread is inside the communicator).  The wrapper object is freed by whichever of the abort and
-// the last in-flight call finishes last (a reference count), so no call touches a freed handle;
-// a graceful vitmi_comm_destroy(0) waits for in-flight calls before ncclCommDestroy.
+// Thread safety.  The communicator is created NON-BLOCKING (ncclCommInitRankConfig, blocking = 0):
+// no RCCL call then waits for a peer (an enqueue returns ncclInProgress and the wait is a poll of
+// ncclCommGetAsyncError), so every RCCL call on a communicator runs under g_mu, and the DP
+// watchdog's abort (vitmi_comm_destroy(1), from its own thread: vitmi/dp.py CommWatchdog) takes
+// g_mu too: ncclCommAbort can never free the handle under another thread's call.  A
+// poll drops the lock between two queries and gives up as soon as the communicator is released.
+// The Comm wrapper is reference-counted (enqueues in flight hold one), so it outlives the handle.
+// Where the RCCL build lacks ncclCommInitRankConfig (or refuses the config) the communicator is
+// blocking: calls then run WITHOUT the lock, because an enqueue blocked on a dead peer is what
+// the abort must release, and the abort is not serialised with them (the older scheme).
+// A graceful vitmi_comm_destroy(0) waits for in-flight calls before ncclCommDestroy.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <condition_variable>
 #include <mutex>
 #include <stdlib.h>
 #include <rccl/rccl.h>
+#include <chrono>
+#include <thread>
 #include <stdio.h>
 #include <string.h>
 #include "common.h"
@@ -40,6 +44,7 @@ struct Rccl {
   void* handle = nullptr;
   decltype(&::ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&::ncclCommInitRank) init_rank = nullptr;
+  decltype(&::ncclCommInitRankConfig) init_rank_config = nullptr;   // optional (non-blocking init)
   decltype(&::ncclAllReduce) all_reduce = nullptr;
   decltype(&::ncclBroadcast) broadcast = nullptr;
   decltype(&::ncclCommDestroy) destroy = nullptr;
@@ -56,6 +61,7 @@ std::condition_variable g_idle;  // a Comm's users dropped to 0 (graceful destro
 struct Comm {
   ncclComm_t comm = nullptr;
   int rank = -1, world = 0;
+  bool nonblocking = false;  // created with blocking = 0: RCCL calls run under g_mu
   int users = 0;           // enqueues in flight (between acquire and release)
   bool detached = false;   // no longer current: destroy / abort took it
   bool released = false;   // its RCCL handle is gone (aborted or destroyed)
@@ -123,6 +129,7 @@ int bind_rccl(void* h) {
       !sym(h, "ncclCommDestroy", r.destroy) || !sym(h, "ncclCommAbort", r.abort) ||
       !sym(h, "ncclGetErrorString", r.err) || !sym(h, "ncclCommGetAsyncError", r.async_err))
     return fail(VITMI_ERR_COMM, "comm: librccl.so lacks an NCCL 2.x entry point");
+  sym(h, "ncclCommInitRankConfig", r.init_rank_config);
   g_rccl = r;
   return VITMI_OK;
 }
@@ -137,6 +144,52 @@ bool dtype_of(int dtype, ncclDataType_t& t) {
   else if (dtype == VITMI_F64) t = ncclFloat64;
   else return false;
   return true;
+}
+
+// Poll a non-blocking communicator until its pending operation (init or an enqueue) has left
+// ncclInProgress; the lock is held only around each query, and a released communicator (the
+// watchdog's abort) ends the wait.  `deadline_s` > 0 bounds it (init).  -> the final state.
+ncclResult_t wait_ready(Comm* c, double deadline_s, bool* released) {
+  const auto t0 = std::chrono::steady_clock::now();
+  *released = false;
+  for (int spin = 0;; ++spin) {
+    ncclResult_t a = ncclSuccess, r;
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (c->released) { *released = true; return ncclInvalidUsage; }
+      r = g_rccl.async_err(c->comm, &a);
+    }
+    if (r != ncclSuccess) return r;
+    if (a != ncclInProgress) return a;
+    if (deadline_s > 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > deadline_s)
+      return ncclInProgress;
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    else std::this_thread::yield();
+  }
+}
+
+// One collective enqueue on the communicator `c` (a reference the caller holds): under g_mu for a
+// non-blocking communicator (re-checking that it was not released), then the poll; without the
+// lock for a blocking one.
+template <typename F>
+int enqueue(Comm* c, const char* what, F call) {
+  ncclResult_t r;
+  if (c->nonblocking) {
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (c->released) return fail(VITMI_ERR_COMM, "comm: %s: communicator aborted", what);
+      r = call(c->comm);
+    }
+    if (r == ncclInProgress) {
+      bool rel = false;
+      r = wait_ready(c, 0, &rel);
+      if (rel) return fail(VITMI_ERR_COMM, "comm: %s: communicator aborted", what);
+    }
+  } else {
+    r = call(c->comm);   // no lock held: an abort from another thread may release this call
+  }
+  return r ? nccl_fail(what, r) : VITMI_OK;
 }
 
 }  // namespace
@@ -166,9 +219,39 @@ extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
   ncclUniqueId id;
   memcpy(id.internal, uid, VITMI_COMM_UID_BYTES);
   ncclComm_t c = nullptr;
+  bool nonblocking = false;
   // the communicator binds to the calling thread's current HIP device; the rendezvous with the
-  // other ranks runs without the lock held
-  if (ncclResult_t r = g_rccl.init_rank(&c, world, id, rank)) return nccl_fail("ncclCommInitRank", r);
+  // other ranks runs without the lock held.  Non-blocking where the library takes a config: the
+  // init is then a poll bounded by VITMI_COMM_INIT_TIMEOUT_S (default 600 s), so a rank whose
+  // peer never joins fails instead of blocking for ever
+  if (g_rccl.init_rank_config) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = g_rccl.init_rank_config(&c, world, id, rank, &cfg);
+    if (r == ncclSuccess || r == ncclInProgress) {
+      nonblocking = true;
+      if (r == ncclInProgress) {
+        const char* e = getenv("VITMI_COMM_INIT_TIMEOUT_S");
+        const double tmo = e && *e ? atof(e) : 600.0;
+        Comm probe;   // not published: only wait_ready's view of the handle
+        probe.comm = c;
+        bool rel = false;
+        r = wait_ready(&probe, tmo > 0 ? tmo : 600.0, &rel);
+        if (r != ncclSuccess) {
+          g_rccl.abort(c);
+          return r == ncclInProgress ? fail(VITMI_ERR_COMM, "comm_init: ncclCommInitRankConfig not done after %g s "
+                                                            "(a peer never joined?)", tmo)
+                                     : nccl_fail("ncclCommInitRankConfig", r);
+        }
+      }
+    } else if (r != ncclInvalidArgument && r != ncclInvalidUsage) {
+      return nccl_fail("ncclCommInitRankConfig", r);
+    } else {
+      c = nullptr;   // the library refused the config: blocking init below
+    }
+  }
+  if (!nonblocking)
+    if (ncclResult_t r = g_rccl.init_rank(&c, world, id, rank)) return nccl_fail("ncclCommInitRank", r);
   std::unique_lock<std::mutex> lk(g_mu);
   if (g_cur != nullptr) {
     lk.unlock();
@@ -179,6 +262,7 @@ extern "C" int vitmi_comm_init(int rank, int world, const char* uid) {
   n->comm = c;
   n->rank = rank;
   n->world = world;
+  n->nonblocking = nonblocking;
   g_cur = n;
   return VITMI_OK;
 }
@@ -217,9 +301,8 @@ extern "C" int vitmi_comm_allreduce_async(void* ptr, int64_t count, int dtype, i
     if (e != hipSuccess) return fail(VITMI_ERR_HIP, "comm_allreduce_async: hipStreamWaitEvent: %s", hipGetErrorString(e));
   }
   const ncclRedOp_t rop = op == VITMI_REDUCE_AVG ? ncclAvg : ncclSum;
-  // no lock held: an abort from another thread may release this call (it then fails here)
-  if (ncclResult_t r = g_rccl.all_reduce(ptr, ptr, (size_t)count, t, rop, ref.c->comm, s)) return nccl_fail("ncclAllReduce", r);
-  return VITMI_OK;
+  return enqueue(ref.c, "ncclAllReduce",
+                 [&](ncclComm_t c) { return g_rccl.all_reduce(ptr, ptr, (size_t)count, t, rop, c, s); });
 }
 
 extern "C" int vitmi_comm_broadcast(void* ptr, int64_t count, int dtype, int root, vitmi_stream_t stream) {
@@ -229,16 +312,25 @@ extern "C" int vitmi_comm_broadcast(void* ptr, int64_t count, int dtype, int roo
   VITMI_CHECK_ARG(ref.c != nullptr, "comm_broadcast: vitmi_comm_init first");
   VITMI_CHECK_ARG(root >= 0 && root < ref.c->world, "comm_broadcast: bad root %d", root);
   if (count == 0) return VITMI_OK;
-  if (ncclResult_t r = g_rccl.broadcast(ptr, ptr, (size_t)count, t, root, ref.c->comm, (hipStream_t)stream))
-    return nccl_fail("ncclBroadcast", r);
-  return VITMI_OK;
+  return enqueue(ref.c, "ncclBroadcast", [&](ncclComm_t c) {
+    return g_rccl.broadcast(ptr, ptr, (size_t)count, t, root, c, (hipStream_t)stream);
+  });
 }
 
 extern "C" int vitmi_comm_check(void) {
   Ref ref;
   if (!ref.c) return VITMI_OK;
-  ncclResult_t a = ncclSuccess;
-  if (ncclResult_t r = g_rccl.async_err(ref.c->comm, &a)) return nccl_fail("ncclCommGetAsyncError", r);
+  ncclResult_t a = ncclSuccess, r;
+  {
+    // (a non-blocking communicator's handle is only touched under the lock; see the header)
+    std::unique_lock<std::mutex> lk(g_mu, std::defer_lock);
+    if (ref.c->nonblocking) {
+      lk.lock();
+      if (ref.c->released) return fail(VITMI_ERR_COMM, "comm_check: communicator aborted");
+    }
+    r = g_rccl.async_err(ref.c->comm, &a);
+  }
+  if (r) return nccl_fail("ncclCommGetAsyncError", r);
   if (a != ncclSuccess && a != ncclInProgress) return nccl_fail("asynchronous error", a);
   return VITMI_OK;
 }
@@ -251,10 +343,18 @@ extern "C" int vitmi_comm_destroy(int abort) {
   c->detached = true;
   // graceful: ncclCommDestroy must not run under an in-flight call; abort: do not wait
   if (!abort) g_idle.wait(lk, [c] { return c->users == 0; });
-  lk.unlock();
-  ncclResult_t r = abort ? g_rccl.abort(c->comm) : g_rccl.destroy(c->comm);
-  lk.lock();
-  c->released = true;
+  ncclResult_t r;
+  if (abort && c->nonblocking) {
+    // under the lock: no other thread is inside an RCCL call on this handle (they all take
+    // g_mu, and none blocks while holding it), and every later one sees `released` first
+    r = g_rccl.abort(c->comm);
+    c->released = true;
+  } else {
+    lk.unlock();
+    r = abort ? g_rccl.abort(c->comm) : g_rccl.destroy(c->comm);
+    lk.lock();
+    c->released = true;
+  }
   const bool free_it = c->users == 0;
   lk.unlock();
   if (free_it) delete c;

@@ -53,8 +53,14 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 // VITMI_BF16F8 operands (the precision knob's cheaper form): x = hi + lo, hi = bf16(x); the row
 // carries hi (bf16) and two OCP e4m3 parts, hi8 = e4m3(hi) and lo8 = e4m3(lo * 2^9), so the two
 // correction products hi.lo + lo.hi run as ONE block-scaled fp8 product (the GEMM's fp8 K-steps,
-// scale 2^-9 on the weight operand).  lo = x - hi is exact in fp32 (|lo| <= 2^-9 |x|), and the
-// fixed 2^9 keeps lo8 in e4m3's range wherever x is (tools/precision_emulate_fp8.py).
+// scale 2^-9 on the weight operand).  lo = x - hi is exact in fp32, at most half a bf16 ulp:
+// |lo| <= 2^(e-8) for 2^e <= |x| < 2^(e+1), so lo8 = lo * 2^9 <= 2^(e+1) <= 2|x|.  The fixed scales
+// bound where the corrections hold (tools/precision_emulate_fp8.py): e4m3 saturates at
+// +-448, so lo8 can clip once |x| > 224 and hi8 once |x| > 448, and past that the product falls back
+// to roughly plain-bf16 accuracy; at the small end hi8 is subnormal below |x| = 2^-6 and lo8 below
+// |lo| = 2^-15, where those terms lose relative precision (but weigh < 2^-6 of a unit operand).
+// tests/test_gpu_f8.py bounds the GEMM error inside the range (|x| up to ~200) and shows the
+// fallback to bf16 accuracy past it.
 // The e4m3 part (2K bytes after the K bf16 of hi) interleaves per 64 k: block j = [hi8 of k
 // 64j..64j+63 | lo8 of the same k] for an A operand, [lo8 | hi8] for a weight, so one 128-B GEMM
 // K-step pairs hi8.lo8 and lo8.hi8 of the same 64 k, and a producer's 64-column tile leaves as

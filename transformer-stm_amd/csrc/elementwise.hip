@@ -206,10 +206,16 @@ thread_local hipStream_t t_fold_streams[FOLD_STREAMS];
 thread_local int t_nfold_streams = 0;
 thread_local hipEvent_t t_fold_events[FOLD_STREAMS] = {};
 
-void note_fold_stream(hipStream_t s) {
+// A stream past the table's FOLD_STREAMS could not be ordered before vitmi_fold_end's stream (the
+// gradient read, or the workspace released, before that fold ran): refuse it instead.
+int note_fold_stream(hipStream_t s) {
   for (int i = 0; i < t_nfold_streams; ++i)
-    if (t_fold_streams[i] == s) return;
-  if (t_nfold_streams < FOLD_STREAMS) t_fold_streams[t_nfold_streams++] = s;
+    if (t_fold_streams[i] == s) return VITMI_OK;
+  if (t_nfold_streams == FOLD_STREAMS)
+    return fail(VITMI_ERR_UNSUPPORTED, "fold: more than %d streams ran deferred folds between vitmi_fold_begin "
+                "and vitmi_fold_end", FOLD_STREAMS);
+  t_fold_streams[t_nfold_streams++] = s;
+  return VITMI_OK;
 }
 
 int launch_folds(const FoldBatch& b, int n, hipStream_t s) {
@@ -230,7 +236,8 @@ int launch_folds(const FoldBatch& b, int n, hipStream_t s) {
 int flush_folds() {
   const int n = t_njobs;
   t_njobs = 0;
-  if (n > 0) note_fold_stream(t_stream);
+  if (n > 0)
+    if (int rc = note_fold_stream(t_stream)) return rc;
   return launch_folds(t_batch, n, t_stream);
 }
 }  // namespace

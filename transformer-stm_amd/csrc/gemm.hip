@@ -273,7 +273,11 @@ __device__ __forceinline__ f32x4 mma8(const Frag<bf16>& a0, const Frag<bf16>& a1
                                                                     12, 13, 14, 15));
   const i32x8 b = __builtin_bit_cast(i32x8, __builtin_shufflevector(b0.v, b1.v, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11,
                                                                     12, 13, 14, 15));
+#ifdef VITMI_F6_TIMING   // DIAGNOSTIC: the same bytes read as e2m3 (MX FP6 rate); results meaningless
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 2, 2, 0, F8_E8M0_LO, 0, F8_E8M0_ONE);
+#else
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, F8_E8M0_LO, 0, F8_E8M0_ONE);
+#endif
 }
 __device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b, f32x4 c) {
 #pragma unroll

@@ -46,10 +46,11 @@ REDUCE_SUM, REDUCE_AVG = 0, 1
 class VitmiComm:
     """The library's RCCL communicator (one per process, bound to the current HIP device).
 
-    No lock is held across a library call: the CommWatchdog thread's abort must be able to run
-    while the training thread is blocked inside an all-reduce enqueue (a dead peer), which the
-    abort then releases with an error.  The library reference-counts the communicator, so an
-    abort never frees it under a call in flight (csrc/comm.cpp).  ``self._lock`` only makes
+    No Python lock is held across a library call: the CommWatchdog thread's abort must be able to
+    run while the training thread waits inside an all-reduce (a dead peer), which the abort then
+    ends with an error.  The library creates the communicator non-blocking, so its RCCL calls never
+    wait on a peer and run serialised with the abort under the library's own lock; a wait is a poll
+    that stops once the communicator is released (csrc/comm.cpp).  ``self._lock`` only makes
     ``destroy`` happen once."""
 
     def __init__(self, rank: int, world: int, uid: bytes):
@@ -590,7 +591,11 @@ def comm_or_fallback(rank: int, world: int, make_group=None):
     """The library's RCCL communicator for the job, or -- when creating it fails on ANY rank (the
     ranks agree over the default, bootstrap process group) -- a torch.distributed process group
     from ``make_group`` (default: a new ``nccl`` group, i.e. torch's RCCL) for the same exchange.
-    Returns (comm or None, group or None, this rank's error text or None)."""
+    Returns (comm or None, group or None, this rank's error text or None).  The library's init is
+    non-blocking and bounded (VITMI_COMM_INIT_TIMEOUT_S, default 600 s; csrc/comm.cpp): a rank
+    whose peer failed inside the collective init times out there and reaches the agreement below
+    instead of blocking for ever; a communicator that did come up is aborted, not destroyed
+    gracefully (its peers may be gone)."""
     err = None
     comm = None
     try:
@@ -602,7 +607,7 @@ def comm_or_fallback(rank: int, world: int, make_group=None):
     if ok.item() == 1:
         return comm, None, None
     if comm is not None:
-        comm.destroy()
+        comm.destroy(abort=True)
     group = make_group() if make_group is not None else dist.new_group(backend="nccl")
     return None, group, err
 
