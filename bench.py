@@ -322,6 +322,9 @@ def main():
     ap.add_argument("--no-optimizer", action="store_true", help="diagnostic only: skip Adam")
     ap.add_argument("--optimizer", choices=["vitmi", "torch"], default="vitmi",
                     help="vitmi: Keras Adam, one fused launch over the arena (+ bf16 shadow); torch: fused torch Adam")
+    ap.add_argument("--attn-policy", type=int, default=0,
+                    help="diagnostic: vitmi_attention_set_policy (0 auto: single-pass backward for N <= 224; "
+                         "3: the two-kernel backward)")
     ap.add_argument("--stats-out", default=None, help=argparse.SUPPRESS)   # evidence child: work table
     ap.add_argument("--roctx", action="store_true", help="ROCTx ranges around the step's phases (vitmi.trace)")
     ap.add_argument("--no-secondary", action="store_true",
@@ -344,6 +347,8 @@ def main():
     dev = torch.device("cuda", gpu)
     if args.roctx:
         trace.enable()
+    if args.attn_policy:
+        ops.attention_set_policy(args.attn_policy)
     cfg = {"c2": config_c2, "c3": config_c3, "c5": config_c5}[args.config]()
     if args.dtype is not None:
         cfg = cfg.replace(dtype=args.dtype)

@@ -184,7 +184,10 @@ def test_asm_load_scanner_catches_both_hazards():
     assert len(bad) == 2 and "v11" in bad[0][1] and "M0" in bad[1][1]
 
 
-def test_dkv_kernels_asm_loads_and_m0(tmp_path):
+@pytest.mark.parametrize("kern", ["attn_bwd_dkv_seq_bf16", "attn_bwd_fused_seq_bf16"])
+def test_dkv_kernels_asm_loads_and_m0(tmp_path, kern):
+    """The persistent dK/dV kernels and the persistent single-pass backward (round 6: the next
+    pair's Q | dO by dma_piece, its K / V / O rows and lse by asm_load16 / asm_load4)."""
     if not (os.path.exists(OBJDUMP) and os.path.exists(LIB)):
         pytest.skip("needs llvm-objdump and the built library")
     lib = tmp_path / "libvitmi.so"
@@ -195,9 +198,9 @@ def test_dkv_kernels_asm_loads_and_m0(tmp_path):
     for f in objs:
         asm = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", f], check=True, capture_output=True,
                              text=True, timeout=300).stdout
-        if "attn_bwd_dkv_seq_bf16" not in asm:
+        if kern not in asm:
             continue
         seen += 1
-        bad += scan_asm_loads(asm.splitlines(), lambda k: "attn_bwd_dkv_seq_bf16" in k)
-    assert seen, "no code object holds the dK/dV kernels"
+        bad += scan_asm_loads(asm.splitlines(), lambda k: kern in k)
+    assert seen, f"no code object holds {kern}"
     assert not bad, "\n".join(f"{k[:50]}: {p}" for k, p in bad[:20])

@@ -1,5 +1,6 @@
-"""Time the bf16 attention kernels at the ViT-B/16 bs=256 shape, whole-sequence path vs the
-streamed path (attention policy 1).  usage: python tools/attn_bench.py [B] [N] [H]"""
+"""Time the bf16 attention kernels at the ViT-B/16 bs=256 shape: the whole-sequence path (its
+single-pass backward, policy 0; its two-kernel backward, policy 3) vs the streamed path (policy 1).
+usage: python tools/attn_bench.py [B] [N] [H]"""
 import os
 import sys
 
@@ -30,7 +31,7 @@ def main():
     qkv = (torch.randn(B * N, 3 * D, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
     do = torch.randn(B * N, D, device="cuda", generator=g).to(torch.bfloat16)
     pairs = B * H * N * N
-    for path, pol in (("seq", 0), ("stream", 1)):
+    for path, pol in (("seq", 0), ("seq2k", 3), ("stream", 1)):
         ops.attention_set_policy(pol)
         o, lse = ops.attention_fwd(qkv, B, N, H, 0.125)
         tf = t(lambda: ops.attention_fwd(qkv, B, N, H, 0.125))

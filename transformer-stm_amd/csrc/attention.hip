@@ -1412,6 +1412,275 @@ __global__ __launch_bounds__(NPMAX * 2) void attn_bwd_dkv_seq_bf16(
   }
 }
 
+// ============================================== single-pass backward (bf16, N <= 32 * 7 = 224)
+// dQ, dK and dV of one (batch, head) in ONE workgroup that loads Q, K, V, dO and O once (the
+// two-kernel path above loads them twice: the dQ kernel's K / V and Q / dO loads were half of its
+// time).  NKB = ceil(N / 32) waves; wave w owns key block w.
+//   prologue  Q and dO images into LDS (LDS-DMA), the wave's K / V rows into registers, delta =
+//             rowsum(dO * O) of the wave's 32 query rows (as the dQ kernel forms it) and lse into
+//             LDS row tables.
+//   phase 1   per query block: S, P, dP - delta and dS = P (dP - delta) with the keys on the lanes
+//             (the dK/dV kernel's arithmetic, in the same order: dK and dV are bitwise its), dV +=
+//             dO^T P and dK += Q^T dS in registers, and dS^T (bf16, the value dK takes) into an LDS
+//             tile [key block][query block] of [32 keys][32 queries].
+//   phase 2   the K rows go from registers into the (now free) Q image; wave w takes query block w:
+//             dQ = dS K over all key blocks from the dS^T tiles (transposed reads) and the K image.
+//   epilogue  dQ, dK, dV leave through per-wave LDS images as whole lines (store_tile32), with the
+//             q/k/v bias-gradient column sums as the two-kernel path forms them.
+// LDS: Q + dO images 2 x 28 KiB, dS^T tiles NKB^2 x 2 KiB (98 KiB at NKB = 7), row tables: one
+// workgroup per CU, as the persistent dK/dV kernel.  No atomics; fixed summation orders.
+// dS^T tile: 64-B rows (32 queries), 16-B chunk c of row r at c ^ ((r >> 2) & 3): the phase-2
+// ds_read_b64_tr_b16 reads are conflict free, the phase-1 8-B writes 2-way.
+__device__ __forceinline__ int ds_off(int row, int ch) { return row * 64 + ((ch ^ ((row >> 2) & 3)) << 4); }
+// frag_tr over a [32][32] tile of 64-B rows: operand X^T[col][k] of the tile X[k][col], element j
+// <-> k-row k0 + 8(j>>2) + 4h + (j&3), col = lane & 31 (frag_tr's k order, c0 = 0)
+__device__ __forceinline__ bf16x8 frag_tr32(const char* t, int k0, int lane) {
+  const int g = lane >> 4, tl = lane & 15, q = tl >> 2, p = tl & 3;
+  bf16x8 f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = k0 + 8 * i + 4 * (g >> 1) + q;
+    s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(s16x4, t + ds_off(row, 2 * (g & 1) + (p >> 1)) + ((p & 1) << 3)));
+    bf16x4 b = __builtin_bit_cast(bf16x4, v);
+    f[4 * i + 0] = b[0];
+    f[4 * i + 1] = b[1];
+    f[4 * i + 2] = b[2];
+    f[4 * i + 3] = b[3];
+  }
+  return f;
+}
+
+template <int NKB>
+__global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int N, int H,
+    float scale, float* __restrict__ colsum, int npairs) {
+  constexpr int NP = NKB * 32;
+  constexpr int IMG = NP * 128;     // one [NP][64] bf16 image
+  constexpr int DT = 32 * 64;       // one dS^T tile [32 keys][32 queries] bf16
+  // the dS^T tiles, and in the epilogue the waves' three output images
+  constexpr int AREA = NKB * NKB * DT > 3 * NKB * ST_BYTES ? NKB * NKB * DT : 3 * NKB * ST_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + AREA];
+  // phase 1: the lse / delta row tables; epilogue: the column-sum partials [3][NKB][64]
+  __shared__ __attribute__((aligned(16))) float tab[3 * NKB * 64];
+  float* l2s = tab;
+  float* dls = tab + NP;
+  float (*red)[NKB][64] = reinterpret_cast<float (*)[NKB][64]>(tab);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int D = H * DH;
+  const int64_t ld = 3 * (int64_t)D, ldb = ld * 2, ldo = (int64_t)D * 2;
+  const int h = lane >> 5;
+  const uint32_t bytes = (uint32_t)((int64_t)N * ldb);
+  const uint32_t obytes = (uint32_t)((int64_t)N * ldo);
+  char* qt = smem;                 // Q image; phase 2: the K image
+  char* dt_ = smem + IMG;          // dO image
+  char* dst = smem + 2 * IMG;      // dS^T tiles [key block][query block]; epilogue: output images
+  const int r32 = wave * 32 + (lane & 31);   // this lane's key (phase 1) and query (delta, phase 2)
+  const int kl = lane & 31;
+  const float c2 = scale * LOG2E;
+  // (batch, head) pairs in DESCENDING order (the out-proj dgrad writing dO finished with the last
+  // rows); pair i of this workgroup's walk is blockIdx.x + i * gridDim.x
+  auto pair_of = [&](int i) { return npairs - 1 - i; };
+  // Loads of a pair.  Q and dO images by inline-asm LDS-DMA (dma_piece) and the K / V / O rows and
+  // lse into registers by inline-asm loads: with compiler-visible loads hipcc drains the prefetch
+  // with vmcnt(0) at the first LDS access it cannot prove disjoint (attn_bwd_dkv_seq_bf16's note);
+  // the kernel's own counted waits retire them.  Rows past N come back zero (range check).
+  auto stage_q = [&](int bh) {
+    const int b = bh / H, hd = bh - b * H;
+    stage_seq_dma(qt, make_rsrc(qkv + (int64_t)b * N * ld + hd * DH, bytes - hd * DH * 2), ldb, NP, NKB, wave, lane);
+  };
+  auto stage_do = [&](int bh) {
+    const int b = bh / H, hd = bh - b * H;
+    stage_seq_dma(dt_, make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2), ldo, NP, NKB, wave, lane);
+  };
+  auto load_regs = [&](int bh, bf16x8 (&kf)[4], bf16x8 (&vf)[4], bf16x8 (&of)[4], float& ls) {
+    const int b = bh / H, hd = bh - b * H;
+    const bf16* base = qkv + (int64_t)b * N * ld;
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+    const uint32_t kvoff = (uint32_t)((int64_t)r32 * ldb + 16 * h), ooff = (uint32_t)((int64_t)r32 * ldo + 16 * h);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = __builtin_bit_cast(bf16x8, asm_load16(rk, kvoff, 32 * s));
+      vf[s] = __builtin_bit_cast(bf16x8, asm_load16(rv, kvoff, 32 * s));
+      of[s] = __builtin_bit_cast(bf16x8, asm_load16(ro, ooff, 32 * s));
+    }
+    ls = asm_load4(make_rsrc(lse + (int64_t)bh * N, (uint32_t)N * 4), (uint32_t)r32 * 4);
+  };
+
+  int i = blockIdx.x;
+  if (i >= npairs) return;
+  int bh = pair_of(i);
+  bf16x8 kf[4], vf[4], of[4];
+  float ls;
+  stage_q(bh);
+  stage_do(bh);
+  load_regs(bh, kf, vf, of, ls);
+  bool first = true;
+  for (;;) {
+    // everything this pair needs has landed: all but the youngest 12 vector-memory ops, which are
+    // the previous pair's output stores (12 per wave; the column-sum stores after them, 0..3 per
+    // wave, only make this wait stricter)
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    first = false;
+    asm volatile("" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(vf[0]), "+v"(vf[1]), "+v"(vf[2]),
+                 "+v"(vf[3]), "+v"(of[0]), "+v"(of[1]), "+v"(of[2]), "+v"(of[3]), "+v"(ls));
+    __syncthreads();   // every wave's Q | dO pieces landed; the previous epilogue is done with tab
+    const int b = bh / H, hd = bh - b * H;
+    {
+      // delta of query row r32 from the dO image and the O row, summed as attn_bwd_dq_seq_bf16
+      // does (bitwise the same value)
+      float part = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 df = *(const bf16x8*)(dt_ + toff(r32, 2 * s + h));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)of[s][j] * (float)df[j];
+      }
+      const float dl = part + __shfl_xor(part, 32, 64);
+      const bool ok = r32 < N;
+      if (h == 0) {
+        l2s[r32] = ok ? ls * LOG2E : INFINITY;   // queries >= N: P = 0
+        dls[r32] = ok ? dl : 0.f;
+        if (ok) delta[(int64_t)bh * N + r32] = dl;
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 1: keys on the lanes (the dK/dV kernel's qblock, plus the dS^T tile)
+    f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int qb = 0; qb < NKB; ++qb) {
+      const int q0 = 32 * qb;
+      f32x16 sa = zero16(), dp;
+      f32x4 L2[4];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int q4 = q0 + 8 * g4 + 4 * h;
+        L2[g4] = *(const f32x4*)(l2s + q4);
+        const f32x4 dl = *(const f32x4*)(dls + q4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dp[4 * g4 + e] = -dl[e];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sa = mfma32(frag_row(qt, q0, s, lane), kf[s], sa);    // S[q][key]
+        dp = mfma32(frag_row(dt_, q0, s, lane), vf[s], dp);   // dP[q][key] - delta[q]
+      }
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = fexp2(fmaf(sa[4 * g4 + e], c2, -L2[g4][e]));
+          sa[4 * g4 + e] = p;
+          dp[4 * g4 + e] = p * dp[4 * g4 + e];
+        }
+      char* tile = dst + (wave * NKB + qb) * DT;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8(sa, s), sb = pack8(dp, s);
+#pragma unroll
+        for (int d2 = 0; d2 < 2; ++d2) {
+          dvt[d2] = mfma32(frag_tr(dt_, q0 + 16 * s, 32 * d2, lane), pb, dvt[d2]);
+          dkt[d2] = mfma32(frag_tr(qt, q0 + 16 * s, 32 * d2, lane), sb, dkt[d2]);
+        }
+        // dS^T[key][q]: elements 0..3 are queries 16s + 4h + 0..3 (chunk 2s), 4..7 are 16s + 8 +
+        // 4h + 0..3 (chunk 2s + 1), half h of each chunk
+        bf16x4 lo4, hi4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          lo4[j] = sb[j];
+          hi4[j] = sb[4 + j];
+        }
+        *(bf16x4*)(tile + ds_off(kl, 2 * s) + 8 * h) = lo4;
+        *(bf16x4*)(tile + ds_off(kl, 2 * s + 1) + 8 * h) = hi4;
+      }
+    }
+    __syncthreads();   // every wave is done with the Q and dO images and wrote its dS^T tiles
+    // the K image where Q was: row r32 = this lane's key, chunk 2s + h holds d = 16s + 8h .. +7
+#pragma unroll
+    for (int s = 0; s < 4; ++s) *(bf16x8*)(qt + toff(r32, 2 * s + h)) = kf[s];
+    const int inext = i + gridDim.x;
+    const bool more = inext < npairs;
+    const int nbh = more ? pair_of(inext) : 0;
+    // the next pair's dO image (the dO image is free) and register rows (kf / vf / of are dead)
+    // land under phase 2 and the epilogue
+    if (more) {
+      stage_do(nbh);
+      load_regs(nbh, kf, vf, of, ls);
+    }
+    __syncthreads();
+
+    // ---- phase 2: wave w takes query block w: dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q]
+    f32x16 dqt[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      const char* tile = dst + (kb * NKB + wave) * DT;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 sf = frag_tr32(tile, 16 * s, lane);
+#pragma unroll
+        for (int d2 = 0; d2 < 2; ++d2) dqt[d2] = mfma32(frag_tr(qt, 32 * kb + 16 * s, 32 * d2, lane), sf, dqt[d2]);
+      }
+    }
+    __syncthreads();   // the K image is free (the next Q lands there); dS^T area -> output images
+    if (more) stage_q(nbh);
+
+    // ---- epilogue: dQ, dK, dV through three images per wave, then their column sums (the q/k/v
+    // bias-gradient partials of this batch row) in one pass, folded in wave order
+    {
+      const bf16* dbase = dqkv + (int64_t)b * N * ld;
+      const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dbase + hd * DH, bytes - hd * DH * 2);
+      const __amdgpu_buffer_rsrc_t rdk = make_rsrc(dbase + D + hd * DH, bytes - (D + hd * DH) * 2);
+      const __amdgpu_buffer_rsrc_t rdv = make_rsrc(dbase + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+      char* scr = dst + 3 * wave * ST_BYTES;
+      const int ln = lane_here();
+      store_tile32(scr, dqt, scale, rdq, ldb, wave * 32, ln);
+      store_tile32(scr + ST_BYTES, dkt, scale, rdk, ldb, wave * 32, ln);
+      store_tile32(scr + 2 * ST_BYTES, dvt, 1.f, rdv, ldb, wave * 32, ln);
+      if (colsum) {
+        // tile32_colsum's sums per image (rows < N, 4 rows x 8 columns per lane, xor folds)
+        const int rr = ln >> 3, cc = ln & 7, row0 = wave * 32;
+#pragma unroll
+        for (int im = 0; im < 3; ++im) {
+          float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (row0 + 8 * j + rr < N) {
+              const bf16x8 v = *(const bf16x8*)(scr + im * ST_BYTES + (8 * j + rr) * ST_PITCH + cc * 16);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) cs[e] += (float)v[e];
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            cs[e] += __shfl_xor(cs[e], 8, 64);
+            cs[e] += __shfl_xor(cs[e], 16, 64);
+            cs[e] += __shfl_xor(cs[e], 32, 64);
+          }
+          if (ln < 8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red[im][wave][ln * 8 + e] = cs[e];
+          }
+        }
+        __syncthreads();
+        for (int x = threadIdx.x; x < 192; x += NKB * 64) {   // (fewer than 3 waves: several each)
+          const int im = x >> 6, c = x & 63;
+          float t = 0.f;
+          for (int w = 0; w < NKB; ++w) t += red[im][w][c];
+          colsum[(int64_t)b * 3 * D + im * D + hd * DH + c] = t;
+        }
+      }
+    }
+    if (!more) break;
+    i = inext;
+    bh = nbh;
+  }
+}
 
 // =============================================================== fp32 path (MFMA, N <= NPMAX)
 // The fp32 parity configuration on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: full fp32
@@ -1889,7 +2158,9 @@ using namespace vitmi;
 // whole-sequence kernels for N <= SEQ_MAX (8 waves, 2 workgroups of <= 64 KiB LDS per CU).
 // Kernel policy (vitmi_attention_set_policy; tests): 0 = auto, 1 = always the streamed kernels,
 // 2 = the whole-sequence 32-query-per-wave forward / dQ (attn_fwd_seq_bf16 / attn_bwd_dq_seq_bf16)
-// where auto takes their 64-query forms (bitwise equal by construction; the tests compare them).
+// where auto takes their 64-query forms (bitwise equal by construction; the tests compare them),
+// and the two-kernel backward; 3 = auto's forward with the two-kernel backward (64-query dQ, then
+// dK/dV) where auto runs the single-pass attn_bwd_fused_seq_bf16 (N <= 224).
 static constexpr int SEQ_MAX = 256;
 
 static int device_cus() {   // compute units of the current device (the persistent dK/dV grid)
@@ -1907,9 +2178,28 @@ static int device_cus() {   // compute units of the current device (the persiste
 static int g_attn_policy = 0;
 static bool seq_path(int N) { return N <= SEQ_MAX && g_attn_policy != 1; }
 static bool q64() { return VITMI_ATTN_Q64 && g_attn_policy != 2; }
+#ifndef VITMI_ATTN_FUSED_BWD
+#define VITMI_ATTN_FUSED_BWD 1
+#endif
+static constexpr int FUSED_NKB = 7;   // the single-pass backward's LDS holds NKB^2 dS^T tiles: N <= 224
+static bool fused_bwd(int N) { return VITMI_ATTN_FUSED_BWD && g_attn_policy == 0 && (N + 31) / 32 <= FUSED_NKB; }
+
+template <int NKB>
+static void launch_fused(int B, int N, int H, float scale, const void* qkv, const void* o, const void* dout,
+                         const float* lse, float* delta, void* dqkv, float* colsum, hipStream_t s) {
+  // persistent: one workgroup per CU (its LDS), each walking the (batch, head) pairs
+  const int npairs = B * H, cus = device_cus();
+  hipLaunchKernelGGL(attn_bwd_fused_seq_bf16<NKB>, dim3(npairs < cus ? npairs : cus), dim3(64 * NKB), 0, s,
+                     (const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, delta, (bf16*)dqkv, N, H, scale,
+                     colsum, npairs);
+  // algorithmic backward = dP, dQ, dV, dK: 8 N^2 dh flops per head (recomputing S is not counted);
+  // bytes: q/k/v/o/dO read and dq/dk/dv written once, lse read and delta written
+  const double bh = (double)B * H, t = bh * N * DH;
+  VITMI_STAT(attn_bwd_fused_seq_bf16<NKB>, 8.0 * bh * N * N * DH, t * 8 * 2 + bh * N * 8);
+}
 
 extern "C" int vitmi_attention_set_policy(int policy) {
-  VITMI_CHECK_ARG(policy >= 0 && policy <= 2, "attention_set_policy: policy must be 0, 1 or 2");
+  VITMI_CHECK_ARG(policy >= 0 && policy <= 3, "attention_set_policy: policy must be 0..3");
   const int prev = g_attn_policy;
   g_attn_policy = policy;
   return prev;
@@ -2011,7 +2301,18 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
   float* delta = (float*)workspace;
   const int64_t rows = (int64_t)B * N * H;
   const int blocks = (int)((rows + 255) / 256);
-  if (dtype == VITMI_BF16 && seq_path(N)) {
+  if (dtype == VITMI_BF16 && seq_path(N) && fused_bwd(N)) {
+    switch ((N + 31) / 32) {
+      case 1: launch_fused<1>(B, N, H, scale, qkv, o, dout, lse, delta, dqkv, colsum, s); break;
+      case 2: launch_fused<2>(B, N, H, scale, qkv, o, dout, lse, delta, dqkv, colsum, s); break;
+      case 3: launch_fused<3>(B, N, H, scale, qkv, o, dout, lse, delta, dqkv, colsum, s); break;
+      case 4: launch_fused<4>(B, N, H, scale, qkv, o, dout, lse, delta, dqkv, colsum, s); break;
+      case 5: launch_fused<5>(B, N, H, scale, qkv, o, dout, lse, delta, dqkv, colsum, s); break;
+      case 6: launch_fused<6>(B, N, H, scale, qkv, o, dout, lse, delta, dqkv, colsum, s); break;
+      default: launch_fused<7>(B, N, H, scale, qkv, o, dout, lse, delta, dqkv, colsum, s); break;
+    }
+    if (colsum_rows) *colsum_rows = colsum ? B : 0;   // one partial row per batch
+  } else if (dtype == VITMI_BF16 && seq_path(N)) {
     // dQ first: it also writes delta, which the dK/dV kernel consumes
     const dim3 block(64 * ((N + 31) / 32));
     {
@@ -2066,7 +2367,9 @@ static int attention_bwd_impl(int dtype, int B, int N, int H, int dh, float scal
     // (recomputing S is not counted); bytes: q/k/v/o/dO read, dq/dk/dv written, lse/delta
     const double es = dtype == VITMI_BF16 ? 2 : 4, bh = (double)B * H, t = bh * N * DH;
     const double fl = 4.0 * bh * N * N * DH;
-    if (dtype == VITMI_BF16 && seq_path(N)) {
+    if (dtype == VITMI_BF16 && seq_path(N) && fused_bwd(N)) {
+      // (launch_fused records its own)
+    } else if (dtype == VITMI_BF16 && seq_path(N)) {
       if ((N + 31) / 32 == 7) {
         if (q64()) VITMI_STAT((attn_bwd_dq_seq64_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
         else VITMI_STAT((attn_bwd_dq_seq_bf16<SEQ_MAX, 7>), fl, t * 6 * es + bh * N * 8);
