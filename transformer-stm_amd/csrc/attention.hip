@@ -694,8 +694,22 @@ __device__ unsigned long long* d_attn_stamps;
       }                                                                                              \
     }                                                                                                \
   } while (0)
+// the single-pass backward: [2][pair][8] = pair start (its loads landed), phase 1 start, phase 1
+// done, phase 2 done, epilogue done; HW_ID, XCC_ID in [6], [7]
+#define FUSED_STAMP(pair, k)                                                                         \
+  do {                                                                                               \
+    if (d_attn_stamps && threadIdx.x == 0) {                                                         \
+      unsigned long long* p_ = d_attn_stamps + ((int64_t)2 * 65536 + (pair)) * 8;                     \
+      p_[k] = __builtin_amdgcn_s_memrealtime();                                                      \
+      if ((k) == 0) {                                                                                \
+        p_[6] = __builtin_amdgcn_s_getreg(4 | (31 << 11));                                           \
+        p_[7] = __builtin_amdgcn_s_getreg(20 | (15 << 11));                                          \
+      }                                                                                              \
+    }                                                                                                \
+  } while (0)
 #else
 #define ATTN_STAMP(kern, k) do {} while (0)
+#define FUSED_STAMP(pair, k) do {} while (0)
 #endif
 
 // stage_seq with the pieces issued by dma_piece (no compiler-visible LDS-DMA; see there)
@@ -1530,6 +1544,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
     asm volatile("" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(vf[0]), "+v"(vf[1]), "+v"(vf[2]),
                  "+v"(vf[3]), "+v"(of[0]), "+v"(of[1]), "+v"(of[2]), "+v"(of[3]), "+v"(ls));
     __syncthreads();   // every wave's Q | dO pieces landed; the previous epilogue is done with tab
+    FUSED_STAMP(bh, 0);
     const int b = bh / H, hd = bh - b * H;
     {
       // delta of query row r32 from the dO image and the O row, summed as attn_bwd_dq_seq_bf16
@@ -1550,6 +1565,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
       }
     }
     __syncthreads();
+    FUSED_STAMP(bh, 1);
 
     // ---- phase 1: keys on the lanes (the dK/dV kernel's qblock, plus the dS^T tile)
     f32x16 dvt[2] = {zero16(), zero16()}, dkt[2] = {zero16(), zero16()};
@@ -1601,6 +1617,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
       }
     }
     __syncthreads();   // every wave is done with the Q and dO images and wrote its dS^T tiles
+    FUSED_STAMP(bh, 2);
     // the K image where Q was: row r32 = this lane's key, chunk 2s + h holds d = 16s + 8h .. +7
 #pragma unroll
     for (int s = 0; s < 4; ++s) *(bf16x8*)(qt + toff(r32, 2 * s + h)) = kf[s];
@@ -1609,10 +1626,14 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
     const int nbh = more ? pair_of(inext) : 0;
     // the next pair's dO image (the dO image is free) and register rows (kf / vf / of are dead)
     // land under phase 2 and the epilogue
-    if (more) {
+#ifndef VITMI_FUSED_PF
+#define VITMI_FUSED_PF 1
+#endif
+    if (more && VITMI_FUSED_PF == 1) {
       stage_do(nbh);
       load_regs(nbh, kf, vf, of, ls);
     }
+    if (more && VITMI_FUSED_PF == 2) load_regs(nbh, kf, vf, of, ls);
     __syncthreads();
 
     // ---- phase 2: wave w takes query block w: dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q]
@@ -1628,7 +1649,13 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
       }
     }
     __syncthreads();   // the K image is free (the next Q lands there); dS^T area -> output images
+    FUSED_STAMP(bh, 3);
     if (more) stage_q(nbh);
+    if (more && VITMI_FUSED_PF == 0) {
+      stage_do(nbh);
+      load_regs(nbh, kf, vf, of, ls);
+    }
+    if (more && VITMI_FUSED_PF == 2) stage_do(nbh);
 
     // ---- epilogue: dQ, dK, dV through three images per wave, then their column sums (the q/k/v
     // bias-gradient partials of this batch row) in one pass, folded in wave order
@@ -1676,6 +1703,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
         }
       }
     }
+    FUSED_STAMP(bh, 4);
     if (!more) break;
     i = inext;
     bh = nbh;
