@@ -198,13 +198,15 @@ int vitmi_attention_bwd(int dtype, int B, int N, int H, int dh, float scale, con
                         const void* o, const void* dout, const float* lse, void* dqkv,
                         void* workspace, size_t ws_bytes, vitmi_stream_t stream);
 size_t vitmi_attention_bwd_workspace_size(int B, int N, int H);
-/* Kernel selection (process-wide; tests): 0 = auto, 1 = always the streamed (64-key LDS-tiled)
- * kernels, 2 = the whole-sequence kernels' 32-query-per-wave forward and dQ forms (auto runs their
- * 64-query forms, bitwise equal).  Returns the previous policy. */
+/* Kernel selection (process-wide; tests): 0 = auto (bf16, N <= 224: the single-pass backward, dQ,
+ * dK and dV in one persistent kernel), 1 = always the streamed (64-key LDS-tiled) kernels, 2 = the
+ * whole-sequence kernels' 32-query-per-wave forward and dQ forms and the two-kernel backward (auto
+ * runs their 64-query forms, bitwise equal), 3 = auto's forward with the two-kernel backward
+ * (64-query dQ, then dK/dV).  Returns the previous policy. */
 int vitmi_attention_set_policy(int policy);
 /* vitmi_attention_bwd plus the qkv bias gradient: dbias[3*H*dh] += column sums of dqkv (the
  * q/k/v Dense biases, models/CvT(Par).py:132-134).  On the bf16 paths the sums come from the
- * dQ and dK/dV kernels' output images (per (batch, head) block on the whole-sequence path,
+ * backward kernels' output images (per (batch, head) block on the whole-sequence path,
  * N <= 256, per (batch, head, 128-row block) on the streamed one, then a fixed-order fold); the
  * fp32 paths take a second pass over dqkv. */
 size_t vitmi_attention_bwd_bias_workspace_size(int B, int N, int H);

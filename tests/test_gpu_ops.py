@@ -431,6 +431,25 @@ def test_attention_64query_forms_bitwise_equal(B, N, H):
         assert torch.equal(a, b), name
 
 
+@pytest.mark.parametrize("B,N,H", [(16, 197, 12), (3, 250, 2), (2, 33, 1)])
+def test_attention_fwd_knob_outputs_64query_bitwise_equal(B, N, H):
+    """The precision knobs' attention forward (vitmi_attention_fwd_x3 / _f8) in its 64-query form
+    (auto policy, round 6) against the 32-query form (policy 2): o, lse and the split outputs o3 /
+    o8 are bitwise equal (the same per-query-block arithmetic and the same fp32 O)."""
+    D = 64 * H
+    qkv = rnd(B * N, 3 * D, dtype=BF, seed=71).to(DEV)
+    out = {}
+    prev = ops.attention_set_policy(0)
+    try:
+        for pol in (0, 2):
+            ops.attention_set_policy(pol)
+            out[pol] = ops.attention_fwd_x3(qkv, B, N, H, 0.125) + ops.attention_fwd_f8(qkv, B, N, H, 0.125)
+    finally:
+        ops.attention_set_policy(prev)
+    for a, b, name in zip(out[0], out[2], ("o", "o3", "lse", "o (f8)", "o8", "lse (f8)")):
+        assert torch.equal(a, b), name
+
+
 @pytest.mark.parametrize("B,N,H", [(48, 197, 12), (3, 224, 2), (2, 193, 1), (5, 64, 3), (2, 17, 3), (1, 1, 2),
                                    (3, 100, 2)])
 def test_attention_single_pass_bwd_vs_two_kernel(B, N, H):

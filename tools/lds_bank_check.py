@@ -80,6 +80,30 @@ def main():
     for R in (128, 256):
         w = max(cost(mnmajor_f32(R, r0, 0, j), HALVES, 4, 32) for r0 in range(0, R, 16) for j in range(8))
         print(f"m/n-major f32 ds_read_b32 R={R} worst:", w)
+    # the single-pass attention backward's dS^T tiles (csrc/attention.hip ds_off: [32 keys][32
+    # queries] bf16, 64-B rows, 16-B chunk c of row r at c ^ ((r >> 2) & 3))
+    w = max(cost(ds_tr32(k0, i), HALVES, 8) for k0 in (0, 16) for i in (0, 1))
+    print("attention dS^T tile ds_read_b64_tr_b16 (phase 2) worst:", w)
+    w = max(cost(ds_write(s_, hi), HALVES, 8) for s_ in (0, 1) for hi in (0, 1))
+    print("attention dS^T tile ds_write_b64 (phase 1) worst:", w)
+
+
+def ds_off(row, ch):
+    return row * 64 + ((ch ^ ((row >> 2) & 3)) << 4)
+
+
+def ds_tr32(k0, i):
+    out = []
+    for lane in range(64):
+        g, tl = lane >> 4, lane & 15
+        q, p = tl >> 2, tl & 3
+        out.append(ds_off(k0 + 8 * i + 4 * (g >> 1) + q, 2 * (g & 1) + (p >> 1)) + ((p & 1) << 3))
+    return out
+
+
+def ds_write(s_, hi):
+    # lane (key = lane & 31, h = lane >> 5) writes 8 B: chunk 2s (+1 for elements 4..7), half h
+    return [ds_off(lane & 31, 2 * s_ + hi) + 8 * (lane >> 5) for lane in range(64)]
 
 
 if __name__ == "__main__":

@@ -875,9 +875,12 @@ __global__ __launch_bounds__(NPMAX * 2, 4) void attn_fwd_seq_bf16(const bf16* __
 // carries two independent softmax chains.  Per query block the arithmetic is attn_fwd_seq_bf16's,
 // in the same order (bitwise equal outputs); 213 VGPRs, two workgroups per CU.  C3: 79.4-80.6 µs
 // against 82.7-83.6 for the 7 x 32-query form (profiles/r05_q64/).  grid B*H, block 256.
-template <int NPMAX>
+// XM (the precision knobs, as attn_fwd_seq_bf16's): 1 also writes o3 = [hi | hi | lo] rows of the
+// fp32 O, 2 the VITMI_BF16F8 rows [hi | hi8 | lo8]; o and lse are the XM = 0 kernel's bit for bit.
+template <int NPMAX, int XM = 0>
 __global__ __launch_bounds__(256, 2) void attn_fwd_seq64_bf16(const bf16* __restrict__ qkv, bf16* __restrict__ o,
-                                                          float* __restrict__ lse, int N, int H, float scale) {
+                                                          float* __restrict__ lse, int N, int H, float scale,
+                                                          bf16* __restrict__ o3 = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[2 * NPMAX * 128];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1001,7 +1004,38 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_seq64_bf16(const bf16* __rest
     __syncthreads();   // O through the (now free) K/V image
     const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, (uint32_t)((int64_t)N * ldo - hd * DH * 2));
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) store_tile32(smem + wave * ST_BYTES, oacc[qb], inv[qb], ro, ldo, q0 + 32 * qb, lane_here());
+    for (int qb = 0; qb < QB; ++qb) {
+      char* scr = smem + wave * ST_BYTES;
+      const int row0 = q0 + 32 * qb;
+      store_tile32(scr, oacc[qb], inv[qb], ro, ldo, row0, lane_here());
+      if constexpr (XM == 2) {
+        // hi (bf16) at columns [0, D) of the 2D-wide row, the head's e4m3 block [hi8 | lo8] at byte
+        // 2D + 128 hd (attn_fwd_seq_bf16<.., 2>'s layout)
+        const int64_t ld8 = 2 * ldo;
+        const uint32_t by8 = (uint32_t)((int64_t)N * ld8);
+        char* base8 = (char*)(o3 + (int64_t)b * N * 2 * D);
+        store_tile32(scr, oacc[qb], inv[qb], make_rsrc(base8 + hd * DH * 2, by8 - hd * DH * 2), ld8, row0, lane_here());
+        store_tile32_f8(scr, oacc[qb], inv[qb], make_rsrc(base8 + 2 * D + hd * 128, by8 - (2 * D + hd * 128)), ld8,
+                        row0, lane_here());
+      }
+      if constexpr (XM == 1) {
+        // hi = bf16(O) twice, then lo = bf16(O - hi), O = oacc * inv as store_tile32 forms it
+        const int64_t ld3 = 3 * ldo;
+        const uint32_t by3 = (uint32_t)((int64_t)N * ld3);
+        bf16* base3 = o3 + (int64_t)b * N * 3 * D + hd * DH;
+        store_tile32(scr, oacc[qb], inv[qb], make_rsrc(base3 + D, by3 - (D + hd * DH) * 2), ld3, row0, lane_here());
+        store_tile32(scr, oacc[qb], inv[qb], make_rsrc(base3, by3 - hd * DH * 2), ld3, row0, lane_here());
+        f32x16 lo[2];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = oacc[qb][dt][r] * inv[qb];
+            lo[dt][r] = v - (float)(bf16)v;
+          }
+        store_tile32(scr, lo, 1.f, make_rsrc(base3 + 2 * D, by3 - (2 * D + hd * DH) * 2), ld3, row0, lane_here());
+      }
+    }
   };
   if (q0 + 32 < N) body(std::integral_constant<int, 2>{});
   else if (q0 < N) body(std::integral_constant<int, 1>{});
@@ -2284,11 +2318,17 @@ extern "C" int vitmi_attention_fwd_x3(int B, int N, int H, int dh, float scale, 
   VITMI_CHECK_ARG(N <= SEQ_MAX, "attention_fwd_x3: N must be <= %d (the whole-sequence kernel)", SEQ_MAX);
   VITMI_CHECK_ARG(qkv && o && o3 && lse, "attention_fwd_x3: null pointer");
   VITMI_CHECK_ARG((int64_t)N * 3 * H * DH * 2 < 0x7fffffffLL, "attention_fwd_x3: one batch row block exceeds 2 GiB");
-  hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, 1>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
-                     (hipStream_t)stream, (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o3);
+  const double bh = (double)B * H, fl = 4.0 * bh * N * N * DH, by = bh * N * DH * 2 * (3 + 1 + 3) + bh * N * 4;
+  if (q64()) {
+    hipLaunchKernelGGL((attn_fwd_seq64_bf16<SEQ_MAX, 1>), dim3(B * H), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o3);
+    VITMI_STAT((attn_fwd_seq64_bf16<SEQ_MAX, 1>), fl, by);
+  } else {
+    hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, 1>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
+                       (hipStream_t)stream, (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o3);
+    VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, 1>), fl, by);
+  }
   VITMI_LAUNCH_CHECK("attention_fwd_x3");
-  const double bh = (double)B * H;
-  VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, 1>), 4.0 * bh * N * N * DH, bh * N * DH * 2 * (3 + 1 + 3) + bh * N * 4);
   return VITMI_OK;
 }
 
@@ -2298,11 +2338,17 @@ extern "C" int vitmi_attention_fwd_f8(int B, int N, int H, int dh, float scale, 
   VITMI_CHECK_ARG(N <= SEQ_MAX, "attention_fwd_f8: N must be <= %d (the whole-sequence kernel)", SEQ_MAX);
   VITMI_CHECK_ARG(qkv && o && o8 && lse, "attention_fwd_f8: null pointer");
   VITMI_CHECK_ARG((int64_t)N * 3 * H * DH * 2 < 0x7fffffffLL, "attention_fwd_f8: one batch row block exceeds 2 GiB");
-  hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, 2>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
-                     (hipStream_t)stream, (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o8);
+  const double bh = (double)B * H, fl = 4.0 * bh * N * N * DH, by = bh * N * DH * 2 * (3 + 1 + 2) + bh * N * 4;
+  if (q64()) {
+    hipLaunchKernelGGL((attn_fwd_seq64_bf16<SEQ_MAX, 2>), dim3(B * H), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o8);
+    VITMI_STAT((attn_fwd_seq64_bf16<SEQ_MAX, 2>), fl, by);
+  } else {
+    hipLaunchKernelGGL((attn_fwd_seq_bf16<SEQ_MAX, 2>), dim3(B * H), dim3(64 * ((N + 31) / 32)), 0,
+                       (hipStream_t)stream, (const bf16*)qkv, (bf16*)o, lse, N, H, scale, (bf16*)o8);
+    VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, 2>), fl, by);
+  }
   VITMI_LAUNCH_CHECK("attention_fwd_f8");
-  const double bh = (double)B * H;
-  VITMI_STAT((attn_fwd_seq_bf16<SEQ_MAX, 2>), 4.0 * bh * N * N * DH, bh * N * DH * 2 * (3 + 1 + 2) + bh * N * 4);
   return VITMI_OK;
 }
 
