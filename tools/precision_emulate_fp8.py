@@ -89,6 +89,10 @@ def make_mm(mode, block):
         if mode == "f8fixed":   # no amax anywhere: hi at scale 1, lo = x - hi at scale 2^-9
             lo_s = 2.0 ** -9
             return ha @ hw.t() + (q8_fixed(ha, 1.0) @ q8_fixed(lw, lo_s).t() + q8_fixed(la, lo_s) @ q8_fixed(hw, 1.0).t())
+        if mode == "f8x":       # one-sided: only the activation's rounding corrected, lo_x . hi_w
+            return ha @ hw.t() + q8_fixed(la, 2.0 ** -9) @ q8_fixed(hw, 1.0).t()
+        if mode == "f8w":       # one-sided: only the weight's rounding corrected, hi_x . lo_w
+            return ha @ hw.t() + q8_fixed(ha, 1.0) @ q8_fixed(lw, 2.0 ** -9).t()
         # fp8 corrections: [hi_a | lo_a] . [lo_w | hi_w]^T, each half its own block scales
         return ha @ hw.t() + (q8(ha, block) @ q8(lw, block).t() + q8(la, block) @ q8(hw, block).t())
     return mm
@@ -133,6 +137,8 @@ def main():
     ap.add_argument("--img", type=int, default=64)
     ap.add_argument("--classes", action="store_true",
                     help="fixed-scale e4m3 corrections with one GEMM class at a time in plain bf16")
+    ap.add_argument("--sides", action="store_true",
+                    help="one-sided e4m3 corrections (lo_x.hi_w or hi_x.lo_w) per GEMM class")
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
@@ -158,6 +164,21 @@ def main():
         base = forward(img, params, cfg, make_mm("fp32", 0))
         print(f"{'C1 ' + str(args.img) + 'px' if args.c1 else f'ViT-B/16 224px depth {args.depth} bs {args.batch}, {args.init} init'}; "
               f"emulator (q/k/v, P bf16; GEMMs fp32) vs oracle: {(base - ref).abs().max().item():.2e}")
+        if args.sides:
+            m = {k: make_mm(k, 0) for k in ("f8fixed", "f8x", "f8w", "bf16")}
+            print(f"{'per-class corrections (f=both, x=lo_x.hi_w, w=hi_x.lo_w, b=none)':<56} logits max-abs vs fp32")
+            combos = [("b", "f", "f", "f", "f"), ("b", "x", "x", "x", "x"), ("b", "w", "w", "w", "w"),
+                      ("f", "x", "x", "x", "x"), ("f", "w", "w", "w", "w"), ("x", "x", "x", "x", "x"),
+                      ("b", "x", "f", "f", "f"), ("b", "w", "f", "f", "f"), ("b", "f", "x", "f", "f"),
+                      ("b", "f", "w", "f", "f"), ("b", "f", "f", "x", "f"), ("b", "f", "f", "w", "f"),
+                      ("b", "f", "f", "f", "x"), ("b", "f", "f", "f", "w"), ("x", "f", "f", "f", "f"),
+                      ("w", "f", "f", "f", "f")]
+            code = {"f": "f8fixed", "x": "f8x", "w": "f8w", "b": "bf16"}
+            for cb in combos:
+                per = {c: m[code[v]] for c, v in zip(("qkv", "proj", "fc1", "fc2", "patch"), cb)}
+                err = (forward(img, params, cfg, m["f8fixed"], per) - ref).abs().max().item()
+                print(f"qkv={cb[0]} proj={cb[1]} fc1={cb[2]} fc2={cb[3]} patch={cb[4]:<22} {err:.2e}", flush=True)
+            return
         if args.classes:
             f8, b16 = make_mm("f8fixed", 0), make_mm("bf16", 0)
             print(f"{'GEMM class in plain bf16 (rest bf16f8)':<56} logits max-abs vs fp32")

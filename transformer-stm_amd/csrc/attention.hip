@@ -1543,7 +1543,35 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
     const int b = bh / H, hd = bh - b * H;
     stage_seq_dma(dt_, make_rsrc(dout + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2), ldo, NP, NKB, wave, lane);
   };
-  auto load_regs = [&](int bh, bf16x8 (&kf)[4], bf16x8 (&vf)[4], bf16x8 (&of)[4], float& ls) {
+// Where the next pair's loads go (round 6, profiles/r06_pf5/): 5 = the O rows right after delta (their
+// last use), the dO image DMA and the K / V rows + lse after phase 1.  Each lane's 16-B row pieces
+// touch 32 lines per instruction, and the cost of those loads (~1.5 us per 4 instructions per wave)
+// lands in whichever phase follows their issue; the O rows hide behind the delta barrier and phase 1
+// (per layer 212-219 vs 234-243 us).  1 = all of them after phase 1, 0 = after phase 2, 2 / 3 = the
+// DMA / the register rows after phase 2, 6 / 7 = K / V spread over phase 2 (and O over phase 1):
+// measured, not better than 5.
+#ifndef VITMI_FUSED_PF
+#define VITMI_FUSED_PF 5
+#endif
+  // the O rows alone (VITMI_FUSED_PF 5 issues them right after delta, their last use)
+  auto load_o = [&](int bh, bf16x8 (&of)[4], int s0 = 0, int s1 = 4) {
+    const int b = bh / H, hd = bh - b * H;
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(o + (int64_t)b * N * D + hd * DH, obytes - hd * DH * 2);
+    const uint32_t ooff = (uint32_t)((int64_t)r32 * ldo + 16 * h);
+#pragma unroll
+    for (int s = s0; s < s1; ++s) of[s] = __builtin_bit_cast(bf16x8, asm_load16(ro, ooff, 32 * s));
+  };
+  // one 16-B piece of the lane's K and V rows (VITMI_FUSED_PF 6 spreads them over phase 2)
+  auto load_kv1 = [&](int bh, bf16x8 (&kf)[4], bf16x8 (&vf)[4], int s) {
+    const int b = bh / H, hd = bh - b * H;
+    const bf16* base = qkv + (int64_t)b * N * ld;
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
+    const __amdgpu_buffer_rsrc_t rv = make_rsrc(base + 2 * D + hd * DH, bytes - (2 * D + hd * DH) * 2);
+    const uint32_t kvoff = (uint32_t)((int64_t)r32 * ldb + 16 * h);
+    kf[s] = __builtin_bit_cast(bf16x8, asm_load16(rk, kvoff, 32 * s));
+    vf[s] = __builtin_bit_cast(bf16x8, asm_load16(rv, kvoff, 32 * s));
+  };
+  auto load_regs = [&](int bh, bf16x8 (&kf)[4], bf16x8 (&vf)[4], bf16x8 (&of)[4], float& ls, bool with_o = true) {
     const int b = bh / H, hd = bh - b * H;
     const bf16* base = qkv + (int64_t)b * N * ld;
     const __amdgpu_buffer_rsrc_t rk = make_rsrc(base + D + hd * DH, bytes - (D + hd * DH) * 2);
@@ -1554,7 +1582,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
     for (int s = 0; s < 4; ++s) {
       kf[s] = __builtin_bit_cast(bf16x8, asm_load16(rk, kvoff, 32 * s));
       vf[s] = __builtin_bit_cast(bf16x8, asm_load16(rv, kvoff, 32 * s));
-      of[s] = __builtin_bit_cast(bf16x8, asm_load16(ro, ooff, 32 * s));
+      if (with_o) of[s] = __builtin_bit_cast(bf16x8, asm_load16(ro, ooff, 32 * s));
     }
     ls = asm_load4(make_rsrc(lse + (int64_t)bh * N, (uint32_t)N * 4), (uint32_t)r32 * 4);
   };
@@ -1598,6 +1626,9 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
         if (ok) delta[(int64_t)bh * N + r32] = dl;
       }
     }
+    const bool more1 = i + (int)gridDim.x < npairs;
+    const int nbh1 = more1 ? pair_of(i + gridDim.x) : 0;
+    if ((VITMI_FUSED_PF == 5 || VITMI_FUSED_PF == 6) && more1) load_o(pair_of(i + gridDim.x), of);   // (of is dead)
     __syncthreads();
     FUSED_STAMP(bh, 1);
 
@@ -1608,6 +1639,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
       const int q0 = 32 * qb;
       f32x16 sa = zero16(), dp;
       f32x4 L2[4];
+      if (VITMI_FUSED_PF == 7 && more1 && qb < 4) load_o(nbh1, of, qb, qb + 1);   // (of is dead after delta)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int q4 = q0 + 8 * g4 + 4 * h;
@@ -1660,14 +1692,20 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
     const int nbh = more ? pair_of(inext) : 0;
     // the next pair's dO image (the dO image is free) and register rows (kf / vf / of are dead)
     // land under phase 2 and the epilogue
-#ifndef VITMI_FUSED_PF
-#define VITMI_FUSED_PF 1
-#endif
     if (more && VITMI_FUSED_PF == 1) {
       stage_do(nbh);
       load_regs(nbh, kf, vf, of, ls);
     }
     if (more && VITMI_FUSED_PF == 2) load_regs(nbh, kf, vf, of, ls);
+    if (more && VITMI_FUSED_PF == 3) stage_do(nbh);
+    if (more && VITMI_FUSED_PF == 5) {
+      stage_do(nbh);
+      load_regs(nbh, kf, vf, of, ls, false);
+    }
+    if (more && (VITMI_FUSED_PF == 6 || VITMI_FUSED_PF == 7)) {
+      stage_do(nbh);
+      ls = asm_load4(make_rsrc(lse + (int64_t)nbh * N, (uint32_t)N * 4), (uint32_t)r32 * 4);
+    }
     __syncthreads();
 
     // ---- phase 2: wave w takes query block w: dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q]
@@ -1675,6 +1713,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       const char* tile = dst + (kb * NKB + wave) * DT;
+      if ((VITMI_FUSED_PF == 6 || VITMI_FUSED_PF == 7) && more && kb < 4) load_kv1(nbh, kf, vf, kb);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16x8 sf = frag_tr32(tile, 16 * s, lane);
@@ -1690,6 +1729,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_bwd_fused_seq_bf16(
       load_regs(nbh, kf, vf, of, ls);
     }
     if (more && VITMI_FUSED_PF == 2) stage_do(nbh);
+    if (more && VITMI_FUSED_PF == 3) load_regs(nbh, kf, vf, of, ls);
 
     // ---- epilogue: dQ, dK, dV through three images per wave, then their column sums (the q/k/v
     // bias-gradient partials of this batch row) in one pass, folded in wave order
