@@ -152,6 +152,18 @@ int vitmi_linear_dgrad_bias(int dtype, int64_t M, int64_t N, int64_t K, const vo
                             vitmi_stream_t stream);
 
 size_t vitmi_linear_wgrad_workspace_size(int dtype, int64_t M, int64_t N, int64_t K);
+/* Grouped weight gradients over ONE row count M: for p < n (n <= 4), dW_p[N[p], K[p]] (f32) +=
+ * dy_p[M, N[p]]^T x_p[M, K[p]], dy_p rows of pitch lddy[p] and x_p of pitch ldx[p] elements (NULL
+ * or 0: dense).  The four weight gradients of a transformer block (models/CvT(Par).py:253-258,
+ * 132-142: fc2, fc1, out-projection, qkv) in one split-K launch over all their tiles and one
+ * reduction launch (bf16; other dtypes and shapes run one vitmi_linear_wgrad-equivalent GEMM per
+ * problem).  workspace >= vitmi_linear_wgrad_group_workspace_size(dtype, n, M, N, K). */
+int vitmi_linear_wgrad_group(int dtype, int n, int64_t M, const int64_t* N, const int64_t* K,
+                             const void* const* dy, const int64_t* lddy, const void* const* x,
+                             const int64_t* ldx, float* const* dw, void* workspace, size_t ws_bytes,
+                             vitmi_stream_t stream);
+size_t vitmi_linear_wgrad_group_workspace_size(int dtype, int n, int64_t M, const int64_t* N,
+                                               const int64_t* K);
 /* db[N] (f32) += sum_m dy[m, n]  (dy [M][ldy] of `dtype`) */
 int vitmi_bias_grad(int dtype, int64_t M, int64_t N, const void* dy, int64_t ldy, float* db,
                     void* workspace, size_t ws_bytes, vitmi_stream_t stream);

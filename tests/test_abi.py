@@ -107,6 +107,27 @@ def test_workspace_queries_are_pure_host():
     assert lib.vitmi_attention_bwd_workspace_size(2, 197, 12) == 2 * 197 * 12 * 4
     assert lib.vitmi_linear_wgrad_workspace_size(1, 50432, 768, 768) > 0
     assert lib.vitmi_bias_grad_workspace_size(50432, 768) > 0
+    # the grouped weight gradients of a ViT-B block: 108 tiles -> 7 slabs each (756 units on 3
+    # rounds of 256 CUs), 7 x (4 x 768 x 3072 / 2 + 768 x 768 + 2304 x 768) fp32 partials
+    import ctypes
+    Ns = (ctypes.c_int64 * 4)(768, 3072, 768, 2304)
+    Ks = (ctypes.c_int64 * 4)(3072, 768, 768, 768)
+    need = lib.vitmi_linear_wgrad_group_workspace_size(1, 4, 50432, Ns, Ks)
+    assert need == 7 * (2 * 768 * 3072 + 768 * 768 + 2304 * 768) * 4
+    assert lib.vitmi_linear_wgrad_group_workspace_size(1, 5, 50432, Ns, Ks) == 0     # n > 4
+    assert lib.vitmi_linear_wgrad_group(1, 5, 50432, Ns, Ks, None, None, None, None, None, None, 0, None) == 1
+
+
+def test_wgrad_group_rejects_bad_arguments():
+    import ctypes
+    lib = _lib.lib()
+    Ns = (ctypes.c_int64 * 2)(768, 768)
+    Ks = (ctypes.c_int64 * 2)(768, 768)
+    # null operand arrays
+    assert lib.vitmi_linear_wgrad_group(1, 2, 1000, Ns, Ks, None, None, None, None, None, None, 0, None) == 1
+    assert b"null" in lib.vitmi_last_error()
+    # nothing to do
+    assert lib.vitmi_linear_wgrad_group(1, 0, 1000, None, None, None, None, None, None, None, None, 0, None) == 0
 
 
 @pytest.mark.parametrize("name", ["vitmi_gemm", "vitmi_attention_fwd", "vitmi_layernorm_bwd"])

@@ -182,6 +182,53 @@ def test_linear_wgrad_split_units(M, N, K):
     assert rel(dw, ref) < 2e-5
 
 
+@pytest.mark.parametrize("M,shapes", [
+    (197 * 24, [(768, 3072), (3072, 768), (768, 768), (2304, 768)]),   # a ViT-B block's four wgrads
+    (197 * 16 + 37, [(256, 512), (520, 264)]),                          # ragged rows and tile edges
+    (4000, [(1024, 4096), (4096, 1024), (3072, 1024)]),                 # ViT-L-like, three problems
+])
+def test_linear_wgrad_group_matches_oracle(M, shapes):
+    """vitmi_linear_wgrad_group: every problem's dW += dy^T x in one grouped launch (the split-K
+    units of all problems in one persistent unit space) and one segment reduction, onto nonzero
+    dW; one x row-strided (the hi part of a split operand).  Reference: fp32 products of the same
+    bf16 operands.  Also run twice: bitwise deterministic."""
+    items, refs = [], []
+    for i, (n, k) in enumerate(shapes):
+        dy = rnd(M, n, dtype=BF, seed=70 + 3 * i)
+        xw = rnd(M, k + (8 if i == 1 else 0), dtype=BF, seed=71 + 3 * i)
+        x = xw[:, :k]
+        prev = rnd(n, k, seed=72 + 3 * i)
+        refs.append(prev + dy.float().t() @ x.float())
+        items.append((dy.to(DEV), xw.to(DEV)[:, :k], prev.to(DEV)))
+    outs = []
+    for _ in range(2):
+        dws = [p.clone() for _, _, p in items]
+        ops.linear_wgrad_group([(dy, x, dw) for (dy, x, _), dw in zip(items, dws)])
+        torch.cuda.synchronize()
+        outs.append(dws)
+    for dw, ref in zip(outs[0], refs):
+        assert rel(dw, ref) < 2e-5
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
+def test_linear_wgrad_group_falls_back_per_problem():
+    """fp32 operands (and a bf16 group with one item) take the per-problem path: same results as
+    ops.linear_wgrad."""
+    M = 700
+    its = [(rnd(M, 96, seed=81).to(DEV), rnd(M, 64, seed=82).to(DEV)),
+           (rnd(M, 128, seed=83).to(DEV), rnd(M, 32, seed=84).to(DEV))]
+    dws = [torch.zeros(96, 64, device=DEV), torch.zeros(128, 32, device=DEV)]
+    ops.linear_wgrad_group([(dy, x, dw) for (dy, x), dw in zip(its, dws)])
+    for (dy, x), dw in zip(its, dws):
+        assert rel(dw, dy.t() @ x) < 1e-5
+    dy, x = rnd(M, 256, dtype=BF, seed=85).to(DEV), rnd(M, 256, dtype=BF, seed=86).to(DEV)
+    a, b = torch.zeros(256, 256, device=DEV), torch.zeros(256, 256, device=DEV)
+    ops.linear_wgrad_group([(dy, x, a)])
+    ops.linear_wgrad(dy, x, b)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("M,N,K", [(256 * 5 + 40, 768, 512), (296, 264, 128)])
 def test_gemm_tn_layout_epilogues(M, N, K, policy):
     """The TN layout (A and B both m/n-major, the weight-gradient operands) through the generic

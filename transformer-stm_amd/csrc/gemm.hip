@@ -99,7 +99,20 @@ struct GemmArgs {
   // VITMI_BF16F8 operands (gemm256<..., F8>): K-steps >= k8 (absolute, 64-bf16 = 128-B steps) are
   // the rows' e4m3 parts, multiplied by the block-scaled fp8 MFMA; the steps before are bf16
   int k8;
+  // grouped weight gradients (gemm256_kernel<false, false, EPI_PARTIAL, float, false, true>): up to
+  // GRP_MAX problems over one reduction length K, each with its own operands and partial slabs;
+  // the folded split-K unit space runs over their concatenated tiles (problem p owns tiles
+  // [tile0, tile0 + tiles)); slab z of problem p at C + z * M * N (fp32, row pitch N)
+  struct Prob {
+    const void* A;
+    const void* B;
+    float* C;
+    int64_t M, N, lda, ldb;
+    int tiles_n, tile0;
+  } grp[4];
+  int ngrp;
 };
+constexpr int GRP_MAX = 4;
 
 // Element (row, col) of a tile-native gelu' buffer (VITMI_EPI_AUX_TILED; bf16 elements): 256x256
 // tiles in row-major tile order, each 128 KiB laid out as gemm256's epilogue registers hold it --
@@ -600,7 +613,7 @@ __device__ __forceinline__ void gelu4(f32x4 x, f32x4& a, f32x4& gp) {
 // Waits: vmcnt(8) at P0 retires B1(s), at P1 A1(s), at P3 A0(s+1),B0(s+1); each sits
 // before a barrier that the later reader passes, with one barrier of slack for the
 // staggered group.
-template <bool AK, bool BKM, int EPI, typename TC, bool F8 = false>
+template <bool AK, bool BKM, int EPI, typename TC, bool F8 = false, bool GRP = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   using namespace g256;
   // two DMA stages + the bias of the current and the next tile (fp32, double-buffered) + one
@@ -638,18 +651,23 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 
   // Operand descriptors with the unit's first k (kb + ks0 K-steps) baked into the base, so
   // the DMA issue only needs the unit-relative K-step.
-  auto rsrc_a = [&](int64_t m0, int ks0) {
+  // (GRP: problem p's operands; otherwise g's)
+  auto rsrc_a = [&](int64_t m0, int ks0, [[maybe_unused]] int p = 0) {
     const int64_t k = kb + (int64_t)ks0 * BK;
-    return AK ? make_rsrc((const char*)g.A + (m0 * g.lda + k) * 2, clamp_bytes((g.M - m0) * g.lda * 2 - k * 2))
-              : make_rsrc((const char*)g.A + (k * g.lda + m0) * 2, clamp_bytes(((g.K - k) * g.lda - m0) * 2));
+    const char* A = (const char*)(GRP ? g.grp[p].A : g.A);
+    const int64_t lda = GRP ? g.grp[p].lda : g.lda, M = GRP ? g.grp[p].M : g.M;
+    return AK ? make_rsrc(A + (m0 * lda + k) * 2, clamp_bytes((M - m0) * lda * 2 - k * 2))
+              : make_rsrc(A + (k * lda + m0) * 2, clamp_bytes(((g.K - k) * lda - m0) * 2));
   };
-  auto rsrc_b = [&](int64_t n0, int ks0) {
+  auto rsrc_b = [&](int64_t n0, int ks0, [[maybe_unused]] int p = 0) {
     const int64_t k = kb + (int64_t)ks0 * BK;
-    return BKM ? make_rsrc((const char*)g.B + (n0 * g.ldb + k) * 2, clamp_bytes((g.N - n0) * g.ldb * 2 - k * 2))
-               : make_rsrc((const char*)g.B + (k * g.ldb + n0) * 2, clamp_bytes(((g.K - k) * g.ldb - n0) * 2));
+    const char* B = (const char*)(GRP ? g.grp[p].B : g.B);
+    const int64_t ldb = GRP ? g.grp[p].ldb : g.ldb, N = GRP ? g.grp[p].N : g.N;
+    return BKM ? make_rsrc(B + (n0 * ldb + k) * 2, clamp_bytes((N - n0) * ldb * 2 - k * 2))
+               : make_rsrc(B + (k * ldb + n0) * 2, clamp_bytes(((g.K - k) * ldb - n0) * 2));
   };
   // unit u -> tile origin, first K-step and K-step count
-  auto unit_of = [&](int u, int64_t& m0_, int64_t& n0_, int& ks0_, int& nk_, int& z_) {
+  auto unit_of = [&](int u, int64_t& m0_, int64_t& n0_, int& ks0_, int& nk_, int& z_, [[maybe_unused]] int& p_) {
     int tl = u;
     ks0_ = 0;
     nk_ = nk;
@@ -666,19 +684,33 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
       nk_ = min(g.ksplit, nk - ks0_);
     }
     int tm_, tn_;
-    tile_rc(g, tl, tm_, tn_);
+    if constexpr (GRP) {
+      // the problem whose tile range holds tl (wave-uniform)
+      int p = 0;
+#pragma unroll
+      for (int q = 1; q < GRP_MAX; ++q)
+        if (q < g.ngrp && tl >= g.grp[q].tile0) p = q;
+      p_ = p;
+      tl -= g.grp[p].tile0;
+      tm_ = tl / g.grp[p].tiles_n;
+      tn_ = tl - tm_ * g.grp[p].tiles_n;
+    } else {
+      tile_rc(g, tl, tm_, tn_);
+    }
     m0_ = (int64_t)tm_ * BM;
     n0_ = (int64_t)tn_ * BN;
   };
   auto sub = [&](int buf, int which) -> char* { return smem + buf * STAGE + which * HALF; };
   // issue half `which` (0=A0 1=B0 2=A1 3=B1) of K-step t into buffer buf
-  auto issue = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int t, int buf, int which) {
+  // (la, lb: the row pitches of the unit the descriptors belong to; g's unless GRP)
+  auto issue = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int t, int buf, int which,
+                   int64_t la, int64_t lb) {
     const int64_t k0 = (int64_t)t * BK;   // relative to the descriptor's k
     const int krow0 = t * BK;
-    if (which == 0) stage_half<true, AK>(sub(buf, 0), ra, g.lda, k0, krow0, 0, wave, lane);
-    if (which == 1) stage_half<false, BKM>(sub(buf, 2), rb, g.ldb, k0, krow0, 0, wave, lane);
-    if (which == 2) stage_half<true, AK>(sub(buf, 1), ra, g.lda, k0, krow0, 1, wave, lane);
-    if (which == 3) stage_half<false, BKM>(sub(buf, 3), rb, g.ldb, k0, krow0, 1, wave, lane);
+    if (which == 0) stage_half<true, AK>(sub(buf, 0), ra, la, k0, krow0, 0, wave, lane);
+    if (which == 1) stage_half<false, BKM>(sub(buf, 2), rb, lb, k0, krow0, 0, wave, lane);
+    if (which == 2) stage_half<true, AK>(sub(buf, 1), ra, la, k0, krow0, 1, wave, lane);
+    if (which == 3) stage_half<false, BKM>(sub(buf, 3), rb, lb, k0, krow0, 1, wave, lane);
   };
 
   // Fragment registers, double-buffered so each phase's ds_reads overlap the previous
@@ -759,13 +791,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
   if (it >= nseq) return;
   int tile = unit_at(it);   // work unit (a whole tile, or a K-range of a tail tile)
   int64_t m0, n0;
-  int ks0, nku, zs;
-  unit_of(tile, m0, n0, ks0, nku, zs);
-  __amdgpu_buffer_rsrc_t ra = rsrc_a(m0, ks0), rb = rsrc_b(n0, ks0);
+  int ks0, nku, zs, pc = 0;
+  unit_of(tile, m0, n0, ks0, nku, zs, pc);
+  __amdgpu_buffer_rsrc_t ra = rsrc_a(m0, ks0, pc), rb = rsrc_b(n0, ks0, pc);
+  int64_t la = GRP ? g.grp[pc].lda : g.lda, lb = GRP ? g.grp[pc].ldb : g.ldb;
   int buf = 0;
   // steps 0 and 1 of the first unit in the loop's issue order (nk >= 2 is a precondition)
-  issue(ra, rb, 0, 0, 0); issue(ra, rb, 0, 0, 1); issue(ra, rb, 0, 0, 3); issue(ra, rb, 0, 0, 2);
-  issue(ra, rb, 1, 1, 0); issue(ra, rb, 1, 1, 1);
+  issue(ra, rb, 0, 0, 0, la, lb); issue(ra, rb, 0, 0, 1, la, lb); issue(ra, rb, 0, 0, 3, la, lb);
+  issue(ra, rb, 0, 0, 2, la, lb);
+  issue(ra, rb, 1, 1, 0, la, lb); issue(ra, rb, 1, 1, 1, la, lb);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");      // A0(0), B0(0) landed
   barrier();
   if (wm) barrier();                                     // waves 4..7 one barrier behind
@@ -805,9 +839,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     const bool has_next = itn < nseq;
     const int next = has_next ? unit_at(itn) : 0;
     int64_t m0n = 0, n0n = 0;
-    int ks0n = 0, nkn = 0, zsn = 0;
-    if (has_next) unit_of(next, m0n, n0n, ks0n, nkn, zsn);
-    const __amdgpu_buffer_rsrc_t ran = rsrc_a(m0n, ks0n), rbn = rsrc_b(n0n, ks0n);
+    int ks0n = 0, nkn = 0, zsn = 0, pn = 0;
+    if (has_next) unit_of(next, m0n, n0n, ks0n, nkn, zsn, pn);
+    const __amdgpu_buffer_rsrc_t ran = rsrc_a(m0n, ks0n, pn), rbn = rsrc_b(n0n, ks0n, pn);
+    const int64_t lan = GRP ? g.grp[pn].lda : g.lda, lbn = GRP ? g.grp[pn].ldb : g.ldb;
 
       // vmcnt counts of the first step after an epilogue that issued S vector-memory ops:
       // 8 + S (capped at the counter's 63): S = 16 (bf16 store), 32 (GELU, fp32 store, split
@@ -836,13 +871,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         const bool h1 = in1 || has_next, h2 = in2 || has_next;
         const __amdgpu_buffer_rsrc_t a1 = in1 ? ra : ran, b1r = in1 ? rb : rbn;
         const __amdgpu_buffer_rsrc_t a2 = in2 ? ra : ran, b2r = in2 ? rb : rbn;
+        const int64_t la1 = !GRP ? g.lda : in1 ? la : lan, lb1 = !GRP ? g.ldb : in1 ? lb : lbn;
+        const int64_t la2 = !GRP ? g.lda : in2 ? la : lan, lb2 = !GRP ? g.ldb : in2 ? lb : lbn;
         const int t1 = in1 ? t + 1 : 0, t2 = in2 ? t + 2 : t + 2 - nku;
         const int fst = FIRST ? ep_ops : 0;
         // P0 (A0,B0): DMA B1(t+1); retire B1(t)
         RD_A(ax, buf, 0);
         RD_B(b0, buf, 0);
         if (h1) {
-          issue(a1, b1r, t1, buf ^ 1, 3);
+          issue(a1, b1r, t1, buf ^ 1, 3, la1, lb1);
           WAITF();
         } else {
           WAITV(0);
@@ -851,7 +888,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         // P1 (A0,B1): DMA A1(t+1); retire A1(t)
         RD_B(b1, buf, 1);
         if (h1) {
-          issue(a1, b1r, t1, buf ^ 1, 2);
+          issue(a1, b1r, t1, buf ^ 1, 2, la1, lb1);
           WAITF();
         } else {
           WAITV(0);
@@ -859,11 +896,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
         COMPUTE(0, 1, ax, b1);
         // P2 (A1,B1): DMA A0(t+2) into the half read at P0
         RD_A(ay, buf, 1);
-        if (h2) issue(a2, b2r, t2, buf, 0);
+        if (h2) issue(a2, b2r, t2, buf, 0, la2, lb2);
         COMPUTE(1, 1, ay, b1);
         // P3 (A1,B0): DMA B0(t+2); retire A0(t+1), B0(t+1)
         if (h2) {
-          issue(a2, b2r, t2, buf, 1);
+          issue(a2, b2r, t2, buf, 1, la2, lb2);
           WAITF();
         } else {
           WAITV(0);
@@ -894,6 +931,23 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
 #undef MMA4F8
 
     stamp(1);
+    if constexpr (GRP) {
+      // raw fp32 partial of slab zs into problem pc's slab area (row pitch N; rows >= M and
+      // columns >= N dropped by the range check and the out-of-range voffset)
+      const int64_t Mp = g.grp[pc].M, Np = g.grp[pc].N;
+      const __amdgpu_buffer_rsrc_t rw =
+          make_rsrc((char*)g.grp[pc].C + ((int64_t)zs * Mp * Np + m0 * Np + n0) * 4, clamp_bytes(((Mp - m0) * Np - n0) * 4));
+      const uint32_t wbase = (uint32_t)(((wm * 128 + lr) * Np + wn * 64 + lc4) * 4);
+      const int rs16 = (int)(16 * Np * 4);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const uint32_t vo = n0 + wn * 64 + ni * 16 + lc4 < Np ? wbase : 0x80000000u;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+          asm volatile(VMEM_SGPR_GUARD "buffer_store_dwordx4 %0, %1, %2, %3 offen offset:%4\n\ts_nop 1"
+                       :: "v"(acc[mi][ni]), "v"(vo), "s"(rw), "s"(mi * rs16), "i"(ni * 64) : "memory");
+      }
+    } else
     if ((EPI != EPI_PARTIAL || g.kz <= 1) && tile >= g.t_full) {
       // K-range of a tail tile: raw fp32 partial into its [256][256] slab
       const __amdgpu_buffer_rsrc_t rw = make_rsrc(g.tail_ws + (int64_t)(tile - g.t_full) * BM * BN, BM * BN * 4);
@@ -1288,6 +1342,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs g, int nwg) {
     }
     if (!has_next) break;
     it = itn; tile = next; m0 = m0n; n0 = n0n; ks0 = ks0n; nku = nkn; zs = zsn; ra = ran; rb = rbn;
+    if constexpr (GRP) {
+      pc = pn;
+      la = lan;
+      lb = lbn;
+    }
   }
   // the leading group owes the staggered group its extra barrier: equal counts per wave
   if (!wm) barrier();
@@ -1343,6 +1402,40 @@ __global__ __launch_bounds__(1024) void splitk_reduce_small_kernel(const float* 
       *(f32x4*)(dst + i) = *(const f32x4*)(dst + i) + t;
     } else {
       for (int64_t e = i; e < n; ++e) dst[e] += t[e - i];
+    }
+  }
+}
+
+// The grouped weight gradients' reduction: segment q (up to GRP_MAX, the problems of one grouped
+// launch) adds its `splits` slabs at ws + off[q] (stride n[q]) onto dst[q], over one flat index space
+// of float4 groups; per element dst + slab 0 + slab 1 + ... as splitk_reduce_kernel sums.
+struct RedSegs {
+  const float* ws[GRP_MAX];
+  float* dst[GRP_MAX];
+  int64_t n[GRP_MAX];
+  int64_t g0[GRP_MAX + 1];   // first float4 group of each segment (prefix sums of ceil(n / 4))
+  int nseg;
+};
+__global__ void splitk_reduce_group_kernel(RedSegs rs, int splits) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gi < rs.g0[rs.nseg]; gi += step) {
+    int q = 0;
+#pragma unroll
+    for (int j = 1; j < GRP_MAX; ++j)
+      if (j < rs.nseg && gi >= rs.g0[j]) q = j;
+    const int64_t i = (gi - rs.g0[q]) * 4, n = rs.n[q];
+    const float* ws = rs.ws[q];
+    float* dst = rs.dst[q];
+    if (i + 4 <= n) {
+      f32x4 a = *(const f32x4*)(dst + i);
+      for (int z = 0; z < splits; ++z) a += *(const f32x4*)(ws + z * n + i);
+      *(f32x4*)(dst + i) = a;
+    } else {
+      for (int64_t e = i; e < n; ++e) {
+        float a = dst[e];
+        for (int z = 0; z < splits; ++z) a += ws[z * n + e];
+        dst[e] = a;
+      }
     }
   }
 }
@@ -1837,6 +1930,151 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   return VITMI_OK;
 }
 
+// ---------------------------------------------------------------- grouped weight gradients
+// dW_p[N_p, K_p] += dy_p[M, N_p]^T x_p[M, K_p] for p < n in ONE gemm256 launch (the K-slabs of
+// every problem folded into one persistent unit space) and one reduction launch.  One launch per
+// problem pays its own ramp, its own chip-wide burst of slab stores at the end and its own
+// reduction; and a small output (the out-projection's 768 x 768: 9 tiles) is cut into 28 slabs of
+// 28 K-steps there, against 7 of 113 here.
+struct WgProb {
+  const void* dy;
+  int64_t lddy;
+  const void* x;
+  int64_t ldx;
+  float* dw;
+  int64_t N, K;
+};
+
+// slabs per tile of a grouped launch: the smallest number of rounds r of the persistent grid whose
+// S = r * avail / tiles units fill >= 95 % of the r rounds (ViT-B: 108 tiles -> S = 7, 756 units
+// on 3 x 256 CUs; ViT-L: 192 -> 4, 768); each split keeps >= 8 K-steps
+static int group_splits(int64_t tiles, int64_t ktiles, int avail) {
+  int best = 1;
+  double beff = 0.0;
+  for (int r = 1; r <= 4; ++r) {
+    int64_t S = (int64_t)r * avail / tiles;
+    if (S < 1) S = 1;
+    if (S > 1 && ktiles / S < 8) break;
+    const double eff = (double)(tiles * S) / ((double)r * avail);
+    if (eff >= 0.95) return (int)S;
+    if (eff > beff) { beff = eff; best = (int)S; }
+  }
+  return best;
+}
+
+static bool group_ok(int dtype, int n, int64_t M, const WgProb* pr) {
+  if (dtype != VITMI_BF16 || n < 2 || n > GRP_MAX || M < 4 * 64 || g_policy == 1) return false;
+  for (int q = 0; q < n; ++q) {
+    const WgProb& w = pr[q];
+    if (w.N <= 0 || w.K <= 0 || (w.K % 8) != 0 || !use256(dtype, w.N, w.K, M, true)) return false;
+    if (((uintptr_t)w.dy % 16) || ((uintptr_t)w.x % 16) || ((w.lddy * 2) % 16) || ((w.ldx * 2) % 16)) return false;
+    if (w.lddy < w.N || w.ldx < w.K || M * w.lddy * 2 >= 0x7fffffffLL || M * w.ldx * 2 >= 0x7fffffffLL) return false;
+  }
+  return true;
+}
+
+static void group_plan(int n, int64_t M, const WgProb* pr, int64_t& tiles, int& S, size_t& need) {
+  init_cus();
+  tiles = 0;
+  int64_t mn = 0;
+  for (int q = 0; q < n; ++q) {
+    tiles += ((pr[q].N + 255) / 256) * ((pr[q].K + 255) / 256);
+    mn += pr[q].N * pr[q].K;
+  }
+  S = group_splits(tiles, (M + 63) / 64, g_cus);
+  need = (size_t)S * mn * sizeof(float);
+}
+
+static size_t wgrad_group_ws(int dtype, int n, int64_t M, const WgProb* pr) {
+  size_t need = 0;
+  if (group_ok(dtype, n, M, pr)) {
+    int64_t tiles;
+    int S;
+    group_plan(n, M, pr, tiles, S, need);
+  }
+  for (int q = 0; q < n; ++q) {   // the per-problem path (the fallback) may need more
+    const int sp = choose_splits(dtype, pr[q].N, pr[q].K, M, 0);
+    const size_t b = sp > 1 ? (size_t)sp * pr[q].N * pr[q].K * sizeof(float) : 0;
+    need = b > need ? b : need;
+  }
+  return need;
+}
+
+static int wgrad_group_impl(int dtype, int n, int64_t M, const WgProb* pr, void* ws, size_t ws_bytes, hipStream_t s) {
+  VITMI_CHECK_ARG(n >= 0 && n <= GRP_MAX, "linear_wgrad_group: 0..%d problems (got %d)", GRP_MAX, n);
+  VITMI_CHECK_ARG(M >= 0, "linear_wgrad_group: negative M");
+  for (int q = 0; q < n; ++q)
+    VITMI_CHECK_ARG(pr[q].dy && pr[q].x && pr[q].dw && pr[q].N >= 0 && pr[q].K >= 0, "linear_wgrad_group: problem %d: "
+                    "null operand or negative size", q);
+  if (n == 0 || M == 0) return VITMI_OK;
+  int64_t tiles = 0;
+  int S = 1;
+  size_t need = 0;
+  const bool grouped = group_ok(dtype, n, M, pr) && (group_plan(n, M, pr, tiles, S, need), S > 1) && ws &&
+                       ws_bytes >= need;
+  if (!grouped) {
+    for (int q = 0; q < n; ++q) {
+      const WgProb& w = pr[q];
+      if (int rc = gemm_impl(dtype, 0, 0, w.N, w.K, M, w.dy, w.lddy, w.x, w.ldx, w.dw, w.K, VITMI_F32,
+                             VITMI_EPI_ACCUM, nullptr, nullptr, 0, nullptr, 0, ws, ws_bytes, s, true))
+        return rc;
+    }
+    return VITMI_OK;
+  }
+  GemmArgs g{};
+  g.K = M;
+  g.lda = pr[0].lddy;   // (unused by the grouped kernel: its operands are the table's)
+  g.ldb = pr[0].ldx;
+  g.M = pr[0].N;
+  g.N = pr[0].K;
+  g.A = pr[0].dy;
+  g.B = pr[0].x;
+  g.ngrp = n;
+  const int64_t ktiles = (M + 63) / 64;
+  RedSegs rs{};
+  rs.nseg = n;
+  int64_t off = 0, t0 = 0;
+  double flops = 0, bytes = 0;
+  for (int q = 0; q < n; ++q) {
+    GemmArgs::Prob& P = g.grp[q];
+    P.A = pr[q].dy; P.lda = pr[q].lddy;
+    P.B = pr[q].x;  P.ldb = pr[q].ldx;
+    P.M = pr[q].N;  P.N = pr[q].K;
+    P.C = (float*)ws + off;
+    P.tiles_n = (int)((P.N + 255) / 256);
+    P.tile0 = (int)t0;
+    t0 += ((P.M + 255) / 256) * P.tiles_n;
+    rs.ws[q] = P.C;
+    rs.dst[q] = pr[q].dw;
+    rs.n[q] = P.M * P.N;
+    rs.g0[q + 1] = rs.g0[q] + (rs.n[q] + 3) / 4;
+    off += (int64_t)S * P.M * P.N;
+    flops += 2.0 * P.M * P.N * M;
+    bytes += (double)M * (P.M + P.N) * 2 + 2.0 * P.M * P.N * 4;
+  }
+  g.ntiles = (int)tiles;
+  g.kz = S;
+  g.kz_steps = (int)((ktiles + S - 1) / S);
+  g.k_per_split = ktiles * 64;
+  g.t_full = (int)(tiles * S);
+  g.nsplit = 1;
+  g.tiles_n = 1;
+  // every split must span >= 2 K-steps (the last one too)
+  VITMI_CHECK_ARG(ktiles - (int64_t)(S - 1) * g.kz_steps >= 2, "linear_wgrad_group: split plan %d x %d over %lld "
+                  "K-steps", S, g.kz_steps, (long long)ktiles);
+  const int nwg = (int)(tiles * S);
+  const int gx = grid256(nwg, 1);
+  hipLaunchKernelGGL((gemm256_kernel<false, false, EPI_PARTIAL, float, false, true>), dim3(gx), dim3(512), 0, s, g, nwg);
+  VITMI_LAUNCH_CHECK("gemm256_kernel (grouped wgrad)");
+  VITMI_STAT((gemm256_kernel<false, false, EPI_PARTIAL, float, false, true>), flops, bytes);
+  int blocks = (int)((rs.g0[n] + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(splitk_reduce_group_kernel, dim3(blocks), dim3(256), 0, s, rs, S);
+  VITMI_LAUNCH_CHECK("splitk_reduce_group_kernel");
+  VITMI_STAT(splitk_reduce_group_kernel, 0, (double)rs.g0[n] * 16 * (S + 2));
+  return VITMI_OK;
+}
+
 }  // namespace vitmi
 
 using namespace vitmi;
@@ -1975,4 +2213,37 @@ extern "C" int vitmi_linear_wgrad(int dtype, int64_t M, int64_t N, int64_t K, co
   // dW[N,K] += sum_m dy[m][n] x[m][k]: A(n,m) = dy (m-major rows of n), B(m,k) = x (k contiguous)
   return gemm_impl(dtype, 0, 0, N, K, M, dy, N, x, K, dw, K, VITMI_F32, VITMI_EPI_ACCUM, nullptr,
                    nullptr, 0, nullptr, 0, workspace, ws_bytes, (hipStream_t)stream, true);
+}
+
+static int wg_probs(int n, const int64_t* N, const int64_t* K, const void* const* dy, const int64_t* lddy,
+                    const void* const* x, const int64_t* ldx, float* const* dw, WgProb* pr) {
+  VITMI_CHECK_ARG(n >= 0 && n <= GRP_MAX, "linear_wgrad_group: 0..%d problems (got %d)", GRP_MAX, n);
+  VITMI_CHECK_ARG(n == 0 || (N && K), "linear_wgrad_group: null size arrays");
+  for (int q = 0; q < n; ++q) {
+    pr[q].N = N[q];
+    pr[q].K = K[q];
+    pr[q].dy = dy ? dy[q] : nullptr;
+    pr[q].x = x ? x[q] : nullptr;
+    pr[q].dw = dw ? dw[q] : nullptr;
+    pr[q].lddy = lddy && lddy[q] > 0 ? lddy[q] : N[q];
+    pr[q].ldx = ldx && ldx[q] > 0 ? ldx[q] : K[q];
+  }
+  return VITMI_OK;
+}
+
+extern "C" size_t vitmi_linear_wgrad_group_workspace_size(int dtype, int n, int64_t M, const int64_t* N,
+                                                          const int64_t* K) {
+  WgProb pr[GRP_MAX];
+  if (n < 0 || n > GRP_MAX || wg_probs(n, N, K, nullptr, nullptr, nullptr, nullptr, nullptr, pr)) return 0;
+  return wgrad_group_ws(dtype, n, M, pr);
+}
+
+extern "C" int vitmi_linear_wgrad_group(int dtype, int n, int64_t M, const int64_t* N, const int64_t* K,
+                                        const void* const* dy, const int64_t* lddy, const void* const* x,
+                                        const int64_t* ldx, float* const* dw, void* workspace, size_t ws_bytes,
+                                        vitmi_stream_t stream) {
+  WgProb pr[GRP_MAX];
+  if (int rc = wg_probs(n, N, K, dy, lddy, x, ldx, dw, pr)) return rc;
+  VITMI_CHECK_ARG(n == 0 || (dy && x && dw), "linear_wgrad_group: null operand arrays");
+  return wgrad_group_impl(dtype, n, M, pr, workspace, ws_bytes, (hipStream_t)stream);
 }

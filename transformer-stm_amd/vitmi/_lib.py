@@ -42,6 +42,8 @@ SIGNATURES = {
     "vitmi_linear_dgrad_workspace_size": (S, [I, L, L, L]),
     "vitmi_linear_wgrad": (I, [I, L, L, L, P, P, P, P, S, P]),
     "vitmi_linear_wgrad_workspace_size": (S, [I, L, L, L]),
+    "vitmi_linear_wgrad_group": (I, [I, I, L, P, P, P, P, P, P, P, P, S, P]),
+    "vitmi_linear_wgrad_group_workspace_size": (S, [I, I, L, P, P]),
     "vitmi_bias_grad": (I, [I, L, L, P, L, P, P, S, P]),
     "vitmi_bias_grad_workspace_size": (S, [L, L]),
     "vitmi_layernorm_fwd": (I, [L, I, P, L, P, P, F, P, I, L, P, P, P]),

@@ -466,15 +466,22 @@ class _BlockFn(torch.autograd.Function):
             dout.__dict__.pop(_LP_ATTR, None)
             seed, rate, site0 = drop
             g2_lp = ops.dropout_apply(g2, seed, site0 + 2, rate, T)
+        # the block's weight gradients, grouped per ops.WGRAD_GROUP (default: the out-projection's
+        # and qkv's in one split-K launch over both outputs' tiles and one reduction, at qkv's
+        # point; the MLP pair where du has just been written)
+        wg = []
         # MLP branch
         # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
         du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=gs(mlp.fc1.bias), aux_tiled=ctx.aux_tiled)
         if gs.wants(mlp.fc2.weight):
-            ops.linear_wgrad(g2_lp, act, gs(mlp.fc2.weight))
+            wg.append((g2_lp, act, gs(mlp.fc2.weight)))
         if not ctx.bias_done and gs.wants(mlp.fc2.bias):
             ops.bias_grad(g2_lp, gs(mlp.fc2.bias))
         if gs.wants(mlp.fc1.weight):
-            ops.linear_wgrad(du, h2, gs(mlp.fc1.weight))
+            wg.append((du, h2, gs(mlp.fc1.weight)))
+        if ops.WGRAD_GROUP in (0, 2, 3):
+            (ops.linear_wgrad_group if ops.WGRAD_GROUP == 2 else _each_wgrad)(wg)
+            wg = []
         dh2 = ops.linear_dgrad(du, w1, T)
         # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
         if drop is None:
@@ -491,12 +498,19 @@ class _BlockFn(torch.autograd.Function):
         # attention branch
         do = ops.linear_dgrad(dx1_lp, wo, T)
         if gs.wants(a_.proj.weight):
-            ops.linear_wgrad(dx1_lp, o, gs(a_.proj.weight))
+            wg.append((dx1_lp, o, gs(a_.proj.weight)))
+        if ops.WGRAD_GROUP == 0:
+            _each_wgrad(wg)
+            wg = []
         # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale, bias_grad=gs(a_.qkv.bias))
         if gs.wants(a_.qkv.weight):
-            ops.linear_wgrad(dqkv, h1, gs(a_.qkv.weight))
+            wg.append((dqkv, h1, gs(a_.qkv.weight)))
+        if ops.WGRAD_GROUP == 0:
+            _each_wgrad(wg)
+            wg = []
         dh1 = ops.linear_dgrad(dqkv, wq, T)
+        ops.linear_wgrad_group(wg)
         # the bf16 copy of dx is for a consumer that takes it (the block below); the patch
         # embedding's backward reads dx in fp32
         want_lp = drop is None and ctx.handover
@@ -504,6 +518,11 @@ class _BlockFn(torch.autograd.Function):
                                       dres=dx1, lp_dtype=lpT if want_lp else None, dxsum=gs(prev))
         out = _handover(dx.view(B, N, D), dx_lp)
         return (out, None, gs.grads([prev])[0], None, None, None) + gs.grads(ps)
+
+
+def _each_wgrad(items):
+    for dy, x, dw in items:
+        ops.linear_wgrad(dy, x, dw)
 
 
 # ======================================================================= embedding

@@ -7,6 +7,8 @@ fallback — a missing library or a bad shape raises.
 """
 from __future__ import annotations
 
+import ctypes
+import os
 import threading
 from typing import Optional, Tuple
 
@@ -231,6 +233,52 @@ def linear_wgrad(dy: Tensor, x: Tensor, dw: Tensor) -> None:
     ws = _ws(ws_n, dy)
     check(lib().vitmi_linear_wgrad(dt(dy.dtype), M, N, K, _p(dy), _p(x), _p(dw), _p(ws), ws.numel(),
                                    _s()), "linear_wgrad")
+
+
+# How a block's backward groups its weight gradients (vitmi/modules.py _BlockFn.backward): 0 = one
+# launch per problem where each gradient's operands are ready, 1 = all four in one launch at the end,
+# 2 = the MLP pair at fc1's point and the attention pair at qkv's, 3 = only the attention pair
+# (out-projection + qkv) grouped, at qkv's point.  Measured (profiles/r06_wgg/): alone, one grouped
+# launch of all four is 52 us (ViT-B) / 79 us (ViT-L) faster than four; in the step the MLP
+# weight gradients run faster where the DGELU GEMM has just written du (their operands still in
+# the caches), so 1 loses that and 3 keeps it: C3 kernel time per step 36.16 (0) / 36.35 (1) /
+# 36.00 ms (3), the out-projection's 28 slabs of 28 K-steps become 7 of 113.
+WGRAD_GROUP = int(os.environ.get("VITMI_WGRAD_GROUP", "3"))
+_WGRAD_GROUP = WGRAD_GROUP != 0
+
+
+def linear_wgrad_group(items) -> None:
+    """For each (dy[M, N_p], x[M, K_p], dw[N_p, K_p]) of ``items`` (at most 4, one row count M):
+    dw (fp32) += dy^T x, all in ONE split-K launch and one reduction (vitmi_linear_wgrad_group; the
+    weight gradients of one transformer block).  x may be row-strided (the hi part of a split
+    operand).  Mixed dtypes, other row counts or more than 4 items run one linear_wgrad each."""
+    items = [t for t in items if t is not None]
+    if not items:
+        return
+    if not _WGRAD_GROUP:   # (A/B switch: VITMI_WGRAD_GROUP=0 runs one launch per problem)
+        for dy, x, dw in items:
+            linear_wgrad(dy, x, dw)
+        return
+    M = items[0][0].numel() // items[0][0].shape[-1]
+    dt0 = items[0][0].dtype
+    if len(items) == 1 or len(items) > 4 or any(
+            dy.dtype != dt0 or x.dtype != dt0 or dy.numel() // dy.shape[-1] != M or not dy.is_contiguous()
+            or x.stride(-1) != 1 or dw.dtype != torch.float32 or not dw.is_contiguous() for dy, x, dw in items):
+        for dy, x, dw in items:
+            linear_wgrad(dy, x, dw)
+        return
+    n = len(items)
+    arr = lambda t, v: (t * n)(*v)  # noqa: E731
+    Ns = arr(ctypes.c_int64, [dy.shape[-1] for dy, _, _ in items])
+    Ks = arr(ctypes.c_int64, [x.shape[-1] for _, x, _ in items])
+    ws_n = lib().vitmi_linear_wgrad_group_workspace_size(dt(dt0), n, M, Ns, Ks)
+    ws = _ws(ws_n, items[0][0])
+    check(lib().vitmi_linear_wgrad_group(
+        dt(dt0), n, M, Ns, Ks, arr(ctypes.c_void_p, [_p(dy) for dy, _, _ in items]),
+        arr(ctypes.c_int64, [dy.shape[-1] for dy, _, _ in items]),
+        arr(ctypes.c_void_p, [_p(x) for _, x, _ in items]),
+        arr(ctypes.c_int64, [x.stride(0) if x.dim() == 2 else x.shape[-1] for _, x, _ in items]),
+        arr(ctypes.c_void_p, [_p(dw) for _, _, dw in items]), _p(ws), ws.numel(), _s()), "linear_wgrad_group")
 
 
 def bias_grad(dy: Tensor, db: Tensor) -> None:
