@@ -26,7 +26,6 @@ product is exact fp32 (f32-input MFMA).
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional
 
 import torch
