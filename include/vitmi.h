@@ -37,7 +37,7 @@ enum {
   VITMI_F64 = 2,    /* comm only */
   VITMI_BF16X3 = 3, /* vitmi_layernorm_fwd's y only: bf16 rows [hi | hi | lo] of 3D columns, the
                        split-bf16 A operand of the precision knob (vitmi_split_bf16x3) */
-  VITMI_BF16F8 = 4  /* the knob's cheaper form (ViTConfig dtype "bf16f8"): a row of K values is 4K
+  VITMI_BF16F8 = 4, /* the knob's cheaper form (ViTConfig dtype "bf16f8"): a row of K values is 4K
                        bytes (2K bf16 units), [hi = bf16(x) (K bf16) | OCP e4m3 part (2K bytes)],
                        the e4m3 part in 64-k blocks of 128 B, [hi8 | lo8] for an A operand
                        (activations) and [lo8 | hi8] for a weight, hi8 = e4m3(hi), lo8 =
@@ -46,6 +46,15 @@ enum {
                        GEMM runs K/64 bf16 K-steps (hi.hi) and K/64 block-scaled fp8 K-steps
                        (hi.lo + lo.hi, v_mfma_scale_f32_16x16x128_f8f6f4): 2K-equivalent MFMA
                        work instead of bf16x3's 3K.  Also vitmi_layernorm_fwd's y dtype. */
+  VITMI_BF16F8W = 5 /* the weight-side correction alone (the bf16f8 knob's qkv GEMM): a row of K values
+                       is 3K bytes (1.5K bf16 units), [hi = bf16(x) (K bf16) | one OCP e4m3 byte per
+                       k (K bytes)], the byte hi8 = e4m3(hi) for an A operand (activations) and lo8 =
+                       e4m3((x - hi) * 2^9) for a weight (vitmi_split_bf16f8 patterns 2 / 3; K % 128
+                       == 0).  vitmi_linear_fwd dtype (x and w both so): K/64 bf16 K-steps (hi.hi) and
+                       K/128 block-scaled fp8 K-steps (hi.lo_w only): 1.5K-equivalent work.  The qkv
+                       GEMM's error is its weight rounding's (q and k of every token move together);
+                       the activation side's averages out (tools/precision_sides.py).  Also
+                       vitmi_layernorm_fwd's y dtype (A-operand rows). */
 };
 
 /* GEMM epilogues (all apply `bias` (fp32, may be NULL) first where it applies) */
@@ -418,13 +427,18 @@ int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int64_t ld_src
                        int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
 /* VITMI_BF16F8 rows: src fp32 [rows][ld_src] (K % 64 == 0) -> dst [rows][ld_dst >= 2K bf16 units],
  * pattern 0 the A-operand layout (e4m3 blocks [hi8 | lo8]), pattern 1 the weight layout ([lo8 | hi8]);
- * hi_copy as above. */
+ * patterns 2 / 3: the VITMI_BF16F8W rows (ld_dst >= 1.5K bf16 units, K % 128 == 0), [hi | hi8] (A
+ * operand) / [hi | lo8] (weight); hi_copy as above. */
 int vitmi_split_bf16f8(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst, int64_t ld_dst,
                        int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream);
 /* Up to 8 dense weights (srcs[j] fp32 [rows[j]][K[j]]) to pattern-1 VITMI_BF16F8 rows (dsts[j]
  * [rows[j]][2 K[j]] bf16 units) in one launch (the knob's per-forward weight split). */
 int vitmi_split_bf16f8_weights(int n, const float* const* srcs, void* const* dsts, const int64_t* rows,
                                const int64_t* K, vitmi_stream_t stream);
+/* The same with a layout per weight: patterns[j] 1 (VITMI_BF16F8 rows, [rows][2K]) or 3
+ * (VITMI_BF16F8W rows [hi | lo8], [rows][1.5K], K % 128 == 0: the qkv weight of the bf16f8 knob). */
+int vitmi_split_bf16f8_weights_mixed(int n, const float* const* srcs, void* const* dsts, const int64_t* rows,
+                                     const int64_t* K, const int* patterns, vitmi_stream_t stream);
 
 /* fp32 -> bf16 cast of n elements (weight shadows for the bf16 MFMA path) */
 int vitmi_cast_f32_bf16(int64_t n, const float* src, void* dst, vitmi_stream_t stream);

@@ -126,6 +126,77 @@ def test_bf16f8_gemm_residual_and_bf16_out():
     assert torch.equal(yb, y.to(BF))
 
 
+def parts_w(y8, K):
+    """(hi bf16 [rows, K], e4m3 bytes [rows, K]) of VITMI_BF16F8W rows [rows, 1.5K] (one byte per k)."""
+    b = y8.contiguous().cpu().view(torch.uint8)[:, 2 * K:]
+    return y8[:, :K].cpu(), b
+
+
+@pytest.mark.parametrize("rows,K", [(197 * 3, 768), (37, 3072), (5, 128)])
+def test_split_bf16f8w_bytes(rows, K):
+    """vitmi_split_bf16f8 patterns 2 / 3 (VITMI_BF16F8W): [hi | hi8] and [hi | lo8], bit for bit the CPU
+    conversions, from a row-strided source with values over 2^-12 .. 2^10; and the mixed weight
+    splitter (one launch, a pattern per weight) gives the same rows as the single-tensor calls."""
+    g = torch.Generator().manual_seed(17)
+    mag = torch.exp2(torch.randint(-12, 11, (rows, K + 8), generator=g).float())
+    x = (rnd(rows, K + 8, seed=171) * mag).to(DEV)[:, 4:4 + K]
+    x = x.contiguous() if (x.data_ptr() % 16) else x
+    a8, hi = ops.split_bf16f8(x, 2, hi_copy=True)
+    w8, _ = ops.split_bf16f8(x, 3)
+    assert a8.shape == (rows, K + K // 2) and w8.shape == (rows, K + K // 2)
+    h, h8, l8 = ref_parts(x)
+    ah, a1 = parts_w(a8, K)
+    wh, w1 = parts_w(w8, K)
+    assert torch.equal(ah, h) and torch.equal(hi.cpu(), h) and torch.equal(wh, h)
+    assert torch.equal(a1, h8) and torch.equal(w1, l8)
+    xc = x.contiguous()
+    w_mix = ops.split_bf16f8_weights([xc, xc], [3, 1])
+    assert torch.equal(w_mix[0], w8) and torch.equal(w_mix[1], ops.split_bf16f8(xc, 1)[0])
+
+
+@pytest.mark.parametrize("M,D", [(197 * 3, 768), (37, 256), (5, 1024)])
+def test_layernorm_fwd_writes_f8w_rows(M, D):
+    """layernorm_fwd with out_dtype BF16F8W: what split_bf16f8(.., 2) makes of the fp32 kernel's y."""
+    x = (rnd(M, D + 4, seed=195) * 2 + 0.5).to(DEV)[:, :D]
+    w = (1 + 0.3 * rnd(D, seed=196)).to(DEV)
+    b = (0.2 * rnd(D, seed=197)).to(DEV)
+    y8, m8, r8 = ops.layernorm_fwd(x, w, b, 1e-6, ops.BF16F8W)
+    yf, mf, rf = ops.layernorm_fwd(x, w, b, 1e-6, torch.float32)
+    ref, _ = ops.split_bf16f8(yf, 2)
+    assert y8.shape == (M, D + D // 2) and torch.equal(y8, ref)
+    assert torch.equal(m8, mf) and torch.equal(r8, rf)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 320, 256), (197 * 4, 2304, 768), (25600, 768, 768)])
+def test_bf16f8w_gemm(M, N, K):
+    """The weight-side form (VITMI_BF16F8W, the knob's qkv GEMM): K/64 bf16 K-steps, then K/128 e4m3
+    K-steps of hi8(x) . lo8(w) / 2^9.  Against that product emulated in fp64 from the CPU parts, and
+    against the exact product: it removes the weight rounding's share of the plain bf16 GEMM's
+    error (x's rounding stays).  (300, 320, 256): ragged M with the switch inside a unit; (25600,
+    768, 768): the tail split."""
+    x = rnd(M, K, seed=292).to(DEV)
+    w = (rnd(N, K, seed=293) * 0.05).to(DEV)
+    b = (rnd(N, seed=294) * 0.1).to(DEV)
+    x8, _ = ops.split_bf16f8(x, 2)
+    w8, _ = ops.split_bf16f8(w, 3)
+    y = ops.linear_fwd(x8, w8, b, torch.float32, f8="w").double().cpu()
+    xh, x8h, _ = ref_parts(x)
+    wh, _, w8l = ref_parts(w)
+    emu = xh.double() @ wh.double().t() + (deq(x8h) @ deq(w8l).t()) / 512.0 + b.double().cpu()
+    xb = xh.double()
+    half = xb @ w.double().cpu().t() + b.double().cpu()       # x rounded, w exact
+    scale = half.norm()
+    e_emu = ((y - emu).norm() / scale).item()
+    e_half = ((y - half).norm() / scale).item()
+    y1 = ops.linear_fwd(x.to(BF), w.to(BF), b, torch.float32).double().cpu()
+    e_plain = ((y1 - half).norm() / scale).item()
+    print(f"bf16f8w GEMM {M}x{N}x{K}: vs emulation {e_emu:.2e}, vs (bf16 x) . (fp32 w) {e_half:.2e}, plain {e_plain:.2e}")
+    assert e_emu < 1e-5, e_emu
+    assert e_half < 2e-4 and e_plain > 5 * e_half, (e_half, e_plain)
+    yb = ops.linear_fwd(x8, w8, b, BF, f8="w")
+    assert torch.equal(yb.cpu(), y.float().to(BF))
+
+
 @pytest.mark.parametrize("M,N,K", [(197 * 8, 3072, 768), (50, 256, 192)])
 def test_linear_fwd_gelu_split_f8(M, N, K):
     """VITMI_EPI_SPLIT_F8: the fc1 epilogue writes gelu(u) as VITMI_BF16F8 A-operand rows.  hi8 is

@@ -1793,14 +1793,19 @@ static int gemm_impl(int dtype, int ak, int bk, int64_t M, int64_t N, int64_t K,
   epi &= ~(VITMI_EPI_AUX_TILED | VITMI_EPI_SPLIT_X3 | VITMI_EPI_SPLIT_F8);
   // VITMI_BF16F8: rows of 2K bf16 units ([hi | e4m3 parts]); the kernel sees bf16 operands over
   // K' = 2K with the e4m3 K-steps from K/64 on (GemmArgs::k8)
-  const bool f8 = dtype == VITMI_BF16F8;
+  // VITMI_BF16F8W (the weight-side correction alone): rows of 1.5K bf16 units [hi | one e4m3 byte per
+  // k]; K' = 1.5K with the K/128 e4m3 K-steps (128 k each: hi8 of x against lo8 of w) from K/64 on
+  const bool f8w = dtype == VITMI_BF16F8W;
+  const bool f8 = dtype == VITMI_BF16F8 || f8w;
   int64_t k8 = 0;
   if (f8) {
     VITMI_CHECK_ARG(ak && bk && !allow_split, "gemm: VITMI_BF16F8 operands: forward linear layers (k-major A and B) only");
-    VITMI_CHECK_ARG(K % 64 == 0 && N % 16 == 0, "gemm: VITMI_BF16F8 needs K %% 64 == 0 and N %% 16 == 0");
-    VITMI_CHECK_ARG(lda >= 2 * K && ldb >= 2 * K, "gemm: VITMI_BF16F8 rows are 2K bf16 units (lda, ldb >= 2K)");
+    VITMI_CHECK_ARG(K % (f8w ? 128 : 64) == 0 && N % 16 == 0, "gemm: VITMI_BF16F8%s needs K %% %d == 0 and N %% 16 == 0",
+                    f8w ? "W" : "", f8w ? 128 : 64);
+    const int64_t kr = f8w ? K + K / 2 : 2 * K;
+    VITMI_CHECK_ARG(lda >= kr && ldb >= kr, "gemm: VITMI_BF16F8 rows are 2K (VITMI_BF16F8W: 1.5K) bf16 units");
     k8 = K / 64;
-    K *= 2;
+    K = kr;
     dtype = VITMI_BF16;
   }
   if (sf8) {
@@ -2121,6 +2126,7 @@ extern "C" size_t vitmi_aux_tiled_bytes(int64_t rows, int64_t cols) {
 
 extern "C" size_t vitmi_linear_fwd_workspace_size(int dtype, int64_t M, int64_t N, int64_t K) {
   if (dtype == VITMI_BF16F8) return tail_ws_bytes(M, N, 2 * K);   // (K' = 2K bf16 units)
+  if (dtype == VITMI_BF16F8W) return tail_ws_bytes(M, N, K + K / 2);
   return use256(dtype, M, N) ? tail_ws_bytes(M, N, K) : 0;
 }
 
@@ -2132,7 +2138,7 @@ extern "C" int vitmi_linear_fwd(int dtype, int64_t M, int64_t N, int64_t K, cons
   VITMI_CHECK_ARG(eb == VITMI_EPI_STORE || eb == VITMI_EPI_BIAS_GELU || eb == VITMI_EPI_RESIDUAL,
                   "linear_fwd: bad epilogue %d", epilogue);
   const int64_t ldy = (epilogue & VITMI_EPI_SPLIT_X3) ? 3 * N : (epilogue & VITMI_EPI_SPLIT_F8) ? 2 * N : N;
-  const int64_t ldk = dtype == VITMI_BF16F8 ? 2 * K : K;   // VITMI_BF16F8 rows: 2K bf16 units
+  const int64_t ldk = dtype == VITMI_BF16F8 ? 2 * K : dtype == VITMI_BF16F8W ? K + K / 2 : K;   // (bf16 units)
   return gemm_impl(dtype, 1, 1, M, N, K, x, ldk, w, ldk, y, ldy, y_dtype, epilogue, bias, aux, N,
                    residual, N, workspace, ws_bytes, (hipStream_t)stream, false);
 }

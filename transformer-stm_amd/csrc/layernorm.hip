@@ -48,6 +48,8 @@ __device__ __forceinline__ f32x4 load4<bf16>(const bf16* p) {
 struct SplitX3 {};
 // ... and of the VITMI_BF16F8 knob: rows of 2D bf16 units, [hi | hi8 | lo8] (common.h split_f8)
 struct SplitF8 {};
+// ... and of its weight-side form (VITMI_BF16F8W): rows of 1.5D bf16 units, [hi | hi8] (one byte per k)
+struct SplitF8W {};
 
 template <int NV, typename TY>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const float* __restrict__ x,
@@ -105,6 +107,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t M, int D, const flo
         uint8_t* f8 = (uint8_t*)(yr + D) + f8_off(c);
         *(uint32_t*)f8 = hi8;
         *(uint32_t*)(f8 + 64) = lo8;
+      } else if constexpr (std::is_same_v<TY, SplitF8W>) {
+        bf16* yr = (bf16*)y + row * ldy;
+        bf16x4 hi;
+        uint32_t hi8, lo8;
+        split_f8(o, hi, hi8, lo8);
+        put((bf16x4*)(yr + c), hi);
+        *(uint32_t*)((uint8_t*)(yr + D) + c) = hi8;
       } else {
         store4<TY>(y + row * ldy + c, o);
       }
@@ -331,6 +340,12 @@ static void ln_fwd_launch(hipStream_t s, int64_t M, int D, const float* x, int64
     VITMI_STAT((ln_fwd_kernel<NV, SplitF8>), 0, (double)M * D * (4 + 4) + 8.0 * M);
     return;
   }
+  if (ydt == VITMI_BF16F8W) {
+    hipLaunchKernelGGL((ln_fwd_kernel<NV, SplitF8W>), grid, dim3(256), 0, s, M, D, x, ldx, gamma, beta, eps,
+                       (SplitF8W*)y, ldy, mean, rstd);
+    VITMI_STAT((ln_fwd_kernel<NV, SplitF8W>), 0, (double)M * D * (4 + 3) + 8.0 * M);
+    return;
+  }
   if (ydt == VITMI_BF16)
     hipLaunchKernelGGL((ln_fwd_kernel<NV, bf16>), grid, dim3(256), 0, s, M, D, x, ldx, gamma, beta,
                        eps, (bf16*)y, ldy, mean, rstd);
@@ -372,18 +387,23 @@ extern "C" int vitmi_layernorm_fwd(int64_t M, int D, const float* x, int64_t ldx
                                    vitmi_stream_t stream) {
   VITMI_CHECK_ARG(D > 0 && D % 4 == 0 && D <= 2048, "layernorm: D must be a multiple of 4 in [4, 2048]");
   VITMI_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "layernorm: strides must be multiples of 4");
-  VITMI_CHECK_ARG(y_dtype == VITMI_F32 || y_dtype == VITMI_BF16 || y_dtype == VITMI_BF16X3 || y_dtype == VITMI_BF16F8,
-                  "layernorm_fwd: y dtype must be VITMI_F32, VITMI_BF16, VITMI_BF16X3 or VITMI_BF16F8");
-  VITMI_CHECK_ARG(ldx >= D && ldy >= (y_dtype == VITMI_BF16X3 ? 3LL * D : y_dtype == VITMI_BF16F8 ? 2LL * D : (int64_t)D),
-                  "layernorm_fwd: ldx >= D and ldy >= D (3D for VITMI_BF16X3, 2D for VITMI_BF16F8) required");
+  VITMI_CHECK_ARG(y_dtype == VITMI_F32 || y_dtype == VITMI_BF16 || y_dtype == VITMI_BF16X3 || y_dtype == VITMI_BF16F8 ||
+                      y_dtype == VITMI_BF16F8W,
+                  "layernorm_fwd: y dtype must be VITMI_F32, VITMI_BF16, VITMI_BF16X3, VITMI_BF16F8 or VITMI_BF16F8W");
+  VITMI_CHECK_ARG(ldx >= D && ldy >= (y_dtype == VITMI_BF16X3 ? 3LL * D : y_dtype == VITMI_BF16F8 ? 2LL * D
+                                      : y_dtype == VITMI_BF16F8W ? 3LL * D / 2 : (int64_t)D),
+                  "layernorm_fwd: ldx >= D and ldy >= D (3D for VITMI_BF16X3, 2D for VITMI_BF16F8, 1.5D for "
+                  "VITMI_BF16F8W) required");
   VITMI_CHECK_ARG(y_dtype != VITMI_BF16F8 || D % 64 == 0, "layernorm_fwd: VITMI_BF16F8 needs D %% 64 == 0");
+  VITMI_CHECK_ARG(y_dtype != VITMI_BF16F8W || D % 128 == 0, "layernorm_fwd: VITMI_BF16F8W needs D %% 128 == 0");
   if (M == 0) return VITMI_OK;
   VITMI_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: null pointer");
   hipStream_t s = (hipStream_t)stream;
 #ifndef VITMI_LN_FWD_SMALL
 #define VITMI_LN_FWD_SMALL 1
 #endif
-  if (VITMI_LN_FWD_SMALL && (D == 64 || D == 128) && y_dtype != VITMI_BF16X3 && y_dtype != VITMI_BF16F8) {
+  if (VITMI_LN_FWD_SMALL && (D == 64 || D == 128) && y_dtype != VITMI_BF16X3 && y_dtype != VITMI_BF16F8 &&
+      y_dtype != VITMI_BF16F8W) {
     const int rw = 64 / (D / 4);
     const dim3 grid((unsigned)((M + 4 * rw - 1) / (4 * rw)));
     if (D == 64) {

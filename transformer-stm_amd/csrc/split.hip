@@ -61,9 +61,13 @@ __global__ __launch_bounds__(256) void split_f8_kernel(int64_t rows, int64_t K, 
     split_f8(*(const f32x4*)(src + r * ld_src + c), hi, hi8, lo8);
     bf16* d = dst + r * ld_dst;
     *(bf16x4*)(d + c) = hi;
-    uint8_t* f8 = (uint8_t*)(d + K) + f8_off(c);   // (common.h: 64-k blocks, [first | second])
-    *(uint32_t*)f8 = pattern == 0 ? hi8 : lo8;
-    *(uint32_t*)(f8 + 64) = pattern == 0 ? lo8 : hi8;
+    if (pattern >= 2) {   // VITMI_BF16F8W: one byte per k, hi8 (A) or lo8 (weight)
+      *(uint32_t*)((uint8_t*)(d + K) + c) = pattern == 2 ? hi8 : lo8;
+    } else {
+      uint8_t* f8 = (uint8_t*)(d + K) + f8_off(c);   // (common.h: 64-k blocks, [first | second])
+      *(uint32_t*)f8 = pattern == 0 ? hi8 : lo8;
+      *(uint32_t*)(f8 + 64) = pattern == 0 ? lo8 : hi8;
+    }
     if (copy) *(bf16x4*)(copy + r * ld_copy + c) = hi;
   }
 }
@@ -75,6 +79,7 @@ struct SplitBatch {
   bf16* dst[8];
   int64_t K[8];
   int64_t start[9];   // prefix sums of rows * K / 4 (thread items)
+  int pat[8];         // 1: VITMI_BF16F8 weight rows [hi | lo8, hi8 blocks]; 3: VITMI_BF16F8W [hi | lo8]
   int n;
 };
 __global__ __launch_bounds__(256) void split_f8_batch_kernel(SplitBatch b) {
@@ -87,6 +92,12 @@ __global__ __launch_bounds__(256) void split_f8_batch_kernel(SplitBatch b) {
     bf16x4 hi;
     uint32_t hi8, lo8;
     split_f8(*(const f32x4*)(b.src[j] + r * K + c), hi, hi8, lo8);
+    if (b.pat[j] == 3) {
+      bf16* d = b.dst[j] + r * (K + K / 2);
+      *(bf16x4*)(d + c) = hi;
+      *(uint32_t*)((uint8_t*)(d + K) + c) = lo8;
+      continue;
+    }
     bf16* d = b.dst[j] + r * 2 * K;
     *(bf16x4*)(d + c) = hi;
     uint8_t* f8 = (uint8_t*)(d + K) + f8_off(c);
@@ -122,13 +133,17 @@ extern "C" int vitmi_split_bf16x3(int64_t rows, int64_t K, const float* src, int
   return VITMI_OK;
 }
 
-extern "C" int vitmi_split_bf16f8_weights(int n, const float* const* srcs, void* const* dsts, const int64_t* rows,
-                                          const int64_t* K, vitmi_stream_t stream) {
+extern "C" int vitmi_split_bf16f8_weights_mixed(int n, const float* const* srcs, void* const* dsts,
+                                                const int64_t* rows, const int64_t* K, const int* patterns,
+                                                vitmi_stream_t stream) {
   VITMI_CHECK_ARG(n >= 1 && n <= 8 && srcs && dsts && rows && K, "split_bf16f8_weights: 1..8 weights");
   SplitBatch b{};
   b.n = n;
   for (int j = 0; j < n; ++j) {
-    VITMI_CHECK_ARG(rows[j] > 0 && K[j] > 0 && K[j] % 64 == 0, "split_bf16f8_weights: weight %d: K %% 64 and rows", j);
+    b.pat[j] = patterns ? patterns[j] : 1;
+    VITMI_CHECK_ARG(b.pat[j] == 1 || b.pat[j] == 3, "split_bf16f8_weights: weight %d: pattern must be 1 or 3", j);
+    VITMI_CHECK_ARG(rows[j] > 0 && K[j] > 0 && K[j] % (b.pat[j] == 3 ? 128 : 64) == 0,
+                    "split_bf16f8_weights: weight %d: K %% %d and rows", j, b.pat[j] == 3 ? 128 : 64);
     VITMI_CHECK_ARG(srcs[j] && dsts[j] && ((uintptr_t)srcs[j] % 16) == 0 && ((uintptr_t)dsts[j] % 16) == 0,
                     "split_bf16f8_weights: weight %d: null or unaligned pointer", j);
     b.src[j] = srcs[j];
@@ -142,12 +157,20 @@ extern "C" int vitmi_split_bf16f8_weights(int n, const float* const* srcs, void*
   return VITMI_OK;
 }
 
+extern "C" int vitmi_split_bf16f8_weights(int n, const float* const* srcs, void* const* dsts, const int64_t* rows,
+                                          const int64_t* K, vitmi_stream_t stream) {
+  return vitmi_split_bf16f8_weights_mixed(n, srcs, dsts, rows, K, nullptr, stream);
+}
+
 extern "C" int vitmi_split_bf16f8(int64_t rows, int64_t K, const float* src, int64_t ld_src, void* dst,
                                   int64_t ld_dst, int pattern, void* hi_copy, int64_t ld_copy, vitmi_stream_t stream) {
-  VITMI_CHECK_ARG(rows >= 0 && K > 0 && K % 64 == 0, "split_bf16f8: K must be a positive multiple of 64");
-  VITMI_CHECK_ARG(pattern == 0 || pattern == 1, "split_bf16f8: pattern must be 0 (A: [hi|hi8|lo8]) or 1 (W: [hi|lo8|hi8])");
-  VITMI_CHECK_ARG(ld_src >= K && ld_src % 4 == 0 && ld_dst >= 2 * K && ld_dst % 4 == 0,
-                  "split_bf16f8: strides must be multiples of 4, ld_src >= K, ld_dst >= 2K (bf16 units)");
+  VITMI_CHECK_ARG(pattern >= 0 && pattern <= 3, "split_bf16f8: pattern must be 0 (A: [hi|hi8|lo8]), 1 (W: "
+                  "[hi|lo8|hi8]), 2 (A: [hi|hi8]) or 3 (W: [hi|lo8])");
+  VITMI_CHECK_ARG(rows >= 0 && K > 0 && K % (pattern >= 2 ? 128 : 64) == 0,
+                  "split_bf16f8: K must be a positive multiple of %d", pattern >= 2 ? 128 : 64);
+  VITMI_CHECK_ARG(ld_src >= K && ld_src % 4 == 0 && ld_dst >= (pattern >= 2 ? K + K / 2 : 2 * K) && ld_dst % 4 == 0,
+                  "split_bf16f8: strides must be multiples of 4, ld_src >= K, ld_dst >= 2K (1.5K for patterns 2 / 3; "
+                  "bf16 units)");
   VITMI_CHECK_ARG(!hi_copy || (ld_copy >= K && ld_copy % 4 == 0), "split_bf16f8: bad ld_copy");
   if (rows == 0) return VITMI_OK;
   VITMI_CHECK_ARG(src && dst, "split_bf16f8: null pointer");

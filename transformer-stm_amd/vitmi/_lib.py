@@ -64,6 +64,7 @@ SIGNATURES = {
     "vitmi_split_bf16x3": (I, [L, L, P, L, P, L, I, P, L, P]),
     "vitmi_split_bf16f8": (I, [L, L, P, L, P, L, I, P, L, P]),
     "vitmi_split_bf16f8_weights": (I, [I, P, P, P, P, P]),
+    "vitmi_split_bf16f8_weights_mixed": (I, [I, P, P, P, P, P, P]),
     "vitmi_fold_begin": (I, []),
     "vitmi_fold_end": (I, [P]),
     "vitmi_dropout_hash": (U, [U, U, U, U]),

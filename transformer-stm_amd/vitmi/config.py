@@ -54,10 +54,11 @@ class ViTConfig:
     # product: 2K- instead of 3K-equivalent forward GEMM work, include/vitmi.h VITMI_BF16F8)
     # or 'fp32' (f32-input MFMA, exact fp32 products)
     dtype: str = "bf16"
-    # the precision knobs' qkv GEMM on split operands (True) or plain bf16 (False); None = the
-    # knob's default: split for 'bf16x3', plain for 'bf16f8' (q, k, v are rounded to bf16 right
-    # after that GEMM: vitmi/modules.py Block.split_qkv)
-    split_qkv: "bool | None" = None
+    # the precision knobs' qkv GEMM on split operands (True), plain bf16 (False) or, for 'bf16f8',
+    # with the weight-side correction alone ("weight": VITMI_BF16F8W, needs embed_dim % 128 == 0);
+    # None = the knob's default: split for 'bf16x3', "weight" for 'bf16f8' (plain where
+    # embed_dim % 128 != 0).  vitmi/modules.py Block.split_qkv
+    split_qkv: "bool | str | None" = None
 
     @property
     def grid(self) -> int:

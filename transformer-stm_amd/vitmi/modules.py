@@ -320,12 +320,15 @@ class Block(nn.Module):
             self.norm2 = LayerNorm(dim, eps)
         self.mlp = Mlp(dim, int(dim * mlp_ratio), dtype)
         self.dtype = dtype
-        # the precision knobs' qkv GEMM: split operands (True) or plain bf16 (False).  q, k and v
-        # are rounded to bf16 right after it, so its corrections buy little: depth-12 logits
-        # 1.8e-4 -> 6.4e-4 (random init) / 2.3e-4 -> 7.5e-4 (default init) for 'bf16f8' in
-        # emulation (tools/precision_emulate_fp8.py --classes).  Default: split for 'bf16x3', plain
-        # for 'bf16f8' (ViTConfig.split_qkv overrides)
-        self.split_qkv = dtype == "bf16x3"
+        # the precision knobs' qkv GEMM: split operands (True), plain bf16 (False) or, for 'bf16f8',
+        # the weight-side correction alone ("weight", VITMI_BF16F8W).  Of the qkv GEMM's error, the
+        # weight rounding's is the part that matters (every token's q and k move together; the
+        # activations' rounding averages out): depth-12 ViT-B logits over 8 images, RMS / max, 1.7e-4
+        # / 3.4e-4 with "weight" against 3.4e-4 / 7.1e-4 plain, smoke model 1.8e-4 against 9.6e-4
+        # (tools/precision_sides.py, profiles/r06_sides/), at 1.5K- instead of 2K-equivalent work.
+        # Default: split for 'bf16x3', "weight" for 'bf16f8' where dim % 128 == 0 (else plain);
+        # ViTConfig.split_qkv overrides
+        self.split_qkv = True if dtype == "bf16x3" else ("weight" if dtype == "bf16f8" and dim % 128 == 0 else False)
         self.eps = eps
         self.drop_rate = 0.0     # set by VisionTransformer / the caller (Keras default 0.1)
         self.drop_seed: Optional[int] = None   # fixed seed (tests); None = drawn per forward
@@ -399,9 +402,12 @@ class _BlockFn(torch.autograd.Function):
         product, 2K-equivalent MFMA work instead of 3K (emulated 1.8-2.3e-4 at depth 12).
 
         blk.split_qkv False: the qkv GEMM runs on plain bf16 operands (LN1 writes bf16, the
-        weight's bf16 shadow); the other three GEMMs as above."""
+        weight's bf16 shadow); "weight" ('bf16f8'): LN1 writes VITMI_BF16F8W rows [hi | hi8] and the
+        weight is split [hi | lo8], so the GEMM adds hi8 . lo8 / 2^9 to hi . hi (the weight-side
+        correction alone, K/128 e4m3 K-steps); the other three GEMMs as above."""
         f8 = blk.dtype == "bf16f8"
-        sq = blk.split_qkv
+        sq = blk.split_qkv is True
+        wq8 = f8 and blk.split_qkv == "weight" and D % 128 == 0
         if drop is not None:
             raise ValueError(f"vitmi: dtype '{blk.dtype}' is the parity / evaluation knob; dropout is not supported")
         n1, n2 = blk.norm1, blk._norm2
@@ -409,15 +415,18 @@ class _BlockFn(torch.autograd.Function):
         split = ops.split_bf16f8 if f8 else ops.split_bf16x3
         ln_out = ops.BF16F8 if f8 else ops.BF16X3
 
-        weights = ((a_.qkv.weight,) if sq else ()) + (a_.proj.weight, mlp.fc1.weight, mlp.fc2.weight)
+        weights = ((a_.qkv.weight,) if sq or wq8 else ()) + (a_.proj.weight, mlp.fc1.weight, mlp.fc2.weight)
         if f8:   # the block's split weights in one launch
-            split_w = dict(zip(map(id, weights), ops.split_bf16f8_weights(weights)))
+            pats = [3 if wq8 and i == 0 else 1 for i in range(len(weights))]
+            split_w = dict(zip(map(id, weights), ops.split_bf16f8_weights(weights, pats)))
 
         def w3(p):
             return split_w[id(p)] if f8 else split(p.detach(), 1)[0]
-        h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps, ln_out if sq else torch.bfloat16)
-        # the qkv GEMM's operands: split, or plain bf16 (h1 and the weight's bf16 shadow)
-        qa, qw, qf8 = (h1_3, w3(a_.qkv.weight), f8) if sq else (h1_3, wlp[0], False)
+        h1_3, m1, r1 = ops.layernorm_fwd(x2, n1.weight, n1.bias, blk.eps,
+                                         ln_out if sq else ops.BF16F8W if wq8 else torch.bfloat16)
+        # the qkv GEMM's operands: split, weight-side split, or plain bf16 (h1 and the weight's bf16 shadow)
+        qa, qw, qf8 = ((h1_3, w3(a_.qkv.weight), f8) if sq else (h1_3, split_w[id(a_.qkv.weight)], "w") if wq8
+                       else (h1_3, wlp[0], False))
         if N <= ops.ATTN_SEQ_MAX:   # q, k, v leave the GEMM epilogue in bf16
             qkv = ops.linear_fwd(qa, qw, a_.qkv.bias, torch.bfloat16, f8=qf8)
             o, o3, lse = (ops.attention_fwd_f8 if f8 else ops.attention_fwd_x3)(qkv, B, N, H, a_.scale)
@@ -438,7 +447,7 @@ class _BlockFn(torch.autograd.Function):
                                   aux_tiled=True, split_x3=not f8, split_f8=f8, f8=f8)
         out = ops.linear_fwd(act3, w3(mlp.fc2.weight), mlp.fc2.bias, F32, ops.EPI_RESIDUAL, residual=x1, f8=f8)
         # the bf16 backward's operands: hi parts of the split activations (row-strided views)
-        h1, h2, act = (h1_3[:, :D] if sq else h1_3), h2_3[:, :D], act3[:, :mlp.fc1.weight.shape[0]]
+        h1, h2, act = (h1_3[:, :D] if sq or wq8 else h1_3), h2_3[:, :D], act3[:, :mlp.fc1.weight.shape[0]]
         ctx.aux_tiled = True
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dg, act, *wlp)
         return out

@@ -24,6 +24,7 @@ EPI_AUX_TILED = 0x100   # gelu' in the library's tile-native layout (include/vit
 EPI_SPLIT_X3 = 0x200    # BIAS_GELU output as [hi | hi | lo] rows (the precision knob)
 EPI_SPLIT_F8 = 0x400    # BIAS_GELU output as VITMI_BF16F8 A-operand rows (the knob's bf16f8 form)
 BF16F8_DT = 4           # VITMI_BF16F8: rows of 2K bf16 units, [hi | e4m3 parts] (include/vitmi.h)
+BF16F8W_DT = 5          # VITMI_BF16F8W: rows of 1.5K bf16 units, [hi | hi8 (A) or lo8 (weight)]
 LOSS_CE, LOSS_MSE = 0, 1
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
@@ -117,7 +118,7 @@ def dropout_params(p: float):
 
 def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dtype,
                epilogue: int = EPI_STORE, residual: Optional[Tensor] = None, dropout=None,
-               aux_tiled: bool = False, split_x3: bool = False, f8: bool = False, split_f8: bool = False):
+               aux_tiled: bool = False, split_x3: bool = False, f8=False, split_f8: bool = False):
     """y = x W^T + b (+GELU, +residual).  x [M,K], w [N,K] (same dtype).  Returns y
     (and gelu'(pre-activation), the saved GELU derivative, for EPI_BIAS_GELU).
     ``dropout`` = (seed, site, rate) fuses the dropout of the GELU output / of the branch
@@ -127,14 +128,20 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
     ``split_x3`` (EPI_BIAS_GELU, bf16): y is [M, 3N], each row [hi | hi | lo] of the fp32 GELU
     output (VITMI_EPI_SPLIT_X3, the precision knob's fc2 A operand).
     ``f8``: x [M, 2K] and w [N, 2K] are VITMI_BF16F8 rows (split_bf16f8 patterns 0 / 1; the bf16f8
-    knob); ``split_f8`` (with f8, EPI_BIAS_GELU): y is [M, 2N] in the A-operand layout."""
+    knob); ``split_f8`` (with f8, EPI_BIAS_GELU): y is [M, 2N] in the A-operand layout.
+    ``f8="w"``: x [M, 1.5K] and w [N, 1.5K] are VITMI_BF16F8W rows (patterns 2 / 3: the weight-side
+    correction alone, the knob's qkv GEMM)."""
     assert x.is_contiguous() and w.is_contiguous() and x.dtype == w.dtype
     M, K = x.numel() // x.shape[-1], x.shape[-1]
     N = w.shape[0]
     assert w.shape[1] == K
     assert not split_x3 or (epilogue == EPI_BIAS_GELU and dropout is None)
     assert not split_f8 or (f8 and epilogue == EPI_BIAS_GELU and dropout is None)
-    if f8:
+    f8w = f8 == "w"
+    if f8w:
+        assert x.dtype == torch.bfloat16 and K % 3 == 0 and dropout is None and not split_f8
+        K = K * 2 // 3
+    elif f8:
         assert x.dtype == torch.bfloat16 and K % 2 == 0 and dropout is None
         K //= 2
     y = torch.empty(*x.shape[:-1], 3 * N if split_x3 else 2 * N if split_f8 else N, dtype=out_dtype,
@@ -156,7 +163,7 @@ def linear_fwd(x: Tensor, w: Tensor, bias: Optional[Tensor], out_dtype: torch.dt
     if probe:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    xdt = BF16F8_DT if f8 else dt(x.dtype)
+    xdt = BF16F8W_DT if f8w else BF16F8_DT if f8 else dt(x.dtype)
     nws = lib().vitmi_linear_fwd_workspace_size(xdt, M, N, K)
     ws = _ws(nws, x) if nws else None
     if dropout is not None and dropout[2] > 0:
@@ -308,22 +315,24 @@ def gemm(a: Tensor, b: Tensor, a_kmajor: bool, b_kmajor: bool, M: int, N: int, K
 # ---------------------------------------------------------------- LayerNorm
 BF16X3 = "bf16x3"   # layernorm_fwd out_dtype of the precision knob (VITMI_BF16X3)
 BF16F8 = "bf16f8"   # ... of its bf16f8 form (VITMI_BF16F8 A-operand rows)
+BF16F8W = "bf16f8w"  # ... and of the weight-side form (VITMI_BF16F8W A-operand rows [hi | hi8])
 ATTN_SEQ_MAX = 256  # largest N of the whole-sequence attention kernels (csrc/attention.hip SEQ_MAX)
 
 
 def layernorm_fwd(x: Tensor, w: Tensor, b: Tensor, eps: float, out_dtype):
     """x fp32 [..., D] (rows may be strided) -> (y [rows, D] contiguous, mean, rstd).
     out_dtype BF16X3: y is bf16 [rows, 3D], each row [hi | hi | lo] of the fp32 result;
-    BF16F8: y is [rows, 2D] bf16 units, each row the VITMI_BF16F8 A-operand layout."""
+    BF16F8: y is [rows, 2D] bf16 units, each row the VITMI_BF16F8 A-operand layout; BF16F8W: [rows,
+    1.5D], the VITMI_BF16F8W A-operand rows [hi | hi8]."""
     assert x.dtype == torch.float32
     M, ldx = _rows(x)
     D = x.shape[-1]
-    x3, f8 = out_dtype == BF16X3, out_dtype == BF16F8
-    width = 3 * D if x3 else 2 * D if f8 else D
-    y = torch.empty(M, width, dtype=torch.bfloat16 if x3 or f8 else out_dtype, device=x.device)
+    x3, f8, f8w = out_dtype == BF16X3, out_dtype == BF16F8, out_dtype == BF16F8W
+    width = 3 * D if x3 else 2 * D if f8 else D + D // 2 if f8w else D
+    y = torch.empty(M, width, dtype=torch.bfloat16 if x3 or f8 or f8w else out_dtype, device=x.device)
     mean = torch.empty(M, dtype=torch.float32, device=x.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x.device)
-    code = 3 if x3 else BF16F8_DT if f8 else dt(out_dtype)
+    code = 3 if x3 else BF16F8_DT if f8 else BF16F8W_DT if f8w else dt(out_dtype)
     check(lib().vitmi_layernorm_fwd(M, D, _p(x), ldx, _p(w), _p(b), float(eps), _p(y), code,
                                     y.shape[1], _p(mean), _p(rstd), _s()), "layernorm_fwd")
     return y, mean, rstd
@@ -581,19 +590,23 @@ def split_bf16x3(x: Tensor, pattern: int, hi_copy: bool = False):
     return x3, hi
 
 
-def split_bf16f8_weights(ws):
-    """Dense fp32 weights [N_j, K_j] (up to 8) -> their pattern-1 VITMI_BF16F8 rows [N_j, 2 K_j], one
-    launch (vitmi_split_bf16f8_weights)."""
-    import ctypes
+def split_bf16f8_weights(ws, patterns=None):
+    """Dense fp32 weights [N_j, K_j] (up to 8) -> their pattern-1 VITMI_BF16F8 rows [N_j, 2 K_j] (or,
+    where patterns[j] == 3, VITMI_BF16F8W rows [hi | lo8] [N_j, 1.5 K_j]), one launch
+    (vitmi_split_bf16f8_weights_mixed)."""
     ws = [w.detach() for w in ws]
     n = len(ws)
-    assert 1 <= n <= 8 and all(w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2 for w in ws)
-    outs = [torch.empty(w.shape[0], 2 * w.shape[1], dtype=torch.bfloat16, device=w.device) for w in ws]
+    pats = list(patterns) if patterns is not None else [1] * n
+    assert 1 <= n <= 8 and len(pats) == n and all(
+        w.dtype == torch.float32 and w.is_contiguous() and w.dim() == 2 for w in ws)
+    outs = [torch.empty(w.shape[0], (w.shape[1] * 3 // 2) if p == 3 else 2 * w.shape[1], dtype=torch.bfloat16,
+                        device=w.device) for w, p in zip(ws, pats)]
     srcs = (ctypes.c_void_p * n)(*[_p(w) for w in ws])
     dsts = (ctypes.c_void_p * n)(*[_p(o) for o in outs])
     rows = (ctypes.c_int64 * n)(*[w.shape[0] for w in ws])
     ks = (ctypes.c_int64 * n)(*[w.shape[1] for w in ws])
-    check(lib().vitmi_split_bf16f8_weights(n, srcs, dsts, rows, ks, _s()), "split_bf16f8_weights")
+    check(lib().vitmi_split_bf16f8_weights_mixed(n, srcs, dsts, rows, ks, (ctypes.c_int * n)(*pats), _s()),
+          "split_bf16f8_weights")
     return outs
 
 
@@ -604,9 +617,10 @@ def split_bf16f8(x: Tensor, pattern: int, hi_copy: bool = False):
     assert x.dtype == torch.float32
     rows, ld = _rows(x)
     K = x.shape[-1]
-    x8 = torch.empty(rows, 2 * K, dtype=torch.bfloat16, device=x.device)
+    width = K + K // 2 if pattern >= 2 else 2 * K   # patterns 2 / 3: VITMI_BF16F8W [hi | hi8] / [hi | lo8]
+    x8 = torch.empty(rows, width, dtype=torch.bfloat16, device=x.device)
     hi = torch.empty(rows, K, dtype=torch.bfloat16, device=x.device) if hi_copy else None
-    check(lib().vitmi_split_bf16f8(rows, K, _p(x), ld, _p(x8), 2 * K, int(pattern), _p(hi), K, _s()),
+    check(lib().vitmi_split_bf16f8(rows, K, _p(x), ld, _p(x8), width, int(pattern), _p(hi), K, _s()),
           "split_bf16f8")
     return x8, hi
 
