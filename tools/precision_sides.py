@@ -1,8 +1,24 @@
-import sys, os, torch
-sys.path.insert(0, '/root/repo'); sys.path.insert(0, '/root/repo/tools'); sys.path.insert(0, '/root/repo/transformer-stm_amd')
-import precision_emulate_fp8 as pe
-from oracle import vit_ref
-from vitmi.config import preset, ViTConfig
+"""Which side of each forward GEMM's bf16 rounding costs the logits? (a CPU emulation, round 6)
+
+Per GEMM class (qkv, proj, fc1, fc2, patch) the corrections of the bf16f8 knob run both (f: hi.lo_w
++ lo_x.hi_w in fixed-scale e4m3, as built), only the weight side (w: hi_x.lo_w), only the activation
+side (x: lo_x.hi_w) or none (b: plain bf16), on the fp32 oracle's forward (tools/
+precision_emulate_fp8.py's emulator).  Prints logits max-abs over the first 2 images (the bench's
+parity sample), over all images, and the RMS, against the fp32 oracle.
+usage: python tools/precision_sides.py vitb|smoke COMBO[,COMBO...] [images]
+       COMBO = five letters for qkv, proj, fc1, fc2, patch, e.g. wffff (profiles/r06_sides/)"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "tools"), os.path.join(ROOT, "transformer-stm_amd")):
+    sys.path.insert(0, _p)
+import precision_emulate_fp8 as pe  # noqa: E402
+from oracle import vit_ref  # noqa: E402
+from vitmi.config import ViTConfig, preset  # noqa: E402
+
 torch.set_num_threads(8)
 code = {"f": "f8fixed", "x": "f8x", "w": "f8w", "b": "bf16"}
 m = {k: pe.make_mm(v, 0) for k, v in code.items()}
