@@ -478,6 +478,7 @@ class _BlockFn(torch.autograd.Function):
         # and qkv's in one split-K launch over both outputs' tiles and one reduction, at qkv's
         # point; the MLP pair where du has just been written)
         wg = []
+        wr = _WgradRunner()
         # MLP branch
         # fc1's bias gradient = column sums of du, fused into the DGELU epilogue
         du = ops.linear_dgrad(g2_lp, w2, T, ops.EPI_DGELU, aux=u, bias_grad=gs(mlp.fc1.bias), aux_tiled=ctx.aux_tiled)
@@ -488,7 +489,7 @@ class _BlockFn(torch.autograd.Function):
         if gs.wants(mlp.fc1.weight):
             wg.append((du, h2, gs(mlp.fc1.weight)))
         if ops.WGRAD_GROUP in (0, 2, 3):
-            (ops.linear_wgrad_group if ops.WGRAD_GROUP == 2 else _each_wgrad)(wg)
+            wr.run(ops.linear_wgrad_group if ops.WGRAD_GROUP == 2 else _each_wgrad, wg)
             wg = []
         dh2 = ops.linear_dgrad(du, w1, T)
         # LN2 backward + residual; its column sums of dx1 are the out-proj bias grad
@@ -508,24 +509,67 @@ class _BlockFn(torch.autograd.Function):
         if gs.wants(a_.proj.weight):
             wg.append((dx1_lp, o, gs(a_.proj.weight)))
         if ops.WGRAD_GROUP == 0:
-            _each_wgrad(wg)
+            wr.run(_each_wgrad, wg)
             wg = []
         # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
         dqkv = ops.attention_bwd(qkv, o, do, lse, B, N, a_.num_heads, a_.scale, bias_grad=gs(a_.qkv.bias))
         if gs.wants(a_.qkv.weight):
             wg.append((dqkv, h1, gs(a_.qkv.weight)))
         if ops.WGRAD_GROUP == 0:
-            _each_wgrad(wg)
+            wr.run(_each_wgrad, wg)
             wg = []
         dh1 = ops.linear_dgrad(dqkv, wq, T)
-        ops.linear_wgrad_group(wg)
+        wr.run(ops.linear_wgrad_group, wg)
         # the bf16 copy of dx is for a consumer that takes it (the block below); the patch
         # embedding's backward reads dx in fp32
         want_lp = drop is None and ctx.handover
         dx, dx_lp = ops.layernorm_bwd(dh1, x2, m1, r1, n1.weight, gs(n1.weight), gs(n1.bias),
                                       dres=dx1, lp_dtype=lpT if want_lp else None, dxsum=gs(prev))
+        wr.join()
         out = _handover(dx.view(B, N, D), dx_lp)
         return (out, None, gs.grads([prev])[0], None, None, None) + gs.grads(ps)
+
+
+import os as _os
+# the block backward's weight gradients on a side stream (VITMI_WGRAD_STREAM=0: the current one).
+# They depend on nothing the dgrad chain computes after them, so their launches fill the tails
+# and ramps of the chain's: C3 backward 22.98-23.02 -> 22.77-22.83 ms (profiles/r06_side/)
+_WG_SIDE = _os.environ.get("VITMI_WGRAD_STREAM", "1") == "1"
+_SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+class _WgradRunner:
+    """Runs weight-gradient launches on a side stream ordered after the current stream's work so
+    far (or on the current stream); join() orders the current stream after all of them, so every
+    gradient the backward returns is final in stream order.  Their operands are the backward's
+    locals and saved tensors, alive until it returns (after join): no cross-stream reuse."""
+
+    def __init__(self):
+        self.main = torch.cuda.current_stream()
+        self.side = None
+        if _WG_SIDE:
+            dev = self.main.device.index
+            if dev not in _SIDE_STREAMS:
+                _SIDE_STREAMS[dev] = torch.cuda.Stream(device=self.main.device)
+            self.side = _SIDE_STREAMS[dev]
+
+    def run(self, fn, items):
+        if not items:
+            return
+        if self.side is None:
+            fn(items)
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            fn(items)
+
+    def join(self):
+        if self.side is not None:
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            self.main.wait_event(ev)
 
 
 def _each_wgrad(items):
