@@ -26,6 +26,7 @@ product is exact fp32 (f32-input MFMA).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -530,11 +531,10 @@ class _BlockFn(torch.autograd.Function):
         return (out, None, gs.grads([prev])[0], None, None, None) + gs.grads(ps)
 
 
-import os as _os
 # the block backward's weight gradients on a side stream (VITMI_WGRAD_STREAM=0: the current one).
 # They depend on nothing the dgrad chain computes after them, so their launches fill the tails
 # and ramps of the chain's: C3 backward 22.98-23.02 -> 22.77-22.83 ms (profiles/r06_side/)
-_WG_SIDE = _os.environ.get("VITMI_WGRAD_STREAM", "1") == "1"
+_WG_SIDE = os.environ.get("VITMI_WGRAD_STREAM", "1") == "1"
 _SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 
 
