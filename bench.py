@@ -332,6 +332,9 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-optimizer", action="store_true", help="diagnostic only: skip Adam")
+    ap.add_argument("--adam-overlap", type=int, choices=[0, 1], default=int(os.environ.get("VITMI_ADAM_OVERLAP", "0")),
+                    help="vitmi Adam steps each gradient bucket on a side stream as the backward (or, on the "
+                         "vitmi comm leg, its all-reduce) finishes it (optim.Adam.overlap_with)")
     ap.add_argument("--optimizer", choices=["vitmi", "torch"], default="vitmi",
                     help="vitmi: Keras Adam, one fused launch over the arena (+ bf16 shadow); torch: fused torch Adam")
     ap.add_argument("--attn-policy", type=int, default=0,
@@ -395,6 +398,8 @@ def main():
     dp.broadcast_parameters(model, group=group, comm=comm)
     if args.optimizer == "vitmi":
         opt = optim.Adam(model, learning_rate=1e-3)     # keras.optimizers.Adam(1e-3), models/CvT(Par).py:458
+        if args.adam_overlap:
+            opt.overlap_with(red)
     else:
         try:
             opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
@@ -500,7 +505,8 @@ def main():
                                + (f" + {args.grad_dtype} grad all-reduce ({comm_leg} RCCL, "
                                   f"{args.bucket_mb:g} MiB buckets)" if world > 1 else "")
                                + " + Adam step",
-                   "optimizer": "keras Adam (vitmi fused)" if args.optimizer == "vitmi" else "torch fused Adam",
+                   "optimizer": (("keras Adam (vitmi fused, per bucket beside the backward)" if args.adam_overlap
+                                  else "keras Adam (vitmi fused)") if args.optimizer == "vitmi" else "torch fused Adam"),
                    "model": model_name, "global_batch": B * world, "seq_len": cfg.seq_len,
                    "parallelism": f"dp{world}",
                    **({"knob_qkv": _knob_qkv(cfg)} if cfg.dtype in ("bf16x3", "bf16f8") else {})},

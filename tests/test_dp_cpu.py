@@ -453,3 +453,27 @@ def test_library_comm_world2_over_functional_stub(tmp_path):
             outs.append(p.communicate()[0])
     for r, (p, o) in enumerate(zip(procs, outs)):
         assert p.returncode == 0 and f"ok {r}" in o, o
+
+
+def test_reducer_notifies_finished_buckets_in_order_at_world1():
+    """GradReducer.listeners (optim.Adam.overlap_with): with nothing to exchange (world 1) every
+    bucket is announced once, in order, as soon as the finished prefix covers it; the rest at
+    the next step again from the first bucket."""
+    flat = torch.zeros(1000)
+    red = dp.GradReducer(flat, bucket_mb=256 * 4 / (1 << 20), cuts=[100, 600, 1000])
+    assert not red._active
+    seen = []
+    red.listeners.append(lambda s, e, st: seen.append((s, e, st)))
+    for _ in range(2):
+        seen.clear()
+        red.start()
+        red.mark_ready(50)
+        assert seen == []
+        red.mark_ready(100)
+        assert seen == [(0, 100, None)]
+        red.mark_ready(700)
+        assert [x[:2] for x in seen] == [(0, 100), (100, 356), (356, 600)]
+        red.mark_ready(1000)
+        red.finish()
+        assert [x[:2] for x in seen] == red.bounds
+        assert red.bounds[-1][1] == 1000

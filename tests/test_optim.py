@@ -142,3 +142,50 @@ def test_adam_arena_skips_frozen_parameters():
         keep[o:o + p.numel()] = False
     assert np.array_equal(arena.flat.cpu().numpy()[keep], ref[keep])
     assert torch.equal(arena.flat_lp, arena.flat.to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+def test_adam_overlap_matches_single_launch_bitwise():
+    """Adam.overlap_with (world 1): the buckets the backward finishes are stepped on a side
+    stream during it, the rest in step(); parameters, moments and the bf16 shadow equal the plain
+    single launch bit for bit over three steps.  A frozen parameter turns the overlap off for the
+    step (the plain path's skip rule)."""
+    from vitmi import dp
+    from vitmi.config import ViTConfig
+    from vitmi.modules import VisionTransformer, cross_entropy
+    cfg = ViTConfig(img_size=32, patch_size=8, in_chans=3, num_classes=3, embed_dim=128, depth=3, num_heads=2,
+                    dtype="bf16")
+    g = torch.Generator().manual_seed(7)
+    img = torch.rand(4, 3, 32, 32, generator=g).to(DEV)
+    tgt = torch.randint(0, 3, (4,), generator=g).to(DEV)
+    runs = []
+    for overlap in (False, True):
+        model = VisionTransformer(cfg).to(DEV)
+        model.reset_parameters(seed=8)
+        red = dp.attach(model, bucket_mb=0.25)
+        opt = optim.Adam(model, learning_rate=1e-3)
+        if overlap:
+            opt.overlap_with(red)
+        arena = model.arena()
+        side = []
+        for t in range(4):
+            if t == 3:
+                model.blocks[1].attn.proj.weight.requires_grad_(False)
+            opt.zero_grad()
+            red.start()
+            cross_entropy(model(img), tgt).backward()
+            red.finish()
+            if overlap:
+                side.append(opt._ov["done"])
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append((arena.flat.clone(), opt._m.clone(), opt._v.clone(), arena.flat_lp.clone()))
+        if overlap:
+            assert len(red.bounds) >= 4
+            # steps 0-2: the buckets went on the side stream as the backward finished them (all
+            # of them: the embedding's hooks close the backward); step 3 (a frozen weight): none
+            assert all(d == arena.numel for d in side[:3]), side
+            assert side[3] == 0, side
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    assert torch.equal(runs[1][3], runs[1][0].to(torch.bfloat16))

@@ -295,6 +295,10 @@ class GradReducer:
         # embedding's parameters) and by finish(): exchanged after the backward's compute
         self.tail_launched: List[int] = []
         self._burst: List[int] = []
+        # called as f(start, end, stream) when bucket [start, end) holds its final (reduced)
+        # gradient, ready on `stream` (None: the current stream): world 1, or the vitmi comm leg
+        # with its side stream (vitmi.optim.Adam.overlap_with)
+        self.listeners: List[Callable[[int, int, Optional["torch.cuda.Stream"]], None]] = []
 
     def _restore_reserve(self) -> None:
         if self._prev_reserve is not None:
@@ -360,15 +364,26 @@ class GradReducer:
         self.launch_log.append((self._ready, self._next))
         self._next += 1
 
+    def _notify(self, i: int, stream) -> None:
+        s, e = self.bounds[i]
+        for f in self.listeners:
+            f(s, e, stream)
+
     def mark_ready(self, end: int) -> None:
         """Gradients in flat[0:end] are final: launch every bucket inside that prefix."""
-        if not self._active:
-            return
         self._ready = max(self._ready, end)
+        if not self._active:
+            # nothing to exchange: the buckets are final as they are (listeners only)
+            while self.listeners and self._next < len(self.bounds) and self.bounds[self._next][1] <= self._ready:
+                self._notify(self._next, None)
+                self._next += 1
+            return
         burst = []
         while self._next < len(self.bounds) and self.bounds[self._next][1] <= self._ready:
             burst.append(self._next)
             self._launch()
+            if self.comm is not None and self._side is not None:
+                self._notify(self._next - 1, self._side)
         if burst:
             self._burst = burst
 

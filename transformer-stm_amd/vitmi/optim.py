@@ -54,6 +54,52 @@ class Adam:
             self.params = [p for p in target if p.requires_grad]
             self._m = [torch.zeros_like(p) for p in self.params]
             self._v = [torch.zeros_like(p) for p in self.params]
+        self._ov = None   # overlap_with state
+
+    def overlap_with(self, red) -> None:
+        """Step each gradient bucket of ``red`` (``vitmi.dp.attach``'s reducer) as soon as the
+        backward has finished it (world 1) or its all-reduce has (the vitmi comm leg): the update
+        of the blocks behind the backward runs on a side stream beside it, and ``step()`` only
+        launches the rest and joins.  The update is the same launch over the same elements, in
+        another order of ranges (elementwise, so bitwise the same result).  Needs one backward per
+        ``step()`` (no gradient accumulation across backwards) and every arena parameter
+        trainable; otherwise that step runs the plain single launch.  The learning rate is read
+        when the backward finishes its first bucket."""
+        if self._arena is None:
+            raise ValueError("vitmi Adam.overlap_with: needs a model with a parameter arena")
+        if red.flat.data_ptr() != self._arena.grad.data_ptr() or red.flat.numel() != self._arena.grad.numel():
+            raise ValueError("vitmi Adam.overlap_with: the reducer is not over this model's gradient arena")
+        self._ov = {"stream": torch.cuda.Stream(device=self._arena.flat.device), "done": 0, "alpha": None,
+                    "skip": False}
+        red.listeners.append(self._on_bucket)
+
+    def _launch(self, s0: int, e0: int, alpha: float) -> None:
+        arena, lp = self._arena, self._arena.flat_lp
+        check(lib().vitmi_adam_step(e0 - s0, ops._p(arena.flat[s0:]), ops._p(arena.grad[s0:]), ops._p(self._m[s0:]),
+                                    ops._p(self._v[s0:]), ops._p(lp[s0:]) if lp is not None else None, alpha,
+                                    self.beta_1, self.beta_2, self.epsilon, self.grad_scale, ops._s()),
+              "adam_step")
+
+    @torch.no_grad()
+    def _on_bucket(self, s0: int, e0: int, stream) -> None:
+        ov = self._ov
+        if ov["skip"]:
+            return
+        if ov["alpha"] is None:
+            # the first bucket of this backward
+            if not all(p.requires_grad for p in self._arena.params) or s0 != 0:
+                ov["skip"] = True
+                return
+            ov["alpha"] = keras_alpha(self.learning_rate, self.beta_1, self.beta_2, self.iterations + 1)
+        if s0 != ov["done"]:
+            raise RuntimeError("vitmi Adam: gradient buckets finished out of order")
+        side = ov["stream"]
+        ready = torch.cuda.Event()
+        ready.record(stream if stream is not None else torch.cuda.current_stream(self._arena.flat.device))
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            self._launch(s0, e0, ov["alpha"])
+        ov["done"] = e0
 
     # -- keras-style schedule hook
     @property
@@ -89,6 +135,14 @@ class Adam:
             # Parameters with no gradient (frozen, or zero_grad(set_to_none) and no backward) are
             # not stepped, as in torch / Keras: the launch covers the runs of the arena between them
             stepping = [p.requires_grad and p.grad is not None for p in arena.params]
+            ov, done = self._ov, 0
+            if ov is not None:
+                done, ov_alpha = ov["done"], ov["alpha"]
+                ov["done"], ov["alpha"], ov["skip"] = 0, None, False
+                if done:
+                    # the buckets the backward finished were stepped on the side stream
+                    torch.cuda.current_stream(arena.flat.device).wait_stream(ov["stream"])
+                    alpha = ov_alpha
             if not any(stepping):
                 return
             lp = arena.flat_lp
@@ -96,11 +150,9 @@ class Adam:
                 arena.refresh_lp()          # the skipped parameters' shadow must be current too
             arena.bind_grads(fill_missing=all(stepping))
             for s0, e0 in arena.runs(stepping):
-                n = e0 - s0
-                check(lib().vitmi_adam_step(n, ops._p(arena.flat[s0:]), ops._p(arena.grad[s0:]), ops._p(self._m[s0:]),
-                                            ops._p(self._v[s0:]), ops._p(lp[s0:]) if lp is not None else None, alpha,
-                                            self.beta_1, self.beta_2, self.epsilon, self.grad_scale, ops._s()),
-                      "adam_step")
+                s0 = max(s0, done)
+                if e0 > s0:
+                    self._launch(s0, e0, alpha)
             arena.mark_lp_fresh()
             return
         for p, m, v in zip(self.params, self._m, self._v):
