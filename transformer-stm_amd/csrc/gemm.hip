@@ -131,9 +131,28 @@ __device__ __forceinline__ int64_t aux_at(const GemmArgs& g, int64_t row, int64_
 // (tile-row, tile-col) of tile index tl: row-major over the tiles_n tile columns (a persistent
 // block walks consecutive tiles, so an XCD's concurrent tiles share A row panels in its L2;
 // grouped column-major orders measured 0.5-1 % slower end to end)
+// row panels per tile group (0: row-major tiles).  C3 step 7292-7314 -> 7335-7350 img/s over
+// three rounds (GM 5 and 7 as row-major; fc1 + GELU 308-313 -> 299-304 µs, DGELU 297-302 -> 288;
+// profiles/r06_gm*)
+#ifndef VITMI_TILE_GM
+#define VITMI_TILE_GM 6
+#endif
 __device__ __forceinline__ void tile_rc(const GemmArgs& g, int tl, int& tm, int& tn) {
-  tm = tl / g.tiles_n;
-  tn = tl - tm * g.tiles_n;
+  if constexpr (VITMI_TILE_GM > 1) {
+    // groups of GM row panels walked column by column: an XCD's 32 concurrent tiles span GM row
+    // panels x 32/GM column panels instead of ~3 x all of them, and the next ones reuse the
+    // same GM row panels from its L2
+    const int tiles_m = (int)((g.M + 255) >> 8);
+    const int per = VITMI_TILE_GM * g.tiles_n;
+    const int grp = tl / per, r = tl - grp * per;
+    const int m0 = grp * VITMI_TILE_GM;
+    const int gm = tiles_m - m0 < VITMI_TILE_GM ? tiles_m - m0 : VITMI_TILE_GM;
+    tn = r / gm;
+    tm = m0 + (r - tn * gm);
+  } else {
+    tm = tl / g.tiles_n;
+    tn = tl - tm * g.tiles_n;
+  }
 }
 
 // internal epilogues: split-K partial slab, and GELU / residual with a fused dropout
